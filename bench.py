@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""MIDASPOM posterior-grid benchmark (BASELINE.json metric).
+
+A "step" = one pass of the hot path over one (e, c) grid slab per rank: the
+per-c coefficient kernels plus the forward-recursion kernel over every grid
+point, and -- with N > 1 ranks -- the single RCCL gather of the log-likelihood
+slabs to rank 0.  Units = grid points x year transitions = s^2 (tmax - 1) per
+rank; value = units over all ranks / max-over-ranks wall time (weak scaling:
+each rank owns an s x s slab of an (N s) x s grid).
+
+Workload: 64 patches x 50 years (synthetic,
+Appendix C generator, md5-checked), 512 x 512 grid, -m 400 -d 100, FP64.
+Launch:  python bench.py [--gpus N --steps K --warmup W]
+         torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import midaspom_amd as mdp  # noqa: E402
+from midaspom_amd import synth  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, AMD datasheet
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    2: dict(gen=synth.CONFIG2, s=512, name="config2: 64 patches x 50 years, 512x512 (e,c) grid"),
+    3: dict(gen=synth.CONFIG3, s=1024, name="config3: 256 patches x 200 years, 1024x1024 (e,c) grid"),
+}
+
+
+def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, budget_s=12.0):
+    """Oracle (CPU restatement of the reference dense CBLAS path, naive dgemm)
+    on a bounded, evenly strided sample of the same grid points; also the
+    parity of the GPU run at those points."""
+    import oracle
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                         os.cpu_count() or 1))
+    om = oracle.OracleModel.load(input_path, 400.0, 0.5, 100.0)
+    ne, nc = lik_gpu.shape
+    # calibrate single-point cost, then size the sample for ~budget_s of wall
+    t0 = time.perf_counter()
+    om.loglik_points(g_e[:4], g_c[:4], threads=1)
+    per_pt = (time.perf_counter() - t0) / 4
+    npts = int(min(ne * nc, max(threads * 8, budget_s * threads / per_pt)))
+    stride = max(1, int(np.floor(np.sqrt(ne * nc / npts))))
+    ie = np.arange(0, ne, stride)
+    ic = np.arange(0, nc, stride)
+    ee, cc = np.meshgrid(ie, ic, indexing="ij")
+    ee, cc = ee.ravel(), cc.ravel()
+    t0 = time.perf_counter()
+    ref = om.loglik_points(g_e[ee], g_c[cc], threads=threads)
+    wall = time.perf_counter() - t0
+    got = lik_gpu[ee, cc]
+    with np.errstate(invalid="ignore", over="ignore"):
+        pg, pr = np.exp(got - ltot_gpu), np.exp(ref - ltot_gpu)
+    fin = np.isfinite(pr)
+    dabs = float(np.abs(pg[fin] - pr[fin]).max()) if fin.any() else 0.0
+    big = fin & (pr > 1e-14)
+    drel = float((np.abs(pg[big] - pr[big]) / pr[big]).max()) if big.any() else 0.0
+    dlog = float(np.abs(got[fin] - ref[fin]).max()) if fin.any() else 0.0
+    return {
+        "value": ee.size * (tmax - 1) / wall,
+        "unit": "grid-point-timestep evals/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{ee.size} grid points (every {stride}th e and c of the {ne}x{nc} grid), "
+                  f"oracle/spom_oracle.c dense formulation with naive dgemm, {threads} threads, "
+                  f"{wall:.1f} s",
+    }, {"max_abs_dposterior": dabs, "max_rel_dposterior": drel, "max_abs_dloglik": dlog,
+        "points_checked": int(ee.size)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    cfg = CONFIGS[args.config]
+    s = cfg["s"]
+    tmpdir = Path(tempfile.mkdtemp(prefix="mdp_bench_"))
+    inp = tmpdir / "occupancies.txt"
+    synth.write(inp, **cfg["gen"])
+    model = mdp.Model.load(inp, m=400.0, p=0.5, d=100.0)
+    tmax = model.tmax
+
+    # weak scaling: rank r owns e-rows [r*s, (r+1)*s) of an (world*s) x s grid
+    g_all, _ = mdp.grid(world * s, 0.0, 1.0)
+    g_e = g_all[rank * s:(rank + 1) * s].copy()
+    g_c, win = mdp.grid(s, 0.0, 1.0)
+
+    eng = mdp.Engine(model, devices=[dev.index])
+    eng.set_grid(g_e, g_c)
+    out = torch.empty((s, s), dtype=torch.float64, device=dev)
+    gathered = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        eng.run(out.data_ptr(), s, stream)
+        if world > 1:
+            dist.gather(out, gathered, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    eng.set_profiling(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    kms = eng.kernel_ms()
+    eng.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    units = world * s * s * (tmax - 1) * args.steps
+    work = eng.work(s, s)
+    info = eng.info()
+    fwd_ms = kms.get("k_forward", float("nan"))
+    achieved_tf = work["flop_impl"] / (fwd_ms * 1e-3) / 1e12
+    result = {
+        "metric": "grid-point x timestep likelihood evals/sec",
+        "value": units / dt,
+        "unit": "grid-point-timestep evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY.md Appendix C generator, md5-checked input)",
+        "config": {"workload": cfg["name"], "patches": model.n, "years": tmax, "grid": [world * s, s],
+                   "per_rank_grid": [s, s], "nvar": model.nvar, "nstates": model.nstates,
+                   "nextid": model.nextid, "parallelism": f"e-row slabs x{world}" + (", RCCL gather" if world > 1 else "")},
+        "kernel_ms": kms,
+        "roofline": {
+            "kernel": "k_forward",
+            "bound": "mfma",
+            "compute_unit": "FP64 VALU (MI355X FP64 vector peak = FP64 matrix peak)",
+            "achieved": achieved_tf,
+            "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tf / FP64_PEAK_TFLOPS,
+            "traffic": None,
+            "flop_per_launch": work["flop_impl"],
+            "flop_per_launch_survey_dense": work["flop_survey"],
+            "survey_dense_equiv_tflops": work["flop_survey"] / (fwd_ms * 1e-3) / 1e12,
+            "uses_per_point": info["nuses"],
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        lik = torch.empty((s, s), dtype=torch.float64, device=dev)
+        eng.run(lik.data_ptr(), s, stream)
+        torch.cuda.synchronize(dev)
+        lik_h = lik.cpu().numpy()
+        ltot = mdp.log_total(lik_h, win)
+        cpu, parity = cpu_baseline(inp, g_e, g_c, lik_h, ltot, tmax)
+        result["cpu_baseline"] = cpu
+        result["parity"] = parity
+    else:
+        result["cpu_baseline"] = None
+    eng.close()
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+/*
+ * include/midaspom.h -- C ABI of the MI355X-native MIDASPOM posterior-grid engine.
+ *
+ * The reference (nalcala/MIDASPOM) is one monolithic main() per program with
+ * no library API; these entry points are the seams a C caller of the
+ * reference's pipeline would bind.  Each declaration cites
+ * the region of /root/reference/sources/main_MIDASPOM.c it replaces.
+ *
+ * Conventions
+ *  - plain pointers and sizes only; no torch / HIP types in signatures
+ *    (streams are passed as void*, i.e. a hipStream_t or NULL);
+ *  - every int-returning function returns MDP_OK (0) or a negative MDP_E*
+ *    code; the reason is in mdp_last_error() (thread-local).  Nothing aborts
+ *    or exits across the ABI;
+ *  - an engine is not re-entrant; one host thread drives all its devices;
+ *  - results are deterministic (no atomics in any reduction).
+ */
+#ifndef MIDASPOM_H
+#define MIDASPOM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDP_OK 0
+#define MDP_EINVAL (-1)       /* bad argument / malformed problem          */
+#define MDP_EIO (-2)          /* cannot open / write a file                */
+#define MDP_ENOMEM (-3)       /* host or device allocation failed          */
+#define MDP_EHIP (-4)         /* HIP runtime error                         */
+#define MDP_ENODEV (-5)       /* no usable GPU                             */
+#define MDP_EUNSUPPORTED (-6) /* problem outside the engine's limits       */
+
+#define MDP_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ */
+/* Host model: parse + state enumeration (the reference's L2 layer)    */
+/* ------------------------------------------------------------------ */
+
+/* Parsed and enumerated observation model (opaque, host memory). */
+typedef struct mdp_model mdp_model;
+
+/* Read an occupancy file and enumerate its states.
+ * Replaces main_MIDASPOM.c:137-287 (parse :141-167 with quirk Q6, variable
+ * columns :172-175, dispersal M :177-188, state bits :198-211, per-year
+ * observed states + float32 prior :214-255, short-id dedup :256-287).
+ * m = mean dispersal distance (-m), p = prior occupancy of missing year-0
+ * patches (-p, used as float32 like :66), d = segment length (-d). */
+int mdp_model_load(const char *path, double m, float p, double d, mdp_model **out);
+
+/* Same, from an in-memory observation matrix obs[tmax][n] (values -1/0/1). */
+int mdp_model_from_obs(const int32_t *obs, uint32_t n, uint32_t tmax, double m, float p,
+                       double d, mdp_model **out);
+
+void mdp_model_free(mdp_model *model);
+
+/* Read-only view of a model; pointers stay owned by the model. */
+typedef struct mdp_problem {
+    uint32_t n;                 /* patches (columns)                                 */
+    uint32_t tmax;              /* years (rows)                                      */
+    uint32_t nvar;              /* columns ever non-zero; nstates = 2^nvar           */
+    uint32_t nextid;            /* distinct observed states ("short ids")            */
+    const int32_t *obs;         /* [tmax][n] parsed observations                     */
+    const uint32_t *var_cols;   /* [nvar] ascending column indices                   */
+    const double *M;            /* [n][n] dispersal kernel, row-major, diag 0        */
+    const uint32_t *short_state;/* [nextid] state id (first var column = MSB)        */
+    const uint32_t *year_off;   /* [tmax+1] offsets into year_ids                    */
+    const uint32_t *year_ids;   /* [year_off[tmax]] short ids of each year's states  */
+    const float *prior;         /* [year_off[1]] float32 prior of year-0 states      */
+} mdp_problem;
+
+int mdp_model_problem(const mdp_model *model, mdp_problem *view);
+
+/* ------------------------------------------------------------------ */
+/* Grid, normalisation and posterior writer (the reference's L3/L5)    */
+/* ------------------------------------------------------------------ */
+
+/* g[i] = i*win + lo for i < s-1, g[s-1] = hi; returns win = (hi-lo)/(s-1).
+ * Replaces main_MIDASPOM.c:120 and :312-319. */
+double mdp_grid(uint32_t s, double lo, double hi, double *g);
+
+/* Ltot = 2 log(win) + log(sum_k sum_l w_k w_l exp(loglik[k][l])), trapezoid
+ * weights 1/2 at the grid ends.  Replaces main_MIDASPOM.c:413-425. */
+double mdp_log_total(const double *loglik, uint32_t s, double win);
+
+/* Posterior text file: "%.20lf\t" of exp(loglik-ltot) per cell, "\n" per row
+ * (rows = e, columns = c).  Replaces main_MIDASPOM.c:427-436.  raw != 0
+ * writes loglik itself (the MPI build's Ltot == 0 branch,
+ * main_MIDASPOM_MPI.c:527). */
+int mdp_write_posterior(const char *path, const double *loglik, uint32_t s, double ltot,
+                        int raw);
+
+/* ------------------------------------------------------------------ */
+/* GPU likelihood engine (the reference's hot loop, L3 + L4 + L6)      */
+/* ------------------------------------------------------------------ */
+
+typedef struct mdp_engine mdp_engine;
+
+/* Build the engine on n_devices GPUs (devices == NULL -> 0..n_devices-1;
+ * n_devices == 0 -> the calling thread's current HIP device).  Copies the
+ * problem tables to device memory it owns and precomputes the grid-invariant
+ * colonisation sums.  Replaces the setup half of main_MIDASPOM.c:341-360
+ * (per-point recomputation of S = piall*M moves here, once). */
+int mdp_engine_create(const mdp_problem *problem, const int *devices, int n_devices,
+                      mdp_engine **out);
+
+void mdp_engine_destroy(mdp_engine *engine);
+
+/* out[ie*nc + ic] = log L(e[ie], c[ic]) (-inf where L == 0), host memory.
+ * Rows are split over the engine's devices in contiguous slabs (remainder to
+ * device 0, as main_MIDASPOM_MPI.c:361-368).  Replaces main_MIDASPOM.c:341-395
+ * (and the MPI gather :482-506). */
+int mdp_loglik_grid(mdp_engine *engine, const double *e, uint32_t ne, const double *c,
+                    uint32_t nc, double *out);
+
+/* Device-resident variant for single-device engines (one process per GPU):
+ * upload the grid once, then compute into caller-owned device memory
+ * d_out[ie*ld_out + ic] on `stream` (hipStream_t, NULL = engine stream).
+ * mdp_engine_run is asynchronous w.r.t. the host. */
+int mdp_engine_set_grid(mdp_engine *engine, const double *e, uint32_t ne, const double *c,
+                        uint32_t nc);
+int mdp_engine_run(mdp_engine *engine, double *d_out, uint32_t ld_out, void *stream);
+
+/* Kernel timing: when enabled, each run records HIP events around its
+ * kernels on the launch stream.  mdp_engine_kernel_ms fills up to max_k
+ * durations (ms) of the last run, in launch order, and returns the count;
+ * names via mdp_engine_kernel_name. */
+int mdp_engine_set_profiling(mdp_engine *engine, int enable);
+int mdp_engine_kernel_ms(mdp_engine *engine, double *ms, int max_k);
+const char *mdp_engine_kernel_name(int k);
+
+/* Work accounting of one run on a grid of ne x nc points (host arithmetic on
+ * the enumerated problem): flops of the forward kernel in
+ * the implemented factorised form, and the SURVEY.md §8(d) dense-form F_alg. */
+int mdp_engine_work(const mdp_engine *engine, uint64_t ne, uint64_t nc, double *flop_impl,
+                    double *flop_survey, double *bytes_min);
+
+/* Engine facts: number of devices, distinct transition pairs, forward
+ * "uses" (one per consecutive-year state pair), coefficients per c value,
+ * max states per year, selected kernel variant. */
+typedef struct mdp_engine_info {
+    int n_devices;
+    uint32_t npairs;
+    uint32_t nuses;
+    uint32_t ncoef;
+    uint32_t npmax;
+    uint32_t variant;
+} mdp_engine_info;
+int mdp_engine_get_info(const mdp_engine *engine, mdp_engine_info *info);
+
+/* Thread-local description of the last error. */
+const char *mdp_last_error(void);
+
+int mdp_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIDASPOM_H */

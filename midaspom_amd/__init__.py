@@ -1,0 +1,234 @@
+"""midaspom_amd -- MI355X-native MIDASPOM posterior-grid likelihood engine.
+
+Host-side mirror of the reference pipeline (sources/main_MIDASPOM.c) over the
+C ABI of include/midaspom.h:
+
+    model = Model.load("occupancies.txt", m=400, p=0.5, d=100)   # :137-287
+    g, win = grid(101, 0.0, 1.0)                                 # :312-319
+    with Engine(model) as eng:
+        lik = eng.loglik_grid(g, g)                              # :341-395 on the GPU
+    ltot = log_total(lik, win)                                   # :413-425
+    write_posterior("posterior.txt", lik, ltot)                  # :427-436
+
+Every compute call goes through libmidaspom.so (HIP, gfx950); there is no
+CPU fallback in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import MidaspomError, check, lib
+
+__all__ = [
+    "Model", "Engine", "grid", "log_total", "write_posterior", "posterior",
+    "run_file", "MidaspomError",
+]
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class Model:
+    """Parsed + enumerated occupancy model (``mdp_model``)."""
+
+    def __init__(self, handle: ctypes.c_void_p):
+        self._h = handle
+        self._view = _lib.Problem()
+        check(lib().mdp_model_problem(self._h, ctypes.byref(self._view)))
+
+    @classmethod
+    def load(cls, path, m: float = 400.0, p: float = 0.5, d: float = 100.0) -> "Model":
+        h = ctypes.c_void_p()
+        check(lib().mdp_model_load(os.fsencode(str(path)), float(m), float(p), float(d),
+                                   ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_obs(cls, obs, m: float = 400.0, p: float = 0.5, d: float = 100.0) -> "Model":
+        a = np.ascontiguousarray(obs, dtype=np.int32)
+        if a.ndim != 2:
+            raise ValueError("obs must be a 2-D [years][patches] matrix")
+        h = ctypes.c_void_p()
+        check(lib().mdp_model_from_obs(a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                       a.shape[1], a.shape[0], float(m), float(p), float(d),
+                                       ctypes.byref(h)))
+        return cls(h)
+
+    def close(self):
+        if self._h:
+            lib().mdp_model_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- read-only views -------------------------------------------------
+    @property
+    def problem(self) -> _lib.Problem:
+        return self._view
+
+    n = property(lambda s: s._view.n)
+    tmax = property(lambda s: s._view.tmax)
+    nvar = property(lambda s: s._view.nvar)
+    nextid = property(lambda s: s._view.nextid)
+    nstates = property(lambda s: 1 << s._view.nvar)
+
+    @property
+    def obs(self) -> np.ndarray:
+        v = self._view
+        return np.ctypeslib.as_array(v.obs, shape=(v.tmax, v.n)).copy()
+
+    @property
+    def M(self) -> np.ndarray:
+        v = self._view
+        return np.ctypeslib.as_array(v.M, shape=(v.n, v.n)).copy()
+
+    @property
+    def var_cols(self) -> np.ndarray:
+        v = self._view
+        if v.nvar == 0:
+            return np.zeros(0, dtype=np.uint32)
+        return np.ctypeslib.as_array(v.var_cols, shape=(v.nvar,)).copy()
+
+    @property
+    def year_off(self) -> np.ndarray:
+        v = self._view
+        return np.ctypeslib.as_array(v.year_off, shape=(v.tmax + 1,)).copy()
+
+    @property
+    def npstates(self) -> np.ndarray:
+        return np.diff(self.year_off)
+
+    @property
+    def year_ids(self) -> list:
+        off = self.year_off
+        flat = np.ctypeslib.as_array(self._view.year_ids, shape=(int(off[-1]),)).copy()
+        return [flat[off[t]:off[t + 1]] for t in range(self.tmax)]
+
+    @property
+    def short_state(self) -> np.ndarray:
+        v = self._view
+        return np.ctypeslib.as_array(v.short_state, shape=(v.nextid,)).copy()
+
+    @property
+    def prior(self) -> np.ndarray:
+        off = self.year_off
+        return np.ctypeslib.as_array(self._view.prior, shape=(int(off[1]),)).copy()
+
+
+class Engine:
+    """GPU likelihood engine (``mdp_engine``) over one or more devices."""
+
+    def __init__(self, model: Model, devices=None, n_devices: int | None = None):
+        self.model = model  # keep the host tables alive
+        h = ctypes.c_void_p()
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = lib().mdp_engine_create(ctypes.byref(model.problem), arr, len(devices), ctypes.byref(h))
+        else:
+            rc = lib().mdp_engine_create(ctypes.byref(model.problem), None, int(n_devices or 0),
+                                         ctypes.byref(h))
+        check(rc)
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mdp_engine_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def loglik_grid(self, e, c) -> np.ndarray:
+        """log L on the e x c grid (host arrays in, host [ne][nc] out)."""
+        e = np.ascontiguousarray(e, dtype=np.float64)
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        out = np.empty((e.size, c.size), dtype=np.float64)
+        check(lib().mdp_loglik_grid(self._h, _dptr(e), e.size, _dptr(c), c.size, _dptr(out)))
+        return out
+
+    def set_grid(self, e, c) -> None:
+        e = np.ascontiguousarray(e, dtype=np.float64)
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        check(lib().mdp_engine_set_grid(self._h, _dptr(e), e.size, _dptr(c), c.size))
+        self.ne, self.nc = e.size, c.size
+
+    def run(self, d_out: int, ld_out: int, stream: int | None = None) -> None:
+        """Compute into device memory at address ``d_out`` (e.g. a torch
+        tensor's data_ptr()) on hipStream ``stream`` (None = engine stream)."""
+        check(lib().mdp_engine_run(self._h, ctypes.c_void_p(d_out), ld_out,
+                                   ctypes.c_void_p(stream) if stream else None))
+
+    def set_profiling(self, on: bool = True) -> None:
+        check(lib().mdp_engine_set_profiling(self._h, int(bool(on))))
+
+    def kernel_ms(self) -> dict:
+        buf = (ctypes.c_double * 8)()
+        k = check(lib().mdp_engine_kernel_ms(self._h, buf, 8))
+        return {lib().mdp_engine_kernel_name(i).decode(): buf[i] for i in range(k)}
+
+    def info(self) -> dict:
+        inf = _lib.EngineInfo()
+        check(lib().mdp_engine_get_info(self._h, ctypes.byref(inf)))
+        return {f: getattr(inf, f) for f, _ in inf._fields_}
+
+    def work(self, ne: int, nc: int) -> dict:
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(lib().mdp_engine_work(self._h, ne, nc, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return {"flop_impl": a.value, "flop_survey": b.value, "bytes_min": c.value}
+
+
+def grid(s: int, lo: float = 0.0, hi: float = 1.0):
+    """(g, win): the reference's parameter grid (:120, :312-319)."""
+    g = np.empty(int(s), dtype=np.float64)
+    win = lib().mdp_grid(int(s), float(lo), float(hi), _dptr(g))
+    return g, win
+
+
+def log_total(lik: np.ndarray, win: float) -> float:
+    """Trapezoid log normaliser (:413-425)."""
+    a = np.ascontiguousarray(lik, dtype=np.float64)
+    if a.ndim != 2 or a.shape[0] != a.shape[1]:
+        raise ValueError("log_total needs a square s x s grid")
+    return float(lib().mdp_log_total(_dptr(a), a.shape[0], float(win)))
+
+
+def write_posterior(path, lik: np.ndarray, ltot: float, raw: bool = False) -> None:
+    """Posterior text file, reference bit layout (:427-436)."""
+    a = np.ascontiguousarray(lik, dtype=np.float64)
+    check(lib().mdp_write_posterior(os.fsencode(str(path)), _dptr(a), a.shape[0], float(ltot), int(raw)))
+
+
+def posterior(lik: np.ndarray, ltot: float) -> np.ndarray:
+    with np.errstate(invalid="ignore", over="ignore"):
+        return np.exp(lik - ltot)
+
+
+def run_file(input_path, output_path=None, m=400.0, p=0.5, d=100.0, s=101, lo=0.0, hi=1.0,
+             devices=None):
+    """Whole MIDASPOM.out pipeline on the GPU; returns (loglik, ltot)."""
+    model = Model.load(input_path, m=m, p=p, d=d)
+    g, win = grid(s, lo, hi)
+    with Engine(model, devices=devices) as eng:
+        lik = eng.loglik_grid(g, g)
+    ltot = log_total(lik, win)
+    if output_path is not None:
+        write_posterior(output_path, lik, ltot)
+    return lik, ltot

@@ -1,0 +1,125 @@
+"""ctypes binding of the in-tree C ABI (include/midaspom.h).
+
+The shared library is midaspom_amd/_build/libmidaspom.so, built by
+``__graft_entry__.build()`` (``make -C midaspom_amd/csrc``).  There is no
+fallback: importing a compute entry point without the library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+BUILD_DIR = PKG_DIR / "_build"
+LIB_PATH = BUILD_DIR / "libmidaspom.so"
+CLI_PATH = BUILD_DIR / "midaspom"
+
+MDP_OK = 0
+ERRORS = {
+    -1: "MDP_EINVAL",
+    -2: "MDP_EIO",
+    -3: "MDP_ENOMEM",
+    -4: "MDP_EHIP",
+    -5: "MDP_ENODEV",
+    -6: "MDP_EUNSUPPORTED",
+}
+
+
+class MidaspomError(RuntimeError):
+    """A negative return code from the C ABI, with mdp_last_error()."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+c_u32 = ctypes.c_uint32
+c_dbl_p = ctypes.POINTER(ctypes.c_double)
+c_u32_p = ctypes.POINTER(ctypes.c_uint32)
+c_i32_p = ctypes.POINTER(ctypes.c_int32)
+
+
+class Problem(ctypes.Structure):
+    """Mirror of ``mdp_problem``."""
+
+    _fields_ = [
+        ("n", c_u32),
+        ("tmax", c_u32),
+        ("nvar", c_u32),
+        ("nextid", c_u32),
+        ("obs", c_i32_p),
+        ("var_cols", c_u32_p),
+        ("M", c_dbl_p),
+        ("short_state", c_u32_p),
+        ("year_off", c_u32_p),
+        ("year_ids", c_u32_p),
+        ("prior", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
+class EngineInfo(ctypes.Structure):
+    """Mirror of ``mdp_engine_info``."""
+
+    _fields_ = [
+        ("n_devices", ctypes.c_int),
+        ("npairs", c_u32),
+        ("nuses", c_u32),
+        ("ncoef", c_u32),
+        ("npmax", c_u32),
+        ("variant", c_u32),
+    ]
+
+
+# (name, restype, argtypes) for every function declared in include/midaspom.h
+SIGNATURES = [
+    ("mdp_model_load", ctypes.c_int,
+     [ctypes.c_char_p, ctypes.c_double, ctypes.c_float, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
+    ("mdp_model_from_obs", ctypes.c_int,
+     [c_i32_p, c_u32, c_u32, ctypes.c_double, ctypes.c_float, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
+    ("mdp_model_free", None, [ctypes.c_void_p]),
+    ("mdp_model_problem", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Problem)]),
+    ("mdp_grid", ctypes.c_double, [c_u32, ctypes.c_double, ctypes.c_double, c_dbl_p]),
+    ("mdp_log_total", ctypes.c_double, [c_dbl_p, c_u32, ctypes.c_double]),
+    ("mdp_write_posterior", ctypes.c_int, [ctypes.c_char_p, c_dbl_p, c_u32, ctypes.c_double, ctypes.c_int]),
+    ("mdp_engine_create", ctypes.c_int,
+     [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("mdp_engine_destroy", None, [ctypes.c_void_p]),
+    ("mdp_loglik_grid", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_u32, c_dbl_p, c_u32, c_dbl_p]),
+    ("mdp_engine_set_grid", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_u32, c_dbl_p, c_u32]),
+    ("mdp_engine_run", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u32, ctypes.c_void_p]),
+    ("mdp_engine_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("mdp_engine_kernel_ms", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, ctypes.c_int]),
+    ("mdp_engine_kernel_name", ctypes.c_char_p, [ctypes.c_int]),
+    ("mdp_engine_work", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_dbl_p, c_dbl_p, c_dbl_p]),
+    ("mdp_engine_get_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(EngineInfo)]),
+    ("mdp_last_error", ctypes.c_char_p, []),
+    ("mdp_abi_version", ctypes.c_int, []),
+]
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmidaspom.so (once).  Raises if the HIP build is missing."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: the HIP engine is not built "
+                "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+        handle = ctypes.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | ctypes.RTLD_GLOBAL)
+        for name, res, args in SIGNATURES:
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc: int) -> int:
+    """Raise MidaspomError on a negative ABI return code."""
+    if rc < 0:
+        raise MidaspomError(rc, lib().mdp_last_error().decode(errors="replace"))
+    return rc

@@ -1,0 +1,137 @@
+/*
+ * midaspom_amd/csrc/midaspom_cli.c -- `midaspom`, a drop-in for the
+ * reference's bin_linux/MIDASPOM.out (and, with -g N, for
+ * `mpirun -np N MIDASPOM_MPI.out`).
+ *
+ * Same getopt string, defaults and stdout lines as
+ * /root/reference/sources/main_MIDASPOM.c:61-439; the posterior file has the
+ * same bit layout (%.20lf\t per cell, \n per row).  The grid loop :341-395
+ * runs on the GPU through the C ABI in include/midaspom.h.
+ *
+ * Extensions: -g <N> (or MIDASPOM_GPUS=N) spreads the e rows over N GPUs of
+ * this node (contiguous slabs as main_MIDASPOM_MPI.c:361-368).
+ */
+#include <ctype.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "midaspom.h"
+
+int main(int argc, char **argv)
+{
+    printf("------ MIDASPOM, beta version ------\n-> N. Alcala, E. M. Cole, and N. A. Rosenberg <-\n");
+
+    float prior_occ = 0.5f;            /* -p, float32 as :66 */
+    const char *fin = "input.txt";     /* -i */
+    const char *fout = "posterior.txt";/* -o */
+    double seg = 100;                  /* -d (code default, not the manual's 200) */
+    unsigned nstep = 101;              /* -s */
+    double mdisp = 400;                /* -m */
+    double lo = 0.0, hi = 1.0;         /* -l, -u */
+    int ngpu = 0;
+    const char *env = getenv("MIDASPOM_GPUS");
+    if (env) ngpu = atoi(env);
+
+    int c;
+    opterr = 0;
+    while ((c = getopt(argc, argv, "m:p:d:i:o:s:l:u:g:")) != -1) {
+        switch (c) {
+        case 'm': mdisp = atof(optarg); break;
+        case 'p': prior_occ = (float)atof(optarg); break;
+        case 'd': seg = atof(optarg); break;
+        case 'i': fin = optarg; break;
+        case 'o': fout = optarg; break;
+        case 's': nstep = (unsigned)atoi(optarg); break;
+        case 'l': lo = atof(optarg); break;
+        case 'u': hi = atof(optarg); break;
+        case 'g': ngpu = atoi(optarg); break;
+        case '?':
+            /* message set of main_MIDASPOM.c:106-115 */
+            if (optopt == 'c')
+                fprintf(stderr, "Option -%c requires an argument.\n", optopt);
+            else if (isprint(optopt))
+                fprintf(stderr, "Unknown option `-%c'.\n", optopt);
+            else
+                fprintf(stderr, "Unknown option character `\\x%x'.\n", optopt);
+            return 1;
+        default:
+            abort();
+        }
+    }
+    if (nstep < 2) {
+        fprintf(stderr, "midaspom: -s must be at least 2\n");
+        return 1;
+    }
+
+    const double win = mdp_grid(nstep, lo, hi, NULL);
+    printf("Parameters for numerical approximation of the posterior density:\n\tWindow size=%lf, number of steps=%d\n",
+           win, nstep);
+
+    printf("Reading observations from file %s... ", fin);
+    mdp_model *model = NULL;
+    int rc = mdp_model_load(fin, mdisp, prior_occ, seg, &model);
+    if (rc) {
+        fprintf(stderr, "\nmidaspom: %s\n", mdp_last_error());
+        return 2;
+    }
+    mdp_problem pb;
+    mdp_model_problem(model, &pb);
+    printf("done\n");
+    printf("Number of habitat patches: %d\nNumber of sampled years: %d\n", pb.n, pb.tmax);
+
+    printf("Dispersal matrix:\n");
+    for (unsigned i = 0; i < pb.n; i++) {
+        for (unsigned j = 0; j < pb.n; j++) printf("%.3f ", pb.M[(size_t)i * pb.n + j]);
+        printf("\n");
+    }
+    printf("Input occupancy data:\n");
+    for (unsigned t = 0; t < pb.tmax; t++) {
+        printf("Year %d: ", t);
+        for (unsigned j = 0; j < pb.n; j++) printf("%d ", pb.obs[(size_t)t * pb.n + j]);
+        printf("\n");
+    }
+    printf("Number of possible states per year:\n");
+    for (unsigned t = 0; t < pb.tmax; t++) printf("Year %d: %d\n", t, pb.year_off[t + 1] - pb.year_off[t]);
+    printf("Number of states to compute: %d\n", 1u << pb.nvar);
+
+    double *grid = (double *)malloc(sizeof(double) * nstep);
+    double *lik = (double *)malloc(sizeof(double) * (size_t)nstep * nstep);
+    if (!grid || !lik) {
+        fprintf(stderr, "midaspom: out of host memory\n");
+        return 2;
+    }
+    mdp_grid(nstep, lo, hi, grid);
+    setbuf(stdout, NULL);
+
+    time_t start, end;
+    time(&start);
+    printf("Starting parallel likelihood computation\n");
+    mdp_engine *eng = NULL;
+    rc = mdp_engine_create(&pb, NULL, ngpu > 0 ? ngpu : 0, &eng);
+    if (!rc) rc = mdp_loglik_grid(eng, grid, nstep, grid, nstep, lik);
+    if (rc) {
+        fprintf(stderr, "midaspom: %s\n", mdp_last_error());
+        mdp_engine_destroy(eng);
+        return 3;
+    }
+    mdp_engine_destroy(eng);
+    for (unsigned ie = 0; ie < nstep; ie++) printf("%.2f%% done\n", ((float)ie + 1) * 100.0 / nstep);
+    printf("end likelihood computation\n");
+
+    const double ltot = mdp_log_total(lik, nstep, win);
+    printf("Total log-likelihood=%.5lf\n", ltot);
+    printf("Writing output in file %s... ", fout);
+    rc = mdp_write_posterior(fout, lik, nstep, ltot, 0);
+    if (rc) {
+        fprintf(stderr, "midaspom: %s\n", mdp_last_error());
+        return 2;
+    }
+    time(&end);
+    printf("done\n Total running time: %.2lf min\n", difftime(end, start) / 60.0);
+    free(grid);
+    free(lik);
+    mdp_model_free(model);
+    return 0;
+}

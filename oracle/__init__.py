@@ -1,0 +1,188 @@
+"""oracle -- TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of the CPU restatement of the reference likelihood
+(oracle/spom_oracle.c).  Importable only by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg, as the checker / CPU baseline.  The product
+package (midaspom_amd) never imports this module.
+
+Pinning: tests/test_oracle_golden.py checks this oracle against the manual's
+worked example (Manual_linux.pdf p.3) and the reference outputs recorded in
+SURVEY.md §8(c)/Appendix C (posterior md5s, Total log-likelihood values).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+BUILD = ORACLE_DIR / "_build"
+LIB = BUILD / "liboracle.so"
+CLI = BUILD / "orc_main"
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        h = ctypes.CDLL(str(LIB))
+        vp = ctypes.c_void_p
+        h.orc_model_load.argtypes = [ctypes.c_char_p, ctypes.c_double, ctypes.c_float, ctypes.c_double,
+                                     ctypes.POINTER(vp)]
+        h.orc_model_build.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_uint, ctypes.c_uint,
+                                      ctypes.c_double, ctypes.c_float, ctypes.c_double, ctypes.POINTER(vp)]
+        h.orc_model_free.argtypes = [vp]
+        for name in ("orc_model_n", "orc_model_tmax", "orc_model_nvar", "orc_model_nstates",
+                     "orc_model_nextid"):
+            getattr(h, name).argtypes = [vp]
+            getattr(h, name).restype = ctypes.c_uint
+        h.orc_model_np.argtypes = [vp, ctypes.c_uint]
+        h.orc_model_np.restype = ctypes.c_uint
+        h.orc_model_simp.argtypes = [vp, ctypes.c_uint, ctypes.c_uint]
+        h.orc_model_simp.restype = ctypes.c_uint
+        h.orc_model_short2all.argtypes = [vp, ctypes.c_uint]
+        h.orc_model_short2all.restype = ctypes.c_uint
+        h.orc_model_prior.argtypes = [vp, ctypes.c_uint]
+        h.orc_model_prior.restype = ctypes.c_double
+        h.orc_grid.argtypes = [ctypes.c_uint, ctypes.c_double, ctypes.c_double, _dp]
+        h.orc_grid.restype = ctypes.c_double
+        h.orc_loglik_grid_mt.argtypes = [vp, _dp, _dp, ctypes.c_uint, ctypes.c_uint, _dp]
+        h.orc_loglik_points.argtypes = [vp, _dp, _dp, ctypes.c_size_t, _dp]
+        h.orc_ltot.argtypes = [_dp, ctypes.c_uint, ctypes.c_double]
+        h.orc_ltot.restype = ctypes.c_double
+        h.orc_write_posterior.argtypes = [ctypes.c_char_p, _dp, ctypes.c_uint, ctypes.c_double]
+        _lib = h
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(_dp)
+
+
+class OracleModel:
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def load(cls, path, m=400.0, p=0.5, d=100.0):
+        h = ctypes.c_void_p()
+        rc = lib().orc_model_load(os.fsencode(str(path)), m, p, d, ctypes.byref(h))
+        if rc:
+            raise RuntimeError(f"oracle load failed ({rc})")
+        return cls(h)
+
+    @classmethod
+    def from_obs(cls, obs, m=400.0, p=0.5, d=100.0):
+        a = np.ascontiguousarray(obs, dtype=np.int32)
+        h = ctypes.c_void_p()
+        rc = lib().orc_model_build(a.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), a.shape[1], a.shape[0],
+                                   m, p, d, ctypes.byref(h))
+        if rc:
+            raise RuntimeError(f"oracle build failed ({rc})")
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_model_free(self.h)
+            self.h = None
+
+    def _u(self, name, *a):
+        return getattr(lib(), name)(self.h, *a)
+
+    n = property(lambda s: s._u("orc_model_n"))
+    tmax = property(lambda s: s._u("orc_model_tmax"))
+    nvar = property(lambda s: s._u("orc_model_nvar"))
+    nstates = property(lambda s: s._u("orc_model_nstates"))
+    nextid = property(lambda s: s._u("orc_model_nextid"))
+
+    @property
+    def npstates(self):
+        return np.array([self._u("orc_model_np", t) for t in range(self.tmax)])
+
+    @property
+    def year_ids(self):
+        nps = self.npstates
+        return [np.array([self._u("orc_model_simp", t, q) for q in range(nps[t])]) for t in range(self.tmax)]
+
+    @property
+    def short_state(self):
+        return np.array([self._u("orc_model_short2all", a) for a in range(self.nextid)])
+
+    @property
+    def prior(self):
+        return np.array([self._u("orc_model_prior", q) for q in range(self.npstates[0])])
+
+    def loglik_grid(self, e, c=None, threads=None):
+        e = np.ascontiguousarray(e, dtype=np.float64)
+        c = e if c is None else np.ascontiguousarray(c, dtype=np.float64)
+        if e.size != c.size:
+            ee, cc = np.meshgrid(e, c, indexing="ij")
+            return self.loglik_points(ee.ravel(), cc.ravel(), threads).reshape(e.size, c.size)
+        out = np.empty((e.size, c.size))
+        threads = threads or min(8, os.cpu_count() or 1)
+        if np.array_equal(e, c):
+            lib().orc_loglik_grid_mt(self.h, _p(e), _p(c), e.size, threads, _p(out))
+            return out
+        ee, cc = np.meshgrid(e, c, indexing="ij")
+        return self.loglik_points(ee.ravel(), cc.ravel(), threads).reshape(e.size, c.size)
+
+    def loglik_points(self, e, c, threads=None):
+        """loglik at paired points (e[q], c[q]); threads split the list."""
+        e = np.ascontiguousarray(e, dtype=np.float64)
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        out = np.empty(e.size)
+        threads = max(1, min(threads or 1, e.size))
+        if threads == 1:
+            lib().orc_loglik_points(self.h, _p(e), _p(c), e.size, _p(out))
+            return out
+        import concurrent.futures as cf
+        bounds = np.linspace(0, e.size, threads + 1).astype(int)
+
+        def work(i):
+            a, b = bounds[i], bounds[i + 1]
+            if b > a:
+                lib().orc_loglik_points(self.h, _p(e[a:b]), _p(c[a:b]), b - a, _p(out[a:b]))
+        # ctypes releases the GIL during the call, so threads run in parallel
+        with cf.ThreadPoolExecutor(threads) as ex:
+            list(ex.map(work, range(threads)))
+        return out
+
+
+def grid(s, lo=0.0, hi=1.0):
+    g = np.empty(s)
+    win = lib().orc_grid(s, lo, hi, _p(g))
+    return g, win
+
+
+def ltot(lik, win):
+    a = np.ascontiguousarray(lik, dtype=np.float64)
+    return lib().orc_ltot(_p(a), a.shape[0], win)
+
+
+def write_posterior(path, lik, lt):
+    a = np.ascontiguousarray(lik, dtype=np.float64)
+    rc = lib().orc_write_posterior(os.fsencode(str(path)), _p(a), a.shape[0], lt)
+    if rc:
+        raise RuntimeError("oracle write failed")
+
+
+def run(path, out=None, m=400.0, p=0.5, d=100.0, s=101, lo=0.0, hi=1.0, threads=None):
+    """Full reference pipeline on the CPU: returns (loglik, ltot)."""
+    model = OracleModel.load(path, m, p, d)
+    g, win = grid(s, lo, hi)
+    lik = model.loglik_grid(g, g, threads)
+    lt = ltot(lik, win)
+    if out is not None:
+        write_posterior(out, lik, lt)
+    return lik, lt

@@ -1,0 +1,261 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle on the
+same inputs.
+
+Tolerances (written here, per BASELINE north_star / SURVEY.md §8(c)):
+  * log-likelihood: |dlogL| <= LOGLIK_ATOL (1e-9, i.e. 1e-9 relative on L);
+    the factorised GPU form reorders an all-positive sum, so ~1e-13 is typical;
+  * posterior: relative 1e-6 where posterior > 1e-14, absolute 1e-20 below;
+  * -inf log-likelihoods (impossible transitions, underflow) and "-nan"
+    cells must sit at identical positions.
+"""
+from __future__ import annotations
+
+import subprocess
+
+import numpy as np
+import pytest
+
+import midaspom_amd as mdp
+import oracle
+from midaspom_amd import _lib, synth
+
+pytestmark = pytest.mark.gpu
+
+LOGLIK_ATOL = 1e-9
+POST_RTOL = 1e-6
+
+
+def assert_loglik_close(got, ref, atol=LOGLIK_ATOL):
+    got, ref = np.asarray(got), np.asarray(ref)
+    assert got.shape == ref.shape
+    assert np.array_equal(np.isneginf(got), np.isneginf(ref)), "-inf positions differ"
+    assert np.array_equal(np.isnan(got), np.isnan(ref)), "nan positions differ"
+    fin = np.isfinite(ref)
+    if fin.any():
+        err = np.abs(got[fin] - ref[fin]).max()
+        assert err <= atol, f"max |dlogL| = {err:.3e}"
+
+
+def assert_posterior_close(got, ref):
+    got, ref = np.asarray(got), np.asarray(ref)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    big = ok & (ref > 1e-14)
+    if big.any():
+        rel = np.abs(got[big] - ref[big]) / ref[big]
+        assert rel.max() <= POST_RTOL, f"max rel dposterior = {rel.max():.3e}"
+    small = ok & ~big
+    if small.any():
+        assert np.abs(got[small] - ref[small]).max() <= 1e-20
+    assert np.array_equal(got == 0, ref == 0) or np.abs(got - ref)[ok].max() <= 1e-20
+
+
+def gpu_grid(model, e, c=None, **kw):
+    c = e if c is None else c
+    with mdp.Engine(model, **kw) as eng:
+        return eng.loglik_grid(e, c)
+
+
+# ---------------------------------------------------------------------------
+# the SURVEY §8(c) anchor runs, end to end through the Python host
+# ---------------------------------------------------------------------------
+CASES = [
+    ("manual_p3_obs.txt", dict(m=400, d=200, s=5)),
+    ("occupancies.txt", dict(m=400, d=100, s=50)),
+    ("occupancies.txt", dict(m=400, d=100, s=101)),
+    ("occupancies.txt", dict(m=250, d=100, s=33, p=0.2)),
+    ("config2_64x50.txt", dict(m=400, d=100, s=17)),
+    ("config2_64x50.txt", dict(m=400, d=100, s=33, p=0.3)),
+    ("config2_64x50.txt", dict(m=400, d=100, s=21, lo=0.05, hi=0.95)),
+    ("config3_256x200.txt", dict(m=400, d=100, s=9)),
+    ("config3_256x200.txt", dict(m=400, d=100, s=17)),
+    ("config3_256x200.txt", dict(m=400, d=100, s=5)),  # Q4: all underflow -> -nan
+]
+
+
+@pytest.mark.parametrize("fname,f", CASES, ids=[f"{a}-{b}" for a, b in CASES])
+def test_file_runs_match_oracle(golden, fname, f):
+    kw = dict(m=f["m"], p=f.get("p", 0.5), d=f["d"])
+    s, lo, hi = f["s"], f.get("lo", 0.0), f.get("hi", 1.0)
+    g, win = mdp.grid(s, lo, hi)
+    model = mdp.Model.load(golden / fname, **kw)
+    got = gpu_grid(model, g)
+    om = oracle.OracleModel.load(golden / fname, kw["m"], kw["p"], kw["d"])
+    ref = om.loglik_grid(g, g)
+    assert_loglik_close(got, ref)
+    lt_got, lt_ref = mdp.log_total(got, win), oracle.ltot(ref, win)
+    if np.isfinite(lt_ref):
+        assert lt_got == pytest.approx(lt_ref, rel=1e-12)
+        assert f"{lt_got:.5f}" == f"{lt_ref:.5f}"
+    else:
+        assert np.isneginf(lt_got)
+    assert_posterior_close(mdp.posterior(got, lt_got), mdp.posterior(ref, lt_ref))
+
+
+def test_anchor_ltot_values(golden, anchors):
+    """Total log-likelihood lines equal the reference's."""
+    from conftest import run_by_name
+    for name in ["manual_p3", "default_example_s101", "config1_s50", "config2_s17",
+                 "config2_s17_p03", "config3_s9", "config3_s17", "config3_s32"]:
+        r = run_by_name(anchors, name)
+        f = r["flags"]
+        lik, lt = mdp.run_file(golden / r["input"], m=f["m"], p=f.get("p", 0.5), d=f["d"], s=f["s"])
+        assert f"{lt:.5f}" == r["ltot"], name
+
+
+def test_manual_posterior_table(golden, tmp_path):
+    lik, lt = mdp.run_file(golden / "manual_p3_obs.txt", tmp_path / "p.txt", m=400, d=200, s=5)
+    assert np.array_equal(np.round(np.loadtxt(tmp_path / "p.txt"), 6),
+                          np.loadtxt(golden / "manual_p3_posterior.txt"))
+
+
+def test_q5_impossible_transition(tmp_path):
+    obs = np.array([[0, 1, 1, 1], [0, 0, 0, 0], [0, 1, 0, 1]])
+    lik, lt = None, None
+    model = mdp.Model.from_obs(obs)
+    g, win = mdp.grid(3)
+    lik = gpu_grid(model, g)
+    assert np.isneginf(lik).all()
+    mdp.write_posterior(tmp_path / "q5.txt", lik, mdp.log_total(lik, win))
+    assert set((tmp_path / "q5.txt").read_text().split()) == {"-nan"}
+
+
+# ---------------------------------------------------------------------------
+# fuzzing: random problems covering every forward-kernel variant
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(24))
+def test_random_problems(seed):
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(2, 48))
+    nvar = int(rng.integers(1, min(n, 10) + 1))
+    T = int(rng.integers(1, 40))
+    maxm = int(rng.integers(0, 5))  # up to 16 states per year
+    obs = synth.random_obs(rng, n, T, nvar, pmiss=float(rng.choice([0.0, 0.1, 0.3])),
+                           max_missing=maxm, p1=float(rng.uniform(0.2, 0.8)))
+    p = float(rng.choice([0.5, 0.3, 0.7]))
+    m, d = float(rng.choice([100, 400, 1000])), float(rng.choice([50, 100, 200]))
+    s = int(rng.integers(2, 12))
+    lo, hi = float(rng.choice([0.0, 0.1])), float(rng.choice([1.0, 0.9, 1.3]))
+    e, _ = mdp.grid(s, lo, hi)
+    c, _ = mdp.grid(s + 3, 0.0, float(rng.choice([1.0, 2.0])))
+    model = mdp.Model.from_obs(obs, m=m, p=p, d=d)
+    got = gpu_grid(model, e, c)
+    ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c)
+    assert_loglik_close(got, ref)
+
+
+def test_single_year_and_constant_series():
+    for obs in (np.array([[1, 0, -1, 1]]), np.array([[0, 1, 1]] * 6), np.array([[1], [1], [0], [1]])):
+        model = mdp.Model.from_obs(obs)
+        g, _ = mdp.grid(7)
+        ref = oracle.OracleModel.from_obs(obs).loglik_grid(g, g)
+        assert_loglik_close(gpu_grid(model, g), ref)
+
+
+def test_too_many_missing_fails_loudly():
+    obs = np.array([[1, -1, -1, -1, -1, -1, 1], [1, 1, 0, 1, 0, 1, 1]])
+    model = mdp.Model.from_obs(obs)
+    with pytest.raises(mdp.MidaspomError, match="UNSUPPORTED"):
+        mdp.Engine(model)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE full sizes: nested sub-grid / sampled points against the oracle
+# ---------------------------------------------------------------------------
+def test_config2_full_grid_nested(golden):
+    """s = 512: the nested -s 74 sub-grid (511 = 7*73) plus the border rows."""
+    model = mdp.Model.load(golden / "config2_64x50.txt")
+    g, win = mdp.grid(512)
+    got = gpu_grid(model, g)
+    assert np.isfinite(got).all()
+    idx = np.arange(0, 512, 7)
+    om = oracle.OracleModel.load(golden / "config2_64x50.txt")
+    ee, cc = np.meshgrid(g[idx], g[idx], indexing="ij")
+    ref = om.loglik_points(ee.ravel(), cc.ravel(), threads=16).reshape(idx.size, idx.size)
+    assert_loglik_close(got[np.ix_(idx, idx)], ref)
+
+
+def test_config3_full_grid_sampled(golden):
+    model = mdp.Model.load(golden / "config3_256x200.txt")
+    g, win = mdp.grid(1024)
+    got = gpu_grid(model, g)
+    assert np.isfinite(got).all()
+    rng = np.random.default_rng(7)
+    ie, ic = rng.integers(0, 1024, 160), rng.integers(0, 1024, 160)
+    ie[:4], ic[:4] = [0, 1023, 0, 1023], [0, 0, 1023, 1023]
+    om = oracle.OracleModel.load(golden / "config3_256x200.txt")
+    ref = om.loglik_points(g[ie], g[ic], threads=16)
+    assert_loglik_close(got[ie, ic], ref)
+    # posterior normalisation over the whole grid is finite and sums to ~1/win^2 trapezoid
+    lt = mdp.log_total(got, win)
+    assert np.isfinite(lt)
+
+
+def test_grid_split_invariance(golden):
+    """Row slabs computed separately equal the full grid (the multi-GPU and
+    multi-rank partition relies on it)."""
+    model = mdp.Model.load(golden / "config2_64x50.txt")
+    g, _ = mdp.grid(129)
+    with mdp.Engine(model) as eng:
+        full = eng.loglik_grid(g, g)
+        parts = [eng.loglik_grid(g[a:b], g) for a, b in [(0, 40), (40, 41), (41, 129)]]
+    assert np.array_equal(np.vstack(parts), full)
+
+
+def test_device_run_matches_host_path(golden):
+    import torch
+    model = mdp.Model.load(golden / "config2_64x50.txt")
+    g, _ = mdp.grid(96)
+    with mdp.Engine(model) as eng:
+        host = eng.loglik_grid(g, g)
+        eng.set_grid(g, g)
+        out = torch.empty((96, 100), dtype=torch.float64, device="cuda")
+        eng.set_profiling(True)
+        eng.run(out.data_ptr(), 100, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ms = eng.kernel_ms()
+    assert np.array_equal(out[:, :96].cpu().numpy(), host)
+    assert set(ms) == {"k_coltables", "k_coefs", "k_forward"}
+    assert all(v > 0 for v in ms.values())
+
+
+def test_explicit_device_list(golden):
+    model = mdp.Model.load(golden / "occupancies.txt")
+    g, _ = mdp.grid(31)
+    a = gpu_grid(model, g, devices=[0])
+    b = gpu_grid(model, g)
+    assert np.array_equal(a, b)
+
+
+# ---------------------------------------------------------------------------
+# the CLI drop-in
+# ---------------------------------------------------------------------------
+def test_cli_matches_oracle_file(golden, tmp_path):
+    out = tmp_path / "post.txt"
+    r = subprocess.run([str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", "101", "-i",
+                        str(golden / "occupancies.txt"), "-o", str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Total log-likelihood=-39.34251\n" in r.stdout
+    lines = r.stdout.splitlines()
+    assert lines[0] == "------ MIDASPOM, beta version ------"
+    assert lines[3] == "\tWindow size=0.010000, number of steps=101"
+    assert "Number of habitat patches: 8" in lines and "Number of sampled years: 7" in lines
+    assert sum(1 for x in lines if x.endswith("% done")) == 101 and "100.00% done" in lines
+    ref_out = tmp_path / "ref.txt"
+    oracle.run(golden / "occupancies.txt", ref_out, s=101)
+    got_txt, ref_txt = out.read_text(), ref_out.read_text()
+    # identical bit layout: same cell count, tabs and newlines
+    assert [len(l.split("\t")) for l in got_txt.split("\n")] == [len(l.split("\t")) for l in ref_txt.split("\n")]
+    assert_posterior_close(np.loadtxt(out), np.loadtxt(ref_out))
+
+
+def test_cli_all_nan_file(tmp_path):
+    inp = tmp_path / "q5.txt"
+    inp.write_text("0 1 1 1\n0 0 0 0\n0 1 0 1\n")
+    out = tmp_path / "o.txt"
+    r = subprocess.run([str(_lib.CLI_PATH), "-s", "3", "-i", str(inp), "-o", str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    assert "Total log-likelihood=-inf" in r.stdout
+    assert out.read_text() == "-nan\t-nan\t-nan\t\n" * 3

@@ -1,0 +1,96 @@
+"""Pin the CPU oracle to the reference: every anchor in tests/golden/anchors.json
+(manual worked example, SURVEY.md §8(c) / Appendix C outputs of the reference
+itself).  The default-example posterior must be byte-identical to the
+reference built against a naive dgemm (md5)."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+from midaspom_amd import synth
+
+
+def md5(path):
+    return hashlib.md5(open(path, "rb").read()).hexdigest()
+
+
+def _run(golden, anchors, tmp_path, name, threads=8):
+    from conftest import run_by_name
+    r = run_by_name(anchors, name)
+    f = r["flags"]
+    if "obs" in r:
+        inp = tmp_path / "obs.txt"
+        inp.write_text("".join(" ".join(map(str, row)) + "\n" for row in r["obs"]))
+    else:
+        inp = golden / r["input"]
+    out = tmp_path / f"{name}.txt"
+    lik, lt = oracle.run(inp, out, m=f.get("m", 400), p=f.get("p", 0.5), d=f.get("d", 100),
+                         s=f["s"], threads=threads)
+    return r, lik, lt, out
+
+
+def test_inputs_md5(golden, anchors):
+    for fname, h in anchors["inputs_md5"].items():
+        assert md5(golden / fname) == h, fname
+
+
+def test_generator_reproduces_survey_inputs():
+    assert hashlib.md5(synth.generate(**synth.CONFIG2).encode()).hexdigest() == synth.MD5["config2"]
+    assert hashlib.md5(synth.generate(**synth.CONFIG3).encode()).hexdigest() == synth.MD5["config3"]
+
+
+def test_manual_worked_example(golden, anchors, tmp_path):
+    r, lik, lt, out = _run(golden, anchors, tmp_path, "manual_p3")
+    assert f"{lt:.5f}" == r["ltot"]
+    post = np.loadtxt(out)
+    expect = np.loadtxt(golden / r["posterior_6dp"])
+    assert np.array_equal(np.round(post, 6), expect)
+
+
+def test_default_example_bit_exact(golden, anchors, tmp_path):
+    r, lik, lt, out = _run(golden, anchors, tmp_path, "default_example_s101")
+    assert f"{lt:.5f}" == r["ltot"]
+    assert md5(out) == r["md5"]["naive"]
+    post = np.loadtxt(out)
+    assert int((post == 0).sum()) == r["exact_zeros"]
+    assert list(np.unravel_index(post.argmax(), post.shape)) == r["argmax"]
+    assert f"{post.max():.15g}" == repr(r["argmax_value"])
+
+
+@pytest.mark.parametrize("name", ["config1_s50", "config2_s17"])
+def test_ltot_and_argmax(golden, anchors, tmp_path, name):
+    r, lik, lt, out = _run(golden, anchors, tmp_path, name)
+    assert f"{lt:.5f}" == r["ltot"]
+    post = np.loadtxt(out)
+    assert list(np.unravel_index(post.argmax(), post.shape)) == r["argmax"]
+    assert post.max() == pytest.approx(r["argmax_value"], rel=1e-13)
+
+
+def test_config2_posterior_md5(golden, anchors, tmp_path):
+    r, lik, lt, out = _run(golden, anchors, tmp_path, "config2_s17")
+    assert md5(out) == r["md5"]["openblas"]
+
+
+def test_q3_prior_semantics(golden, anchors, tmp_path):
+    r, lik, lt, out = _run(golden, anchors, tmp_path, "config2_s17_p03")
+    assert f"{lt:.5f}" == r["ltot"]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["config3_s9", "config3_s17"])
+def test_config3_anchors(golden, anchors, tmp_path, name):
+    r, lik, lt, out = _run(golden, anchors, tmp_path, name)
+    assert f"{lt:.5f}" == r["ltot"]
+    if "md5" in r:
+        assert md5(out) == r["md5"]["openblas"]
+
+
+@pytest.mark.parametrize("name", ["config3_s5_underflow", "q5_impossible"])
+def test_all_nan_cases(golden, anchors, tmp_path, name):
+    r, lik, lt, out = _run(golden, anchors, tmp_path, name)
+    assert np.isneginf(lt)
+    cells = out.read_text().split()
+    assert cells and all(c == "-nan" for c in cells)
