@@ -67,11 +67,13 @@ def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, budget_s=12.0):
     got = lik_gpu[ee, cc]
     with np.errstate(invalid="ignore", over="ignore"):
         pg, pr = np.exp(got - ltot_gpu), np.exp(ref - ltot_gpu)
-    fin = np.isfinite(pr)
+    fin = np.isfinite(pr) & np.isfinite(pg)
+    same_inf = bool(np.array_equal(np.isneginf(got), np.isneginf(ref)))
     dabs = float(np.abs(pg[fin] - pr[fin]).max()) if fin.any() else 0.0
     big = fin & (pr > 1e-14)
     drel = float((np.abs(pg[big] - pr[big]) / pr[big]).max()) if big.any() else 0.0
-    dlog = float(np.abs(got[fin] - ref[fin]).max()) if fin.any() else 0.0
+    fl = np.isfinite(got) & np.isfinite(ref)
+    dlog = float(np.abs(got[fl] - ref[fl]).max()) if fl.any() else 0.0
     return {
         "value": ee.size * (tmax - 1) / wall,
         "unit": "grid-point-timestep evals/s",
@@ -81,7 +83,7 @@ def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, budget_s=12.0):
                   f"oracle/spom_oracle.c dense formulation with naive dgemm, {threads} threads, "
                   f"{wall:.1f} s",
     }, {"max_abs_dposterior": dabs, "max_rel_dposterior": drel, "max_abs_dloglik": dlog,
-        "points_checked": int(ee.size)}
+        "points_checked": int(ee.size), "neginf_positions_match": same_inf}
 
 
 def main():
