@@ -5,28 +5,34 @@
 // (colonisation pressure :350-358, compPePc :18-50, P = Pe*Pc dgemm :363,
 // forward propagation :368-384, prior sum + log :386-392).
 //
-// Factorisation used.  For observed short states a -> b with
-// bit sets A, B and hidden intermediate state j (extinction first, then
-// colonisation), the reference forms P[a][b] = sum_j Pe[a][j] Pc[j][b] with
+// Factorisation.  For observed short states a -> b with bit
+// sets A, B and hidden intermediate state j (extinction first, then
+// colonisation) the reference forms P[a][b] = sum_j Pe[a][j] Pc[j][b] with
 //   Pe[a][j] = [j <= A] x^{|A|-|j|} y^{|j|}        (x = min(e,1), y = 1-x)
 //   Pc[j][b] = [j <= B] prod_{k : j_k = 0} (B_k ? pC_jk : 1-pC_jk),
-//   pC_jk    = min(1, c * S[j][k]),  S = grid-invariant dispersal sums.
+//   pC_jk    = min(1, c * S[j][k]),   S = grid-invariant dispersal sums.
 // Pe depends on e only through |j| and Pc on c only, so
 //   P[a][b](e,c) = sum_{m=0}^{|A&B|} x^{|A|-m} y^m Q_ab[m](c),
 //   Q_ab[m](c)   = sum_{j <= A&B, |j| = m} Pc[j][b](c).
-// Kernels:
-//   k_colsum     (once per engine) S[k][j]
-//   k_coltables  (per c)  Z[c][j] = prod_{non-var k}(1-pC_jk), PV[c][b][j] = pC_j,var(b)
-//   k_coefs      (per c)  Q[c][pair][m]
-//   k_forward    (per (e,c) point) forward recursion over the years with the
-//                transition entries evaluated from Q in Bernstein/Horner form;
-//                lanes = e values, one c per workgroup so Q is wave-uniform
-//                and streams through the scalar cache (s_load), no LDS.
+// Multiplying by (x+y)^{D-|A|} = 1 makes every transition a homogeneous
+// polynomial of ONE degree D (>= every |A|) with non-negative coefficients
+//   P[a][b](e,c) = sum_{r=0}^{D} R_ab[r](c) W_r(e),  W_r = x^{D-r} y^r,
+//   R_ab[r]      = sum_m Q_ab[m] C(D-|A|, r-m),
+// so a transition costs D+1 FMAs against per-point weights held in VGPRs and
+// per-c coefficients that are wave-uniform (scalar loads, no descriptors).
+//
+// Kernels (per run over an ne x nc grid):
+//   k_zpv      [c][j]     Z = prod_{always-zero k} (1-pC_jk), PV_b = pC_j,var(b)
+//   k_coefs    one WG / c Q (subset sums, LDS) -> R in forward-use order
+//   k_forward  one lane / (e,c) point x EPL: forward recursion over the years,
+//              c wave-uniform, R streamed through the scalar cache.
+// Once per engine: k_colsum builds S.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <new>
@@ -37,9 +43,16 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr uint32_t kOffBits = 22;              // coefficient offset bits in a use descriptor
-constexpr uint32_t kOffMask = (1u << kOffBits) - 1u;
-constexpr int kColTile = 8;                    // c values per k_coltables thread
+constexpr int kZpvJ = 64;       // k_zpv: hidden states per workgroup
+constexpr int kZpvSlices = 4;   // k_zpv: waves splitting the zero-column product
+constexpr int kZpvCT = 2;       // k_zpv: c values per thread
+constexpr int kZpvUnroll = 8;   // k_zpv: S loads in flight per lane
+constexpr int kEPL = 2;         // k_forward: default grid points (e values) per lane
+constexpr int kMaxDeg = 24;
+constexpr unsigned kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), other counters untouched
+constexpr size_t kLdsBudget = 120 * 1024;  // dynamic LDS of k_coefs
+
+__constant__ double c_binom[kMaxDeg + 1][kMaxDeg + 1];
 
 #define HIP_TRY(expr)                                                                     \
     do {                                                                                  \
@@ -53,176 +66,323 @@ constexpr int kColTile = 8;                    // c values per k_coltables threa
 // kernels
 // ---------------------------------------------------------------------------
 
-// S[k][j] = sum over set bits of state j (ascending variable column l, l != k)
-// of M[l][k] -- the reference's per-point sum at :350-357, which skips zero
-// terms exactly, so the result is bit-identical.
+// S2[r][j] = S[col(r)][j]: the colonisation sum of column k = col(r) for
+// hidden state j, i.e. the sum over set bits of j (ascending variable column
+// l, l != k) of M[l][k] -- the reference's per-point sum (:350-357) with its
+// zero terms dropped, bit-identical.  Rows are ordered always-zero columns
+// first, then variable columns, so k_zpv reads them without indirection.
 __global__ __launch_bounds__(kBlock) void k_colsum(const double *__restrict__ M,
                                                    const uint32_t *__restrict__ var_cols,
+                                                   const uint32_t *__restrict__ row_col,
                                                    uint32_t n, uint32_t nvar, uint32_t nstates,
-                                                   double *__restrict__ S)
+                                                   double *__restrict__ S2)
 {
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t k = blockIdx.y;
+    const uint32_t r = blockIdx.y;
     if (j >= nstates) return;
+    const uint32_t k = row_col[r];
     double acc = 0.0;
     for (uint32_t b = 0; b < nvar; ++b) {
         const uint32_t col = var_cols[b];
         if (((j >> (nvar - 1 - b)) & 1u) && col != k) acc += M[(size_t)col * n + k];
     }
-    S[(size_t)k * nstates + j] = acc;
+    S2[(size_t)r * nstates + j] = acc;
 }
 
-// Per c value: Z[c][j] (product over always-zero columns, ascending) and the
-// clamped pressure on each variable column.  One thread = one hidden state j
-// for kColTile consecutive c values (S is read once per tile).
-__global__ __launch_bounds__(kBlock) void k_coltables(
-    const double *__restrict__ S, uint32_t nstates, const uint32_t *__restrict__ nonvar,
-    uint32_t nnv, const uint32_t *__restrict__ var_cols, uint32_t nvar,
-    const double *__restrict__ cvals, uint32_t nc, double *__restrict__ Z, double *__restrict__ PV)
+// ZPV[c][0][j] = prod over always-zero columns (ascending) of (1 - pC_jk);
+// ZPV[c][1+b][j] = pC_j,var(b) = min(1, c S).  A workgroup covers 64 hidden
+// states x kZpvCT c values; its 4 waves each take a quarter of the zero
+// columns (kZpvUnroll loads in flight per lane) and the partial products are
+// multiplied in slice order through LDS.
+__global__ __launch_bounds__(kBlock) void k_zpv(
+    const double *__restrict__ S2, uint32_t nstates, uint32_t nnv, uint32_t nvar,
+    const double *__restrict__ cvals, uint32_t nc, double *__restrict__ ZPV)
 {
-    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t c0 = blockIdx.y * kColTile;
-    if (j >= nstates) return;
-    double c[kColTile], z[kColTile];
+    __shared__ double part[kZpvSlices][kZpvCT][kZpvJ];
+    const uint32_t lane = threadIdx.x % kZpvJ, slice = threadIdx.x / kZpvJ;
+    const uint32_t j = blockIdx.x * kZpvJ + lane;
+    const uint32_t c0 = blockIdx.y * kZpvCT;
+    const bool ok = j < nstates;
+    const uint32_t jj = ok ? j : 0;
+    double c[kZpvCT], z[kZpvCT];
 #pragma unroll
-    for (int t = 0; t < kColTile; ++t) {
+    for (int t = 0; t < kZpvCT; ++t) {
         c[t] = (c0 + t < nc) ? cvals[c0 + t] : 0.0;
         z[t] = 1.0;
     }
-    for (uint32_t q = 0; q < nnv; ++q) {
-        const double s = S[(size_t)nonvar[q] * nstates + j];
+    const uint32_t per = (nnv + kZpvSlices - 1) / kZpvSlices;
+    const uint32_t q0 = slice * per, q1 = min(nnv, q0 + per);
+    uint32_t q = q0;
+    for (; q + kZpvUnroll <= q1; q += kZpvUnroll) {
+        double sv[kZpvUnroll];
 #pragma unroll
-        for (int t = 0; t < kColTile; ++t) {
-            double pc = c[t] * s;
-            pc = pc > 1.0 ? 1.0 : pc;
-            z[t] = z[t] * (1.0 - pc);
-        }
+        for (int u = 0; u < kZpvUnroll; ++u) sv[u] = S2[(size_t)(q + u) * nstates + jj];
+#pragma unroll
+        for (int u = 0; u < kZpvUnroll; ++u)
+#pragma unroll
+            for (int t = 0; t < kZpvCT; ++t)
+                // 1 - min(1, c s), evaluated as max(0, 1 - c s) with one rounding
+                z[t] *= fmax(0.0, fma(-c[t], sv[u], 1.0));
+    }
+    for (; q < q1; ++q) {
+        const double s0 = S2[(size_t)q * nstates + jj];
+#pragma unroll
+        for (int t = 0; t < kZpvCT; ++t) z[t] *= fmax(0.0, fma(-c[t], s0, 1.0));
     }
 #pragma unroll
-    for (int t = 0; t < kColTile; ++t)
-        if (c0 + t < nc) Z[(size_t)(c0 + t) * nstates + j] = z[t];
-    for (uint32_t b = 0; b < nvar; ++b) {
-        const double s = S[(size_t)var_cols[b] * nstates + j];
+    for (int t = 0; t < kZpvCT; ++t) part[slice][t][lane] = z[t];
+    __syncthreads();
+    const size_t rows = (size_t)nvar + 1;
+    if (slice == 0 && ok) {
 #pragma unroll
-        for (int t = 0; t < kColTile; ++t) {
-            if (c0 + t < nc) {
-                double pc = c[t] * s;
-                pc = pc > 1.0 ? 1.0 : pc;
-                PV[((size_t)(c0 + t) * nvar + b) * nstates + j] = pc;
-            }
+        for (int t = 0; t < kZpvCT; ++t) {
+            double zz = part[0][t][lane];
+#pragma unroll
+            for (int sl = 1; sl < kZpvSlices; ++sl) zz *= part[sl][t][lane];
+            if (c0 + t < nc) ZPV[(size_t)(c0 + t) * rows * nstates + j] = zz;
         }
     }
+    if (ok)
+        for (uint32_t b = slice; b < nvar; b += kZpvSlices) {
+            const double sb = S2[(size_t)(nnv + b) * nstates + j];
+#pragma unroll
+            for (int t = 0; t < kZpvCT; ++t)
+                if (c0 + t < nc) {
+                    const double pc = c[t] * sb;
+                    ZPV[((size_t)(c0 + t) * rows + 1 + b) * nstates + j] = pc > 1.0 ? 1.0 : pc;
+                }
+        }
 }
 
-// Q[c][off_p + m] = sum_{j <= A&B, |j| = m} Z[c][j] * prod_{var b, j_b = 0} f_b,
-// f_b = B_b ? pC : 1 - pC (ascending variable column, as compPePc's k loop).
+// One workgroup per c value.
+//  1. (LDS_ZPV) stage this c's Z/PV block in LDS;
+//  2. lanes over transition pairs: Q_ab[m] = sum over subsets j of A&B with
+//     |j| = m of Z_j * prod_{var b not in j} (B_b ? pC : 1-pC)  (subsets
+//     enumerated once, accumulated per popcount in LDS);
+//  3. lanes over (use, r): R[c][use][r] = sum_m Q[m] C(D-|A|, r-m).
+template <bool LDS_ZPV, int NV>
 __global__ __launch_bounds__(kBlock) void k_coefs(
+    const double *__restrict__ ZPV, uint32_t nstates, uint32_t nvar,
     const uint32_t *__restrict__ pairA, const uint32_t *__restrict__ pairB,
-    const uint32_t *__restrict__ pairOff, uint32_t npairs, uint32_t nvar, uint32_t nstates,
-    const double *__restrict__ Z, const double *__restrict__ PV, uint32_t ncoef,
-    double *__restrict__ Q)
+    const uint32_t *__restrict__ pairOff, const uint32_t *__restrict__ items, uint32_t nitems,
+    const uint32_t *__restrict__ use_pair, uint32_t nuses, uint32_t deg,
+    double *__restrict__ R, size_t ldR)
 {
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t ic = blockIdx.y;
-    if (p >= npairs) return;
-    const uint32_t A = pairA[p], B = pairB[p], X = A & B;
-    const uint32_t nX = __popc(X);
-    const double *z = Z + (size_t)ic * nstates;
-    const double *pv = PV + (size_t)ic * nvar * nstates;
-    double *q = Q + (size_t)ic * ncoef + pairOff[p];
-    for (uint32_t m = 0; m <= nX; ++m) {
-        double acc = 0.0;
-        uint32_t sub = X;
-        for (;;) {
-            if ((uint32_t)__popc(sub) == m) {
-                double prod = z[sub];
-                for (uint32_t b = 0; b < nvar; ++b) {
-                    const uint32_t bit = nvar - 1 - b;
-                    if (!((sub >> bit) & 1u)) {
-                        const double f = pv[(size_t)b * nstates + sub];
-                        prod *= ((B >> bit) & 1u) ? f : 1.0 - f;
-                    }
-                }
-                acc += prod;
-            }
-            if (sub == 0) break;
-            sub = (sub - 1) & X;
-        }
-        q[m] = acc;
-    }
-}
-
-// Transition entry P[a][b](e,c) from its coefficient block (wave-uniform
-// pointer -> scalar loads): Horner in x with y^m folded in, then x^{|A|-|X|}.
-__device__ __forceinline__ double eval_transition(const double *__restrict__ q, uint32_t d,
-                                                  double x, double y)
-{
-    const double *cf = q + (d & kOffMask);
-    const uint32_t nX = (d >> kOffBits) & 31u;
-    const uint32_t nA = d >> 27;
-    double acc = cf[0];
-    double yp = 1.0;
-    for (uint32_t m = 1; m <= nX; ++m) {
-        yp *= y;
-        acc = fma(acc, x, cf[m] * yp);
-    }
-    for (uint32_t r = nX; r < nA; ++r) acc *= x;
-    return acc;
-}
-
-// Forward recursion for one grid point per lane.  Q3 semantics of the
-// reference (:368-369): start from a vector of ones over the year-0 states,
-// L = prior0 * sum_l v[l] accumulated as sum_l v[l]*prior0.
-template <int NPMAX>
-__global__ __launch_bounds__(kBlock) void k_forward(
-    const double *__restrict__ Q, uint32_t ncoef, const uint32_t *__restrict__ desc,
-    const uint32_t *__restrict__ npy, uint32_t tmax, double prior0,
-    const double *__restrict__ evals, uint32_t ne, double *__restrict__ out, uint32_t ld_out)
-{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t ic = blockIdx.x;
-    const uint32_t ie = blockIdx.y * kBlock + threadIdx.x;
-    const bool active = ie < ne;
-    const double e = active ? evals[ie] : 0.0;
-    const double x = e > 1.0 ? 1.0 : e;
-    const double y = 1.0 - x;
-    const double *__restrict__ q = Q + (size_t)ic * ncoef;
+    const size_t zsz = (size_t)(nvar + 1) * nstates;
+    const double *zg = ZPV + (size_t)ic * zsz;
+    const double *zpv;
+    double *Qs;
+    if constexpr (LDS_ZPV) {
+        for (size_t i = threadIdx.x; i < zsz; i += kBlock) lds[i] = zg[i];
+        zpv = lds;
+        Qs = lds + zsz;
+    } else {
+        zpv = zg;
+        Qs = lds;
+    }
+    __syncthreads();
+    // one lane per coefficient item (pair p, popcount m): sum over the
+    // C(|X|, m) subsets j of X = A&B with |j| = m (Gosper's sequence of
+    // m-bit patterns over the |X| positions, deposited into X)
+    for (uint32_t it = threadIdx.x; it < nitems; it += kBlock) {
+        const uint32_t w = items[it];
+        const uint32_t p = w >> 5, m = w & 31u;
+        const uint32_t A = pairA[p], B = pairB[p], X = A & B;
+        const uint32_t nX = __popc(X);
+        double acc = 0.0;
+        uint32_t pat = m ? ((1u << m) - 1u) : 0u;
+        const uint32_t lim = 1u << nX;
+        while (pat < lim) {
+            uint32_t sub = 0, xs = X, bits = pat;
+            while (bits) {
+                const uint32_t low = xs & (0u - xs);
+                if (bits & 1u) sub |= low;
+                xs ^= low;
+                bits >>= 1;
+            }
+            // branch-free: every factor load is issued up front; bits of j
+            // contribute an exact 1.0
+            double prod = zpv[sub];
+#pragma unroll
+            for (int b = 0; b < NV; ++b) {
+                if ((uint32_t)b < nvar) {
+                    const uint32_t bit = nvar - 1 - b;
+                    const double f = zpv[(size_t)(1 + b) * nstates + sub];
+                    const double g = ((B >> bit) & 1u) ? f : 1.0 - f;
+                    prod *= ((sub >> bit) & 1u) ? 1.0 : g;
+                }
+            }
+            acc += prod;
+            if (pat == 0) break;
+            const uint32_t t = pat | (pat - 1u);  // next pattern with the same popcount
+            pat = (t + 1u) | (((~t & (0u - ~t)) - 1u) >> (__ffs(pat) ));
+        }
+        Qs[pairOff[p] + m] = acc;
+    }
+    __syncthreads();
+    const uint32_t rs = deg + 1;
+    double *Rc = R + (size_t)ic * ldR;
+    for (uint32_t it = nuses * rs + threadIdx.x; it < (nuses + 2) * rs; it += kBlock) Rc[it] = 0.0;
+    for (uint32_t it = threadIdx.x; it < nuses * rs; it += kBlock) {
+        const uint32_t u = it / rs, r = it - u * rs;
+        const uint32_t p = use_pair[u];
+        const uint32_t A = pairA[p];
+        const uint32_t nA = __popc(A), nX = __popc(A & pairB[p]);
+        const uint32_t lift = deg - nA;
+        const double *q = Qs + pairOff[p];
+        double acc = 0.0;
+        const uint32_t m0 = r > lift ? r - lift : 0;
+        const uint32_t m1 = r < nX ? r : nX;
+        for (uint32_t m = m0; m <= m1; ++m) acc += q[m] * c_binom[lift][r - m];
+        Rc[it] = acc;
+    }
+}
 
-    double v[NPMAX];
-    uint32_t npp = npy[0];
+// Dot product of one transition's coefficients (wave-uniform, SGPRs) with a
+// point's weights, as two interleaved partial sums for FMA latency.
+template <int RS>
+__device__ __forceinline__ double tdot(const double (&rc)[RS], const double (&w)[RS])
+{
+    double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-    for (int k = 0; k < NPMAX; ++k) v[k] = (uint32_t)k < npp ? 1.0 : 0.0;
-    uint32_t u = 0;
-    for (uint32_t t = 1; t < tmax; ++t) {
-        const uint32_t npc = npy[t];
-        double vn[NPMAX];
+    for (int r = 0; r + 1 < RS; r += 2) {
+        a0 = fma(rc[r], w[r], a0);
+        a1 = fma(rc[r + 1], w[r + 1], a1);
+    }
+    if constexpr (RS & 1) a0 = fma(rc[RS - 1], w[RS - 1], a0);
+    return a0 + a1;
+}
+
+// Coefficients are read through the constant address space: the data is
+// read-only for the whole launch, so uniform reads become scalar loads even
+// next to explicit s_waitcnt / sched_barrier intrinsics.
+typedef const __attribute__((address_space(4))) double cdouble;
+
+template <int RS>
+__device__ __forceinline__ void tload(double (&dst)[RS], cdouble *src)
+{
 #pragma unroll
-        for (int l = 0; l < NPMAX; ++l) {
-            double acc = 0.0;
-            if ((uint32_t)l < npc) {
+    for (int r = 0; r < RS; ++r) dst[r] = src[r];
+}
+
+// Forward recursion, EPL grid points per lane (e values ie, ie+256, ...), one
+// c per workgroup.  Program `prog` (padded with one trailing word): one word
+// per step, either a run of `count` consecutive 1x1 transitions (v0 *= P) or
+// one general year (npp -> npc states, the reference's Pold*Pcur at :379).
+// Inside a run the coefficient loads are software-pipelined two transitions
+// ahead (R is padded by two transitions per c, so prefetches never leave it).  Q3 semantics (:368-369): start from ones over the
+// year-0 states; L = sum_l v_l*prior0.
+template <int NPMAX, int DEG, int EPL>
+__global__ __launch_bounds__(kBlock) void k_forward(
+    const double *__restrict__ R, size_t ldR, const uint32_t *__restrict__ prog, uint32_t nprog,
+    uint32_t np0, double prior0, const double *__restrict__ evals, uint32_t ne,
+    double *__restrict__ out, uint32_t ld_out)
+{
+    constexpr int RS = DEG + 1;
+    const uint32_t ic = blockIdx.x;
+    uint32_t ie[EPL];
+    double W[EPL][RS];
+    double v[EPL][NPMAX];
 #pragma unroll
-                for (int k = 0; k < NPMAX; ++k) {
-                    if ((uint32_t)k < npp) {
-                        const double P = eval_transition(q, desc[u], x, y);
-                        ++u;
-                        acc = fma(v[k], P, acc);
+    for (int i = 0; i < EPL; ++i) {
+        ie[i] = blockIdx.y * (kBlock * EPL) + i * kBlock + threadIdx.x;
+        const double e = ie[i] < ne ? evals[ie[i]] : 0.0;
+        const double x = e > 1.0 ? 1.0 : e;
+        const double y = 1.0 - x;
+        double yp[RS];
+        yp[0] = 1.0;
+#pragma unroll
+        for (int r = 1; r < RS; ++r) yp[r] = yp[r - 1] * y;
+        double xp = 1.0;
+#pragma unroll
+        for (int r = DEG; r >= 0; --r) {
+            W[i][r] = xp * yp[r];
+            xp *= x;
+        }
+#pragma unroll
+        for (int k = 0; k < NPMAX; ++k) v[i][k] = (uint32_t)k < np0 ? 1.0 : 0.0;
+    }
+
+    cdouble *rp = (cdouble *)(R + (size_t)ic * ldR);  // next transition
+    uint32_t op = prog[0];
+    for (uint32_t pi = 0; pi < nprog; ++pi) {
+        const uint32_t op_next = prog[pi + 1];
+        if ((op & 1u) == 0) {
+            // run of 1x1 transitions: ping-pong coefficient buffers.  Scalar
+            // loads return out of order, so the only usable wait is
+            // lgkmcnt(0): each half waits for its buffer, THEN issues the
+            // other buffer's loads, then computes -- the loads fly under the
+            // compute (sched_barrier keeps the compiler from sinking them).
+            uint32_t cnt = op >> 1;
+            double r0[RS], r1[RS];
+            tload(r0, rp);
+            for (; cnt >= 2; cnt -= 2) {
+                double P[EPL];
+                __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+                __builtin_amdgcn_sched_barrier(0);
+                tload(r1, rp + RS);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) P[i] = tdot(r0, W[i]);
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * P[i];
+                __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+                __builtin_amdgcn_sched_barrier(0);
+                tload(r0, rp + 2 * RS);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) P[i] = tdot(r1, W[i]);
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * P[i];
+                rp += 2 * RS;
+            }
+            if (cnt) {
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * tdot(r0, W[i]);
+                rp += RS;
+            }
+        } else {
+            const uint32_t npp = (op >> 8) & 0xffu, npc = (op >> 16) & 0xffu;
+            double vn[EPL][NPMAX];
+#pragma unroll
+            for (int l = 0; l < NPMAX; ++l) {
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) vn[i][l] = 0.0;
+                if ((uint32_t)l < npc) {
+#pragma unroll
+                    for (int k = 0; k < NPMAX; ++k) {
+                        if ((uint32_t)k < npp) {
+                            double rc[RS];
+                            tload(rc, rp);
+                            rp += RS;
+#pragma unroll
+                            for (int i = 0; i < EPL; ++i) vn[i][l] = fma(v[i][k], tdot(rc, W[i]), vn[i][l]);
+                        }
                     }
                 }
             }
-            vn[l] = acc;
+#pragma unroll
+            for (int i = 0; i < EPL; ++i)
+#pragma unroll
+                for (int l = 0; l < NPMAX; ++l) v[i][l] = vn[i][l];
         }
-#pragma unroll
-        for (int l = 0; l < NPMAX; ++l) v[l] = vn[l];
-        npp = npc;
+        op = op_next;
     }
-    double L = 0.0;
+    // v beyond the last year's state count is zero: the in-order sum over all
+    // NPMAX slots adds exact zeros only
 #pragma unroll
-    for (int l = 0; l < NPMAX; ++l)
-        if ((uint32_t)l < npp) L += v[l] * prior0;
-    if (active) out[(size_t)ie * ld_out + ic] = log(L);
+    for (int i = 0; i < EPL; ++i) {
+        double L = 0.0;
+#pragma unroll
+        for (int l = 0; l < NPMAX; ++l) L += v[i][l] * prior0;
+        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + ic] = log(L);
+    }
 }
 
 // ---------------------------------------------------------------------------
-// engine
+// host side
 // ---------------------------------------------------------------------------
 
 template <typename T>
@@ -255,27 +415,27 @@ int dev_reserve(T **p, size_t *cap, size_t count)
     *cap = 0;
     int rc = dev_alloc(p, count);
     if (rc) return rc;
-    *cap = count;
+    *cap = count ? count : 1;
     return MDP_OK;
 }
 
-enum { kEvBegin = 0, kEvColTables, kEvCoefs, kEvForward, kNumEv };
-const char *const kKernelNames[] = {"k_coltables", "k_coefs", "k_forward"};
+enum { kEvBegin = 0, kEvZpv, kEvCoefs, kEvForward, kNumEv };
+const char *const kKernelNames[] = {"k_zpv", "k_coefs", "k_forward"};
 
 struct DevCtx {
     int device = 0;
     hipStream_t stream = nullptr;
     double *S = nullptr;
-    uint32_t *var_cols = nullptr, *nonvar = nullptr;
+    uint32_t *var_cols = nullptr, *row_col = nullptr;
     uint32_t *pairA = nullptr, *pairB = nullptr, *pairOff = nullptr;
-    uint32_t *desc = nullptr, *npy = nullptr;
+    uint32_t *use_pair = nullptr, *prog = nullptr, *items = nullptr;
     double *e = nullptr, *c = nullptr;
     size_t cap_e = 0, cap_c = 0;
     uint32_t ne = 0, nc = 0;
-    double *Z = nullptr, *PV = nullptr, *Q = nullptr, *out = nullptr;
-    size_t cap_z = 0, cap_pv = 0, cap_q = 0, cap_out = 0;
-    std::vector<hipEvent_t> ev;   // kNumEv events per profiled run, reused
-    size_t ev_used = 0;           // event sets recorded since the last collect
+    double *ZPV = nullptr, *R = nullptr, *out = nullptr;
+    size_t cap_zpv = 0, cap_r = 0, cap_out = 0;
+    std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
+    size_t ev_used = 0;          // event sets recorded since the last collect
 };
 
 }  // namespace
@@ -283,8 +443,13 @@ struct DevCtx {
 struct mdp_engine {
     uint32_t n = 0, tmax = 0, nvar = 0, nstates = 0, nextid = 0;
     uint32_t npairs = 0, nuses = 0, ncoef = 0, npmax = 1, variant = 0;
+    uint32_t deg = 0;         // homogeneous transition degree D
+    uint32_t maxA = 0;        // max |A| over uses
+    int epl = kEPL;           // k_forward points per lane (MDP_EPL overrides: 1, 2, 4)
+    bool lds_zpv = true;      // k_coefs stages Z/PV in LDS
+    size_t coef_lds = 0;      // k_coefs dynamic LDS bytes
     double prior0 = 1.0;
-    std::vector<uint32_t> np, pairA, pairB, pairOff, desc;
+    std::vector<uint32_t> np, pairA, pairB, pairOff, use_pair, prog, items;
     std::vector<DevCtx> devs;
     int profiling = 0;
     double last_ms[3] = {0, 0, 0};  // mean per run over the last collected runs
@@ -294,21 +459,29 @@ struct mdp_engine {
 
 namespace {
 
-int select_variant(uint32_t npmax, uint32_t *variant)
+constexpr int kDegBuckets[] = {2, 4, 6, 8, 12, 16, 24};
+
+int select_variant(mdp_engine *eng)
 {
-    if (npmax <= 1) *variant = 1;
-    else if (npmax <= 2) *variant = 2;
-    else if (npmax <= 4) *variant = 4;
-    else if (npmax <= 8) *variant = 8;
-    else if (npmax <= 16) *variant = 16;
-    else
+    uint32_t np = 0;
+    for (uint32_t b : {1u, 2u, 4u, 8u, 16u})
+        if (eng->npmax <= b) { np = b; break; }
+    if (!np)
         return mdp_set_error(MDP_EUNSUPPORTED,
                              "a year with %u possible states (more than 4 missing patches) "
-                             "exceeds the register-resident forward kernel (max 16)", npmax);
+                             "exceeds the register-resident forward kernel (max 16)", eng->npmax);
+    uint32_t deg = 0;
+    for (int b : kDegBuckets)
+        if (eng->maxA <= (uint32_t)b) { deg = (uint32_t)b; break; }
+    if (!deg) return mdp_set_error(MDP_EUNSUPPORTED, "%u occupied patches in one state (max %d)", eng->maxA, kMaxDeg);
+    eng->deg = deg;
+    eng->variant = np * 100 + deg;
     return MDP_OK;
 }
 
-// host plan: distinct transition pairs, coefficient offsets, use descriptors
+// Host plan: distinct transition pairs (sorted by |A&B| descending for load
+// balance in k_coefs), Q offsets, the per-use pair index in forward order, and
+// the step program (runs of 1x1 transitions / general years).
 int build_plan(mdp_engine *eng, const mdp_problem *p)
 {
     eng->n = p->n;
@@ -325,10 +498,8 @@ int build_plan(mdp_engine *eng, const mdp_problem *p)
         eng->np[t] = p->year_off[t + 1] - p->year_off[t];
         eng->npmax = std::max(eng->npmax, eng->np[t]);
     }
-    int rc = select_variant(eng->npmax, &eng->variant);
-    if (rc) return rc;
     std::map<uint64_t, uint32_t> pair_index;
-    uint32_t off = 0;
+    std::vector<uint32_t> A0, B0, use0;
     for (uint32_t t = 1; t < p->tmax; ++t) {
         const uint32_t *prev = p->year_ids + p->year_off[t - 1];
         const uint32_t *cur = p->year_ids + p->year_off[t];
@@ -341,27 +512,97 @@ int build_plan(mdp_engine *eng, const mdp_problem *p)
                 auto it = pair_index.find(key);
                 uint32_t pi;
                 if (it == pair_index.end()) {
-                    pi = (uint32_t)eng->pairA.size();
+                    pi = (uint32_t)A0.size();
                     pair_index.emplace(key, pi);
-                    const uint32_t A = p->short_state[a], B = p->short_state[b];
-                    eng->pairA.push_back(A);
-                    eng->pairB.push_back(B);
-                    eng->pairOff.push_back(off);
-                    off += (uint32_t)__builtin_popcount(A & B) + 1u;
-                    if (off > kOffMask)
-                        return mdp_set_error(MDP_EUNSUPPORTED, "too many transition coefficients");
+                    A0.push_back(p->short_state[a]);
+                    B0.push_back(p->short_state[b]);
                 } else {
                     pi = it->second;
                 }
-                const uint32_t A = eng->pairA[pi], B = eng->pairB[pi];
-                const uint32_t nA = (uint32_t)__builtin_popcount(A);
-                const uint32_t nX = (uint32_t)__builtin_popcount(A & B);
-                eng->desc.push_back(eng->pairOff[pi] | (nX << kOffBits) | (nA << 27));
+                use0.push_back(pi);
+                eng->maxA = std::max(eng->maxA, (uint32_t)__builtin_popcount(p->short_state[a]));
             }
     }
+    // sort pairs by subset count (heaviest first), stable
+    std::vector<uint32_t> order(A0.size());
+    for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+        return __builtin_popcount(A0[x] & B0[x]) > __builtin_popcount(A0[y] & B0[y]);
+    });
+    std::vector<uint32_t> rank(order.size());
+    uint32_t off = 0;
+    for (uint32_t r = 0; r < order.size(); ++r) {
+        const uint32_t i = order[r];
+        rank[i] = r;
+        eng->pairA.push_back(A0[i]);
+        eng->pairB.push_back(B0[i]);
+        eng->pairOff.push_back(off);
+        off += (uint32_t)__builtin_popcount(A0[i] & B0[i]) + 1u;
+    }
+    for (uint32_t u : use0) eng->use_pair.push_back(rank[u]);
+    // k_coefs work items (pair, m), heaviest (largest C(|X|, m)) first
+    {
+        std::vector<std::pair<double, uint32_t>> w;
+        for (uint32_t pi = 0; pi < eng->pairA.size(); ++pi) {
+            const uint32_t nX = (uint32_t)__builtin_popcount(eng->pairA[pi] & eng->pairB[pi]);
+            double cnk = 1.0;
+            for (uint32_t m = 0; m <= nX; ++m) {
+                w.emplace_back(-cnk, (pi << 5) | m);
+                cnk = cnk * (double)(nX - m) / (double)(m + 1);
+            }
+        }
+        std::stable_sort(w.begin(), w.end(),
+                         [](const std::pair<double, uint32_t> &a, const std::pair<double, uint32_t> &b) {
+                             return a.first < b.first;
+                         });
+        for (auto &x : w) eng->items.push_back(x.second);
+        if (eng->pairA.size() >= (1u << 27))
+            return mdp_set_error(MDP_EUNSUPPORTED, "too many transition pairs");
+    }
     eng->npairs = (uint32_t)eng->pairA.size();
-    eng->nuses = (uint32_t)eng->desc.size();
+    eng->nuses = (uint32_t)eng->use_pair.size();
     eng->ncoef = off;
+    int rc = select_variant(eng);
+    if (rc) return rc;
+    // step program
+    for (uint32_t t = 1; t < p->tmax;) {
+        if (eng->np[t - 1] == 1 && eng->np[t] == 1) {
+            uint32_t cnt = 0;
+            while (t < p->tmax && eng->np[t - 1] == 1 && eng->np[t] == 1) {
+                ++cnt;
+                ++t;
+            }
+            eng->prog.push_back(cnt << 1);
+        } else {
+            eng->prog.push_back(1u | (eng->np[t - 1] << 8) | (eng->np[t] << 16));
+            ++t;
+        }
+    }
+    eng->prog.push_back(0u);  // pad: the forward kernel reads one word ahead
+    // k_coefs LDS plan
+    const size_t zbytes = (size_t)(eng->nvar + 1) * eng->nstates * sizeof(double);
+    const size_t qbytes = (size_t)eng->ncoef * sizeof(double);
+    if (zbytes + qbytes <= kLdsBudget) {
+        eng->lds_zpv = true;
+        eng->coef_lds = zbytes + qbytes;
+    } else if (qbytes <= kLdsBudget) {
+        eng->lds_zpv = false;
+        eng->coef_lds = qbytes;
+    } else {
+        return mdp_set_error(MDP_EUNSUPPORTED, "%u transition coefficients exceed the LDS budget",
+                             eng->ncoef);
+    }
+    return MDP_OK;
+}
+
+int upload_binomials()  // into the current device's constant bank
+{
+    double h[kMaxDeg + 1][kMaxDeg + 1] = {};
+    for (int a = 0; a <= kMaxDeg; ++a) {
+        h[a][0] = 1.0;
+        for (int b = 1; b <= a; ++b) h[a][b] = h[a][b - 1] * (double)(a - b + 1) / (double)b;
+    }
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_binom), h, sizeof(h)));
     return MDP_OK;
 }
 
@@ -369,42 +610,56 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
 {
     HIP_TRY(hipSetDevice(d.device));
     HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    std::vector<uint32_t> var(p->var_cols, p->var_cols + p->nvar), nonvar;
+    int rc = upload_binomials();
+    if (rc) return rc;
+    std::vector<uint32_t> var(p->var_cols, p->var_cols + p->nvar), row_col;
     std::vector<uint8_t> isvar(p->n, 0);
     for (uint32_t b = 0; b < p->nvar; ++b) isvar[p->var_cols[b]] = 1;
     for (uint32_t k = 0; k < p->n; ++k)
-        if (!isvar[k]) nonvar.push_back(k);
+        if (!isvar[k]) row_col.push_back(k);
+    for (uint32_t b = 0; b < p->nvar; ++b) row_col.push_back(p->var_cols[b]);
     std::vector<double> M(p->M, p->M + (size_t)p->n * p->n);
     double *dM = nullptr;
-    int rc;
     if ((rc = dev_upload(&dM, M))) return rc;
-    if ((rc = dev_upload(&d.var_cols, var)) || (rc = dev_upload(&d.nonvar, nonvar)) ||
+    if ((rc = dev_upload(&d.var_cols, var)) || (rc = dev_upload(&d.row_col, row_col)) ||
         (rc = dev_upload(&d.pairA, eng->pairA)) || (rc = dev_upload(&d.pairB, eng->pairB)) ||
-        (rc = dev_upload(&d.pairOff, eng->pairOff)) || (rc = dev_upload(&d.desc, eng->desc)) ||
-        (rc = dev_upload(&d.npy, eng->np)) ||
+        (rc = dev_upload(&d.pairOff, eng->pairOff)) || (rc = dev_upload(&d.use_pair, eng->use_pair)) ||
+        (rc = dev_upload(&d.prog, eng->prog)) || (rc = dev_upload(&d.items, eng->items)) ||
         (rc = dev_alloc(&d.S, (size_t)p->n * eng->nstates))) {
         (void)hipFree(dM);
         return rc;
     }
     dim3 grid((eng->nstates + kBlock - 1) / kBlock, p->n);
-    hipLaunchKernelGGL(k_colsum, grid, dim3(kBlock), 0, d.stream, dM, d.var_cols, p->n, p->nvar,
-                       eng->nstates, d.S);
+    hipLaunchKernelGGL(k_colsum, grid, dim3(kBlock), 0, d.stream, dM, d.var_cols, d.row_col, p->n,
+                       p->nvar, eng->nstates, d.S);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(d.stream));
     (void)hipFree(dM);
+    if (eng->coef_lds > 64 * 1024) {
+        const void *fns[] = {(const void *)k_coefs<true, 8>,   (const void *)k_coefs<true, 16>,
+                             (const void *)k_coefs<true, 24>,  (const void *)k_coefs<false, 8>,
+                             (const void *)k_coefs<false, 16>, (const void *)k_coefs<false, 24>};
+        for (const void *fn : fns)
+            HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)eng->coef_lds));
+    }
     return MDP_OK;
 }
 
 void free_device(DevCtx &d)
 {
     (void)hipSetDevice(d.device);
-    void *ptrs[] = {d.S, d.var_cols, d.nonvar, d.pairA, d.pairB, d.pairOff, d.desc, d.npy,
-                    d.e, d.c, d.Z, d.PV, d.Q, d.out};
+    void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.use_pair, d.prog, d.items,
+                    d.e, d.c, d.ZPV, d.R, d.out};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
     for (hipEvent_t ev : d.ev) (void)hipEventDestroy(ev);
     if (d.stream) (void)hipStreamDestroy(d.stream);
 }
+
+// per-c coefficient stride: every forward use plus two zero transitions of
+// prefetch padding
+size_t ldR_of(const mdp_engine *eng) { return ((size_t)eng->nuses + 2) * (eng->deg + 1); }
 
 int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const double *c,
                  uint32_t nc)
@@ -412,9 +667,8 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     HIP_TRY(hipSetDevice(d.device));
     int rc;
     if ((rc = dev_reserve(&d.e, &d.cap_e, ne)) || (rc = dev_reserve(&d.c, &d.cap_c, nc)) ||
-        (rc = dev_reserve(&d.Z, &d.cap_z, (size_t)nc * eng->nstates)) ||
-        (rc = dev_reserve(&d.PV, &d.cap_pv, (size_t)nc * eng->nvar * eng->nstates)) ||
-        (rc = dev_reserve(&d.Q, &d.cap_q, (size_t)nc * eng->ncoef)))
+        (rc = dev_reserve(&d.ZPV, &d.cap_zpv, (size_t)nc * (eng->nvar + 1) * eng->nstates)) ||
+        (rc = dev_reserve(&d.R, &d.cap_r, (size_t)nc * ldR_of(eng))))
         return rc;
     if (ne) HIP_TRY(hipMemcpy(d.e, e, ne * sizeof(double), hipMemcpyHostToDevice));
     if (nc) HIP_TRY(hipMemcpy(d.c, c, nc * sizeof(double), hipMemcpyHostToDevice));
@@ -423,19 +677,75 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     return MDP_OK;
 }
 
-int launch_forward(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
+template <int NP, int DEG, int EPL>
+void launch_fwd_epl(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
 {
-    dim3 grid(d.nc, (d.ne + kBlock - 1) / kBlock);
-    switch (eng->variant) {
-#define MDP_FWD(NP)                                                                          \
-    case NP:                                                                                 \
-        hipLaunchKernelGGL(k_forward<NP>, grid, dim3(kBlock), 0, s, d.Q, eng->ncoef, d.desc, \
-                           d.npy, eng->tmax, eng->prior0, d.e, d.ne, out, ld);               \
-        break;
-        MDP_FWD(1) MDP_FWD(2) MDP_FWD(4) MDP_FWD(8) MDP_FWD(16)
-#undef MDP_FWD
-    default:
-        return mdp_set_error(MDP_EUNSUPPORTED, "no forward kernel variant %u", eng->variant);
+    dim3 grid(d.nc, (d.ne + kBlock * EPL - 1) / (kBlock * EPL));
+    hipLaunchKernelGGL((k_forward<NP, DEG, EPL>), grid, dim3(kBlock), 0, s, d.R, ldR_of(eng), d.prog,
+                       (uint32_t)eng->prog.size() - 1, eng->np[0], eng->prior0, d.e, d.ne, out, ld);
+}
+
+template <int NP, int DEG>
+void launch_fwd(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
+{
+    if constexpr (NP <= 4 && DEG <= 8) {
+        if (eng->epl == 1) return launch_fwd_epl<NP, DEG, 1>(eng, d, out, ld, s);
+        if (eng->epl == 4) return launch_fwd_epl<NP, DEG, 4>(eng, d, out, ld, s);
+    }
+    launch_fwd_epl<NP, DEG, kEPL>(eng, d, out, ld, s);
+}
+
+template <int NP>
+int launch_fwd_deg(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
+{
+    switch (eng->deg) {
+    case 2: launch_fwd<NP, 2>(eng, d, out, ld, s); break;
+    case 4: launch_fwd<NP, 4>(eng, d, out, ld, s); break;
+    case 6: launch_fwd<NP, 6>(eng, d, out, ld, s); break;
+    case 8: launch_fwd<NP, 8>(eng, d, out, ld, s); break;
+    case 12: launch_fwd<NP, 12>(eng, d, out, ld, s); break;
+    case 16: launch_fwd<NP, 16>(eng, d, out, ld, s); break;
+    case 24: launch_fwd<NP, 24>(eng, d, out, ld, s); break;
+    default: return mdp_set_error(MDP_EUNSUPPORTED, "no forward kernel for degree %u", eng->deg);
+    }
+    return MDP_OK;
+}
+
+int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
+{
+    int rc;
+    switch (eng->variant / 100) {
+    case 1: rc = launch_fwd_deg<1>(eng, d, out, ld, s); break;
+    case 2: rc = launch_fwd_deg<2>(eng, d, out, ld, s); break;
+    case 4: rc = launch_fwd_deg<4>(eng, d, out, ld, s); break;
+    case 8: rc = launch_fwd_deg<8>(eng, d, out, ld, s); break;
+    case 16: rc = launch_fwd_deg<16>(eng, d, out, ld, s); break;
+    default: return mdp_set_error(MDP_EUNSUPPORTED, "no forward kernel variant %u", eng->variant);
+    }
+    if (rc) return rc;
+    HIP_TRY(hipGetLastError());
+    return MDP_OK;
+}
+
+template <bool LDS, int NV>
+void launch_coefs_nv(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
+{
+    hipLaunchKernelGGL((k_coefs<LDS, NV>), dim3(d.nc), dim3(kBlock), eng->coef_lds, s, d.ZPV,
+                       eng->nstates, eng->nvar, d.pairA, d.pairB, d.pairOff, d.items,
+                       (uint32_t)eng->items.size(), d.use_pair, eng->nuses, eng->deg, d.R, ldR_of(eng));
+}
+
+int launch_coefs(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
+{
+    const uint32_t nv = eng->nvar;
+    if (eng->lds_zpv) {
+        if (nv <= 8) launch_coefs_nv<true, 8>(eng, d, s);
+        else if (nv <= 16) launch_coefs_nv<true, 16>(eng, d, s);
+        else launch_coefs_nv<true, 24>(eng, d, s);
+    } else {
+        if (nv <= 8) launch_coefs_nv<false, 8>(eng, d, s);
+        else if (nv <= 16) launch_coefs_nv<false, 16>(eng, d, s);
+        else launch_coefs_nv<false, 24>(eng, d, s);
     }
     HIP_TRY(hipGetLastError());
     return MDP_OK;
@@ -445,7 +755,7 @@ int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
 {
     HIP_TRY(hipSetDevice(d.device));
     if (d.ne == 0 || d.nc == 0) return MDP_OK;
-    if (d.ne > 65535u * kBlock || d.nc > 0x7fffffffu)
+    if ((d.ne + kBlock - 1) / kBlock > 65535u || d.nc > 0x7fffffffu)
         return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
     const bool prof = eng->profiling != 0;
     hipEvent_t *ev = nullptr;
@@ -462,17 +772,15 @@ int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
         HIP_TRY(hipEventRecord(ev[kEvBegin], s));
     }
     {
-        dim3 grid((eng->nstates + kBlock - 1) / kBlock, (d.nc + kColTile - 1) / kColTile);
-        hipLaunchKernelGGL(k_coltables, grid, dim3(kBlock), 0, s, d.S, eng->nstates, d.nonvar,
-                           eng->n - eng->nvar, d.var_cols, eng->nvar, d.c, d.nc, d.Z, d.PV);
+        dim3 grid((eng->nstates + kZpvJ - 1) / kZpvJ, (d.nc + kZpvCT - 1) / kZpvCT);
+        hipLaunchKernelGGL(k_zpv, grid, dim3(kBlock), 0, s, d.S, eng->nstates, eng->n - eng->nvar,
+                           eng->nvar, d.c, d.nc, d.ZPV);
         HIP_TRY(hipGetLastError());
     }
-    if (prof) HIP_TRY(hipEventRecord(ev[kEvColTables], s));
-    if (eng->npairs) {
-        dim3 grid((eng->npairs + kBlock - 1) / kBlock, d.nc);
-        hipLaunchKernelGGL(k_coefs, grid, dim3(kBlock), 0, s, d.pairA, d.pairB, d.pairOff,
-                           eng->npairs, eng->nvar, eng->nstates, d.Z, d.PV, eng->ncoef, d.Q);
-        HIP_TRY(hipGetLastError());
+    if (prof) HIP_TRY(hipEventRecord(ev[kEvZpv], s));
+    if (eng->nuses) {
+        int rc = launch_coefs(eng, d, s);
+        if (rc) return rc;
     }
     if (prof) HIP_TRY(hipEventRecord(ev[kEvCoefs], s));
     int rc = launch_forward(eng, d, out, ld, s);
@@ -521,6 +829,10 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
     if (rc) {
         delete eng;
         return rc;
+    }
+    if (const char *ev = getenv("MDP_EPL")) {
+        const int v = atoi(ev);
+        if (v == 1 || v == 2 || v == 4) eng->epl = v;
     }
     std::vector<int> ids;
     if (n_devices == 0) {
@@ -649,16 +961,12 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
 {
     if (!eng) return mdp_set_error(MDP_EINVAL, "null engine");
     const double pts = (double)ne * (double)nc;
-    // implemented form, per point: each use costs a (nX+1)-term dot product
-    // (2(nX+1) flops), the (|A|-nX) x-power multiplies, and one FMA into v;
-    // plus the final prior sum.
-    double per_pt = 0;
-    for (uint32_t u = 0; u < eng->nuses; ++u) {
-        const uint32_t dsc = eng->desc[u];
-        const double nX = (double)((dsc >> kOffBits) & 31u), nA = (double)(dsc >> 27);
-        per_pt += 2.0 * (nX + 1.0) + (nA - nX) + 2.0;
-    }
-    per_pt += 2.0 * eng->np[eng->tmax - 1];
+    // k_forward per point: every use is a (D+1)-term dot product (2(D+1)
+    // flops) and one multiply-add into the state vector (2), plus the
+    // (D+1)-term weight setup and the final prior sum.
+    const double D = (double)eng->deg;
+    double per_pt = (double)eng->nuses * (2.0 * (D + 1.0) + 2.0) + 3.0 * (D + 1.0) +
+                    2.0 * (double)eng->npmax;
     if (flop_impl) *flop_impl = per_pt * pts;
     // SURVEY.md §8(d) F_alg (dense-in-j formulation)
     double fwd = 0;
@@ -666,8 +974,9 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     const double falg = 2.0 * eng->n * eng->nstates + (double)eng->nvar * eng->nstates * eng->nextid +
                         2.0 * eng->nstates * eng->npairs + 2.0 * eng->np[0] * fwd;
     if (flop_survey) *flop_survey = falg * pts;
-    // compulsory HBM bytes: per-c coefficient blocks + e values + outputs
-    if (bytes_min) *bytes_min = 8.0 * ((double)nc * eng->ncoef + (double)ne + pts);
+    // compulsory bytes of k_forward: its coefficient stream once per c, the
+    // e values, the output
+    if (bytes_min) *bytes_min = 8.0 * ((double)nc * ldR_of(eng) + (double)ne + pts);
     return MDP_OK;
 }
 
