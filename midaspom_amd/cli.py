@@ -1,0 +1,138 @@
+"""`python -m midaspom_amd` -- the MIDASPOM command line over the GPU engine.
+
+Single process: the same flags, defaults, stdout lines and posterior file as
+bin_linux/MIDASPOM.out (sources/main_MIDASPOM.c:61-439); the compiled drop-in
+is midaspom_amd/_build/midaspom.
+
+Under torchrun (WORLD_SIZE > 1, one process per GPU): the drop-in for
+`mpirun -np N MIDASPOM_MPI.out` -- e-row slabs per rank and one gather to
+rank 0 over RCCL (sources/main_MIDASPOM_MPI.c:361-368, 482-506), including
+that program's extra stdout lines (nextid per rank :301, per-process start /
+end lines :356, :479, send / gather lines :489-507) and its raw-loglik output
+when Ltot == 0 (:527).
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+import time
+
+
+def parse_args(argv):
+    # getopt "m:p:d:i:o:s:l:u:" (:79); code defaults (:66-73), not the manual's
+    ap = argparse.ArgumentParser(prog="midaspom", add_help=True)
+    ap.add_argument("-m", type=float, default=400.0, help="mean dispersal distance")
+    ap.add_argument("-p", type=float, default=0.5, help="prior occupancy of missing year-0 patches")
+    ap.add_argument("-d", type=float, default=100.0, help="segment length")
+    ap.add_argument("-i", default="input.txt", help="occupancy file")
+    ap.add_argument("-o", default="posterior.txt", help="posterior output file")
+    ap.add_argument("-s", type=int, default=101, help="grid steps")
+    ap.add_argument("-l", type=float, default=0.0, help="lower bound")
+    ap.add_argument("-u", type=float, default=1.0, help="upper bound")
+    ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl)")
+    return ap.parse_args(argv)
+
+
+def _print_problem(model, out):
+    pb = model
+    out(f"Number of habitat patches: {pb.n}\nNumber of sampled years: {pb.tmax}\n")
+    out("Dispersal matrix:\n")
+    M = pb.M
+    for i in range(pb.n):
+        out("".join(f"{M[i, j]:.3f} " for j in range(pb.n)) + "\n")
+    out("Input occupancy data:\n")
+    obs = pb.obs
+    for t in range(pb.tmax):
+        out(f"Year {t}: " + "".join(f"{v} " for v in obs[t]) + "\n")
+    out("Number of possible states per year:\n")
+    for t, k in enumerate(pb.npstates):
+        out(f"Year {t}: {k}\n")
+    out(f"Number of states to compute: {pb.nstates}\n")
+
+
+def main(argv=None) -> int:
+    import numpy as np
+
+    import midaspom_amd as mdp
+    from midaspom_amd import dist as mdist
+
+    a = parse_args(sys.argv[1:] if argv is None else argv)
+    rank, world, local = mdist.env_rank_world()
+    root = rank == 0
+
+    def out(text, all_ranks=False):
+        if root or all_ranks:
+            sys.stdout.write(text)
+            sys.stdout.flush()
+
+    if world > 1:
+        out("------ MIDASPOM, beta MPI version ------\n-> N. Alcala, E. M. Cole, and N. A. Rosenberg <-\n")
+    else:
+        out("------ MIDASPOM, beta version ------\n-> N. Alcala, E. M. Cole, and N. A. Rosenberg <-\n")
+    if a.s < 2:
+        sys.stderr.write("midaspom: -s must be at least 2\n")
+        return 1
+    g, win = mdp.grid(a.s, a.l, a.u)
+    out(f"Parameters for numerical approximation of the posterior density:\n\tWindow size={win:f}, "
+        f"number of steps={a.s}\n")
+    out(f"Reading observations from file {a.i}... ")
+    try:
+        model = mdp.Model.load(a.i, m=a.m, p=a.p, d=a.d)
+    except mdp.MidaspomError as exc:
+        sys.stderr.write(f"\nmidaspom: {exc}\n")
+        return 2
+    out("done\n")
+    _print_problem(model, out)
+    start = time.time()
+
+    if world == 1:
+        out("Starting parallel likelihood computation\n")
+        with mdp.Engine(model) as eng:
+            lik = eng.loglik_grid(g, g)
+        for ie in range(a.s):  # ((float)ie+1)*100.0/nstep, exact in double (:394)
+            out(f"{(ie + 1) * 100.0 / a.s:.2f}% done\n")
+        out("end likelihood computation\n")
+    else:
+        import torch
+        import torch.distributed as dist
+
+        backend = a.backend or "nccl"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            compute = mdist.gpu_slab_compute(model, local)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend)
+            compute = mdist.gpu_slab_compute(model, local)
+        out(f"nextid={model.nextid}\n", all_ranks=True)
+        out(f"Starting parallel likelihood computation process {rank + 1}/{world}\n", all_ranks=True)
+        r0, r1 = mdist.row_slab(rank, world, a.s)
+        local_lik = compute(g[r0:r1], g)
+        for ie in range(r0, r1):  # main_MIDASPOM_MPI.c:463
+            out(f"{(ie + 1 - r0) * 100.0 / (r1 - r0):.2f}% done\n")
+        out(f"end likelihood computation process {rank + 1}/{world}\n", all_ranks=True)
+        if not root:
+            out(f"Sending data (proc {rank})... ", all_ranks=True)
+        else:
+            out(f"Gathering data from {world - 1} proc... ")
+        lik = mdist.gather_rows(local_lik, rank, world, a.s, a.s,
+                                device=None if backend == "nccl" else "cpu")
+        out("done\n", all_ranks=True)
+        compute.engine.close()
+        dist.destroy_process_group()
+        if not root:
+            return 0
+
+    ltot = mdp.log_total(lik, win)
+    out(f"Total log-likelihood={ltot:.5f}\n")
+    out(f"Writing output in file {a.o}... ")
+    # the MPI build writes raw log-likelihoods when Ltot == 0 (:527)
+    mdp.write_posterior(a.o, lik, ltot, raw=(world > 1 and ltot == 0))
+    elapsed = int(time.time()) - int(start)
+    out(f"done\n Total running time: {elapsed / 60.0:.2f} min\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

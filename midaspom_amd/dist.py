@@ -1,0 +1,86 @@
+"""One process per GPU: e-row slabs + a single gather (the MIDASPOM_MPI.out
+decomposition, sources/main_MIDASPOM_MPI.c:361-368 and :482-506).
+
+Rank r computes rows [r0, r1) of the s x s log-likelihood grid on its own
+GPU; the slabs meet on rank 0 in ONE collective (torch.distributed gather:
+RCCL over xGMI with the "nccl" backend, gloo on CPU), padded to equal size
+because collectives move equal-sized buffers.  Rank 0 normalises and writes.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional
+
+import numpy as np
+
+
+def row_slab(rank: int, world: int, s: int):
+    """[r0, r1) rows of rank `rank`: floor(s/N) each, the remainder on rank 0
+    (main_MIDASPOM_MPI.c:361-368)."""
+    avg, rem = divmod(s, world)
+    if rank == 0:
+        return 0, avg + rem
+    return rank * avg + rem, (rank + 1) * avg + rem
+
+
+def gather_rows(local, rank: int, world: int, s: int, nc: int, device=None):
+    """Gather every rank's row slab (torch tensor [rows, nc], float64) to rank
+    0 in one collective.  Returns the full [s, nc] numpy grid on rank 0, None
+    elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    avg, rem = divmod(s, world)
+    cap = avg + rem  # the largest slab (rank 0's)
+    dev = local.device if device is None else device
+    buf = torch.zeros((cap, nc), dtype=torch.float64, device=dev)
+    buf[: local.shape[0]] = local
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, parts, dst=0)
+    if rank != 0:
+        return None
+    full = np.empty((s, nc), dtype=np.float64)
+    for r in range(world):
+        r0, r1 = row_slab(r, world, s)
+        full[r0:r1] = parts[r][: r1 - r0].cpu().numpy()
+    return full
+
+
+def distributed_loglik(e, c, rank: int, world: int,
+                       compute: Callable[[np.ndarray, np.ndarray], object], device=None):
+    """Each rank computes its slab with `compute(e_slab, c)` (a torch tensor
+    or numpy array [rows, nc]) and the slabs are gathered to rank 0."""
+    import torch
+
+    r0, r1 = row_slab(rank, world, len(e))
+    local = compute(np.ascontiguousarray(e[r0:r1]), np.ascontiguousarray(c))
+    if not torch.is_tensor(local):
+        local = torch.from_numpy(np.asarray(local, dtype=np.float64))
+    if device is not None:
+        local = local.to(device)
+    return gather_rows(local, rank, world, len(e), len(c), device)
+
+
+def env_rank_world():
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), \
+        int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def gpu_slab_compute(model, device_index: int):
+    """compute(e_slab, c) on this rank's GPU through the C ABI; the result
+    stays in HBM (a torch tensor) until the gather."""
+    import torch
+
+    import midaspom_amd as mdp
+
+    eng = mdp.Engine(model, devices=[device_index])
+
+    def compute(e_slab, c):
+        out = torch.empty((len(e_slab), len(c)), dtype=torch.float64, device=f"cuda:{device_index}")
+        if len(e_slab):
+            eng.set_grid(e_slab, c)
+            eng.run(out.data_ptr(), len(c), torch.cuda.current_stream(device_index).cuda_stream)
+        return out
+
+    compute.engine = eng
+    return compute
