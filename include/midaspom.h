@@ -131,6 +131,11 @@ int mdp_engine_set_profiling(mdp_engine *engine, int enable);
 int mdp_engine_kernel_ms(mdp_engine *engine, double *ms, int max_k);
 const char *mdp_engine_kernel_name(int k);
 
+/* Diagnostics (MDP_DIAG=1 in the environment at engine creation): text
+ * report of per-workgroup s_memtime phase durations (shader cycles) of the
+ * last run's kernels; returns the report length (0 when disabled). */
+int mdp_engine_diag_report(mdp_engine *engine, char *buf, size_t len);
+
 /* Work accounting of one run on a grid of ne x nc points (host arithmetic on
  * the enumerated problem): flops of the forward kernel in
  * the implemented factorised form, and the SURVEY.md §8(d) dense-form F_alg. */

@@ -184,6 +184,12 @@ class Engine:
         k = check(lib().mdp_engine_kernel_ms(self._h, buf, 8))
         return {lib().mdp_engine_kernel_name(i).decode(): buf[i] for i in range(k)}
 
+    def diag_report(self) -> str:
+        """Phase-stamp report of the last run (engine created with MDP_DIAG=1)."""
+        buf = ctypes.create_string_buffer(8192)
+        check(lib().mdp_engine_diag_report(self._h, buf, len(buf)))
+        return buf.value.decode()
+
     def info(self) -> dict:
         inf = _lib.EngineInfo()
         check(lib().mdp_engine_get_info(self._h, ctypes.byref(inf)))

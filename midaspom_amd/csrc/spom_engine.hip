@@ -36,9 +36,11 @@
 #include <cstring>
 #include <map>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "mdp_internal.h"
+#include "spom_jit.h"
 
 namespace {
 
@@ -49,10 +51,34 @@ constexpr int kZpvCT = 2;       // k_zpv: c values per thread
 constexpr int kZpvUnroll = 8;   // k_zpv: S loads in flight per lane
 constexpr int kEPL = 2;         // k_forward: default grid points (e values) per lane
 constexpr int kMaxDeg = 24;
+constexpr int kStampSlots = 8;      // diagnostic stamps per workgroup
+constexpr uint32_t kSubPart = 16;   // k_coefs: subsets per work part
+constexpr uint32_t kOffBits = 22;   // coefficient offset bits in a use descriptor
+constexpr uint32_t kOffMask = (1u << kOffBits) - 1u;
 constexpr unsigned kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), other counters untouched
 constexpr size_t kLdsBudget = 120 * 1024;  // dynamic LDS of k_coefs
+constexpr size_t kFwdLds = 48 * 1024;      // max coefficient block staged by k_forward_lds
+constexpr uint32_t kJitMaxUses = 2048;     // larger programs use the generic kernels
+constexpr size_t kJitMaxLds = 48 * 1024;
 
 __constant__ double c_binom[kMaxDeg + 1][kMaxDeg + 1];
+
+// Diagnostic phase stamps (MDP_DIAG=1): wave 0 of every workgroup records
+// s_memtime at phase boundaries into stamps[block][slot]; a null pointer (the
+// default) skips them with one scalar branch.
+#define MDP_STAMP(stamps, slot)                                                           \
+    do {                                                                                  \
+        if ((stamps) && threadIdx.x == 0)                                                 \
+            (stamps)[(size_t)(blockIdx.x + gridDim.x * blockIdx.y) * kStampSlots + (slot)] = \
+                __builtin_amdgcn_s_memtime();                                             \
+    } while (0)
+// wall-clock stamps (s_memrealtime, 100 MHz, chip-wide) in the last two slots
+#define MDP_RSTAMP(stamps, slot)                                                          \
+    do {                                                                                  \
+        if ((stamps) && threadIdx.x == 0)                                                 \
+            (stamps)[(size_t)(blockIdx.x + gridDim.x * blockIdx.y) * kStampSlots + (slot)] = \
+                __builtin_amdgcn_s_memrealtime();                                         \
+    } while (0)
 
 #define HIP_TRY(expr)                                                                     \
     do {                                                                                  \
@@ -96,9 +122,12 @@ __global__ __launch_bounds__(kBlock) void k_colsum(const double *__restrict__ M,
 // multiplied in slice order through LDS.
 __global__ __launch_bounds__(kBlock) void k_zpv(
     const double *__restrict__ S2, uint32_t nstates, uint32_t nnv, uint32_t nvar,
-    const double *__restrict__ cvals, uint32_t nc, double *__restrict__ ZPV)
+    const double *__restrict__ cvals, uint32_t nc, double *__restrict__ ZPV,
+    unsigned long long *__restrict__ stamps)
 {
     __shared__ double part[kZpvSlices][kZpvCT][kZpvJ];
+    MDP_RSTAMP(stamps, 6);
+    MDP_STAMP(stamps, 0);
     const uint32_t lane = threadIdx.x % kZpvJ, slice = threadIdx.x / kZpvJ;
     const uint32_t j = blockIdx.x * kZpvJ + lane;
     const uint32_t c0 = blockIdx.y * kZpvCT;
@@ -118,11 +147,19 @@ __global__ __launch_bounds__(kBlock) void k_zpv(
 #pragma unroll
         for (int u = 0; u < kZpvUnroll; ++u) sv[u] = S2[(size_t)(q + u) * nstates + jj];
 #pragma unroll
-        for (int u = 0; u < kZpvUnroll; ++u)
+        for (int t = 0; t < kZpvCT; ++t) {
+            // 1 - min(1, c s), evaluated as max(0, 1 - c s) with one rounding;
+            // the batch is multiplied as a tree so only one multiply per
+            // batch sits on the dependency chain
+            double f[kZpvUnroll];
 #pragma unroll
-            for (int t = 0; t < kZpvCT; ++t)
-                // 1 - min(1, c s), evaluated as max(0, 1 - c s) with one rounding
-                z[t] *= fmax(0.0, fma(-c[t], sv[u], 1.0));
+            for (int u = 0; u < kZpvUnroll; ++u) f[u] = fmax(0.0, fma(-c[t], sv[u], 1.0));
+#pragma unroll
+            for (int w = 1; w < kZpvUnroll; w *= 2)
+#pragma unroll
+                for (int u = 0; u + w < kZpvUnroll; u += 2 * w) f[u] *= f[u + w];
+            z[t] *= f[0];
+        }
     }
     for (; q < q1; ++q) {
         const double s0 = S2[(size_t)q * nstates + jj];
@@ -131,6 +168,7 @@ __global__ __launch_bounds__(kBlock) void k_zpv(
     }
 #pragma unroll
     for (int t = 0; t < kZpvCT; ++t) part[slice][t][lane] = z[t];
+    MDP_STAMP(stamps, 1);
     __syncthreads();
     const size_t rows = (size_t)nvar + 1;
     if (slice == 0 && ok) {
@@ -152,92 +190,135 @@ __global__ __launch_bounds__(kBlock) void k_zpv(
                     ZPV[((size_t)(c0 + t) * rows + 1 + b) * nstates + j] = pc > 1.0 ? 1.0 : pc;
                 }
         }
+    MDP_STAMP(stamps, 2);
+    MDP_RSTAMP(stamps, 7);
 }
 
 // One workgroup per c value.
-//  1. (LDS_ZPV) stage this c's Z/PV block in LDS;
-//  2. lanes over transition pairs: Q_ab[m] = sum over subsets j of A&B with
-//     |j| = m of Z_j * prod_{var b not in j} (B_b ? pC : 1-pC)  (subsets
-//     enumerated once, accumulated per popcount in LDS);
-//  3. lanes over (use, r): R[c][use][r] = sum_m Q[m] C(D-|A|, r-m).
-template <bool LDS_ZPV, int NV>
+//  1. stage this c's Z/PV block (LDS_ZPV) and the binomial table in LDS;
+//  2. subset products: lane per part (pair p, 16 consecutive subset indexes k
+//     of X = A&B): j = deposit(k, X), Pc[j][b] = Z_j prod_{var b not in j}
+//     (B_b ? pC : 1-pC) accumulated into the part's per-|j| partial sums;
+//  3. Q_ab[m] = sum of the pair's part partials, in part order;
+//  4. lane per forward use: R[c][use][r] = sum_m Q[m] C(D-|A|, r-m), padded
+//     to the even stride RSP, plus two zero transitions of prefetch padding.
+// Every reduction runs in a fixed order, so results are deterministic.
+template <bool LDS_ZPV, bool LDS_PART, int NV>
 __global__ __launch_bounds__(kBlock) void k_coefs(
     const double *__restrict__ ZPV, uint32_t nstates, uint32_t nvar,
     const uint32_t *__restrict__ pairA, const uint32_t *__restrict__ pairB,
-    const uint32_t *__restrict__ pairOff, const uint32_t *__restrict__ items, uint32_t nitems,
-    const uint32_t *__restrict__ use_pair, uint32_t nuses, uint32_t deg,
-    double *__restrict__ R, size_t ldR)
+    const uint32_t *__restrict__ pairOff, const uint32_t *__restrict__ pairPart0,
+    uint32_t npairs, const uint32_t *__restrict__ partP, const uint32_t *__restrict__ partK0,
+    uint32_t nparts, uint32_t ncoef, const uint32_t *__restrict__ udesc, uint32_t nuses,
+    uint32_t deg, double *__restrict__ R, size_t ldR, double *__restrict__ gpart,
+    unsigned long long *__restrict__ stamps)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    MDP_RSTAMP(stamps, 6);
+    MDP_STAMP(stamps, 0);
     const uint32_t ic = blockIdx.x;
     const size_t zsz = (size_t)(nvar + 1) * nstates;
     const double *zg = ZPV + (size_t)ic * zsz;
-    const double *zpv;
-    double *Qs;
+    double *base = lds;
+    const double *zpv = zg;
     if constexpr (LDS_ZPV) {
-        for (size_t i = threadIdx.x; i < zsz; i += kBlock) lds[i] = zg[i];
-        zpv = lds;
-        Qs = lds + zsz;
-    } else {
-        zpv = zg;
-        Qs = lds;
-    }
-    __syncthreads();
-    // one lane per coefficient item (pair p, popcount m): sum over the
-    // C(|X|, m) subsets j of X = A&B with |j| = m (Gosper's sequence of
-    // m-bit patterns over the |X| positions, deposited into X)
-    for (uint32_t it = threadIdx.x; it < nitems; it += kBlock) {
-        const uint32_t w = items[it];
-        const uint32_t p = w >> 5, m = w & 31u;
-        const uint32_t A = pairA[p], B = pairB[p], X = A & B;
-        const uint32_t nX = __popc(X);
-        double acc = 0.0;
-        uint32_t pat = m ? ((1u << m) - 1u) : 0u;
-        const uint32_t lim = 1u << nX;
-        while (pat < lim) {
-            uint32_t sub = 0, xs = X, bits = pat;
-            while (bits) {
-                const uint32_t low = xs & (0u - xs);
-                if (bits & 1u) sub |= low;
-                xs ^= low;
-                bits >>= 1;
+        for (size_t i0 = 0; i0 < zsz; i0 += 8 * kBlock) {  // 8 loads in flight per lane
+            double t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const size_t i = i0 + u * kBlock + threadIdx.x;
+                if (i < zsz) t[u] = zg[i];
             }
-            // branch-free: every factor load is issued up front; bits of j
-            // contribute an exact 1.0
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const size_t i = i0 + u * kBlock + threadIdx.x;
+                if (i < zsz) lds[i] = t[u];
+            }
+        }
+        zpv = lds;
+        base = lds + zsz;
+    }
+    const uint32_t pw = nvar + 1;  // partial sums per part
+    double *partial = LDS_PART ? base : gpart + (size_t)ic * nparts * pw;
+    double *Qs = LDS_PART ? base + (size_t)nparts * pw : base;
+    double *binom = Qs + ncoef;  // [kMaxDeg+1][kMaxDeg+1]
+    for (uint32_t i = threadIdx.x; i < (kMaxDeg + 1) * (kMaxDeg + 1); i += kBlock)
+        binom[i] = c_binom[i / (kMaxDeg + 1)][i % (kMaxDeg + 1)];
+    __syncthreads();
+    MDP_STAMP(stamps, 1);
+
+    for (uint32_t it = threadIdx.x; it < nparts; it += kBlock) {
+        const uint32_t p = partP[it], k0 = partK0[it];
+        const uint32_t B = pairB[p], X = pairA[p] & B;
+        const uint32_t nX = __popc(X);
+        double *acc = partial + (size_t)it * pw;
+        for (uint32_t m = 0; m <= nX; ++m) acc[m] = 0.0;
+        const uint32_t k1 = min(k0 + kSubPart, 1u << nX);
+        for (uint32_t k = k0; k < k1; ++k) {
+            // deposit the bits of k into the positions of X (once X's bits are
+            // used up `low` is 0 and the remaining steps are no-ops)
+            uint32_t sub = 0, xs = X;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const uint32_t low = xs & (0u - xs);
+                sub |= ((k >> i) & 1u) ? low : 0u;
+                xs ^= low;
+            }
+            // branch-free: every factor load is issued up front (rows past
+            // nvar are clamped and neutralised); bits of j contribute 1.0
+            double f[NV];
+#pragma unroll
+            for (int b = 0; b < NV; ++b) {
+                const uint32_t row = (uint32_t)b < nvar ? (uint32_t)b : nvar - 1;
+                f[b] = zpv[(size_t)(1 + row) * nstates + sub];
+            }
             double prod = zpv[sub];
 #pragma unroll
             for (int b = 0; b < NV; ++b) {
-                if ((uint32_t)b < nvar) {
-                    const uint32_t bit = nvar - 1 - b;
-                    const double f = zpv[(size_t)(1 + b) * nstates + sub];
-                    const double g = ((B >> bit) & 1u) ? f : 1.0 - f;
-                    prod *= ((sub >> bit) & 1u) ? 1.0 : g;
-                }
+                const uint32_t bit = nvar - 1 - (uint32_t)b;  // wraps past nvar: masked below
+                const double g = ((B >> bit) & 1u) ? f[b] : 1.0 - f[b];
+                const bool skip = (uint32_t)b >= nvar || ((sub >> bit) & 1u);
+                prod *= skip ? 1.0 : g;
             }
-            acc += prod;
-            if (pat == 0) break;
-            const uint32_t t = pat | (pat - 1u);  // next pattern with the same popcount
-            pat = (t + 1u) | (((~t & (0u - ~t)) - 1u) >> (__ffs(pat) ));
+            acc[__popc(k)] += prod;
         }
-        Qs[pairOff[p] + m] = acc;
     }
     __syncthreads();
-    const uint32_t rs = deg + 1;
-    double *Rc = R + (size_t)ic * ldR;
-    for (uint32_t it = nuses * rs + threadIdx.x; it < (nuses + 2) * rs; it += kBlock) Rc[it] = 0.0;
-    for (uint32_t it = threadIdx.x; it < nuses * rs; it += kBlock) {
-        const uint32_t u = it / rs, r = it - u * rs;
-        const uint32_t p = use_pair[u];
-        const uint32_t A = pairA[p];
-        const uint32_t nA = __popc(A), nX = __popc(A & pairB[p]);
-        const uint32_t lift = deg - nA;
-        const double *q = Qs + pairOff[p];
-        double acc = 0.0;
-        const uint32_t m0 = r > lift ? r - lift : 0;
-        const uint32_t m1 = r < nX ? r : nX;
-        for (uint32_t m = m0; m <= m1; ++m) acc += q[m] * c_binom[lift][r - m];
-        Rc[it] = acc;
+    MDP_STAMP(stamps, 2);
+    for (uint32_t p = threadIdx.x; p < npairs; p += kBlock) {
+        const uint32_t nX = __popc(pairA[p] & pairB[p]);
+        const uint32_t q0 = pairPart0[p], q1 = pairPart0[p + 1];
+        double *q = Qs + pairOff[p];
+        for (uint32_t m = 0; m <= nX; ++m) {
+            double a = 0.0;
+            for (uint32_t t = q0; t < q1; ++t) a += partial[(size_t)t * pw + m];
+            q[m] = a;
+        }
     }
+    __syncthreads();
+    MDP_STAMP(stamps, 3);
+    const uint32_t rsp = (deg + 2) & ~1u;
+    double *Rc = R + (size_t)ic * ldR;
+    for (uint32_t it = nuses * rsp + threadIdx.x; it < (nuses + 2) * rsp; it += kBlock) Rc[it] = 0.0;
+    for (uint32_t u = threadIdx.x; u < nuses; u += kBlock) {
+        const uint32_t d = udesc[u];
+        const double *q = Qs + (d & kOffMask);
+        const uint32_t nX = (d >> kOffBits) & 31u, nA = d >> 27;
+        const uint32_t lift = deg - nA;
+        const double *bl = binom + lift * (kMaxDeg + 1);
+        double *dst = Rc + (size_t)u * rsp;
+        for (uint32_t r = 0; r < rsp; ++r) {
+            double a = 0.0;
+            if (r <= deg) {
+                const uint32_t m0 = r > lift ? r - lift : 0;
+                const uint32_t m1 = r < nX ? r : nX;
+                for (uint32_t m = m0; m <= m1; ++m) a += q[m] * bl[r - m];
+            }
+            dst[r] = a;
+        }
+    }
+    MDP_STAMP(stamps, 4);
+    MDP_RSTAMP(stamps, 7);
 }
 
 // Dot product of one transition's coefficients (wave-uniform, SGPRs) with a
@@ -267,6 +348,20 @@ __device__ __forceinline__ void tload(double (&dst)[RS], cdouble *src)
     for (int r = 0; r < RS; ++r) dst[r] = src[r];
 }
 
+// RS coefficients from a 16-byte aligned LDS block (ds_read_b128 pairs).
+template <int RS>
+__device__ __forceinline__ void tload_l(double (&dst)[RS], const double *src)
+{
+    const double2 *s2 = (const double2 *)src;
+#pragma unroll
+    for (int r = 0; r + 1 < RS; r += 2) {
+        const double2 q = s2[r / 2];
+        dst[r] = q.x;
+        dst[r + 1] = q.y;
+    }
+    if constexpr (RS & 1) dst[RS - 1] = src[RS - 1];
+}
+
 // Forward recursion, EPL grid points per lane (e values ie, ie+256, ...), one
 // c per workgroup.  Program `prog` (padded with one trailing word): one word
 // per step, either a run of `count` consecutive 1x1 transitions (v0 *= P) or
@@ -281,6 +376,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(
     double *__restrict__ out, uint32_t ld_out)
 {
     constexpr int RS = DEG + 1;
+    constexpr int RSP = (DEG + 2) & ~1;  // per-transition stride in R
     const uint32_t ic = blockIdx.x;
     uint32_t ie[EPL];
     double W[EPL][RS];
@@ -322,7 +418,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(
                 double P[EPL];
                 __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
                 __builtin_amdgcn_sched_barrier(0);
-                tload(r1, rp + RS);
+                tload(r1, rp + RSP);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < EPL; ++i) P[i] = tdot(r0, W[i]);
@@ -330,18 +426,18 @@ __global__ __launch_bounds__(kBlock) void k_forward(
                 for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * P[i];
                 __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
                 __builtin_amdgcn_sched_barrier(0);
-                tload(r0, rp + 2 * RS);
+                tload(r0, rp + 2 * RSP);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < EPL; ++i) P[i] = tdot(r1, W[i]);
 #pragma unroll
                 for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * P[i];
-                rp += 2 * RS;
+                rp += 2 * RSP;
             }
             if (cnt) {
 #pragma unroll
                 for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * tdot(r0, W[i]);
-                rp += RS;
+                rp += RSP;
             }
         } else {
             const uint32_t npp = (op >> 8) & 0xffu, npc = (op >> 16) & 0xffu;
@@ -356,7 +452,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(
                         if ((uint32_t)k < npp) {
                             double rc[RS];
                             tload(rc, rp);
-                            rp += RS;
+                            rp += RSP;
 #pragma unroll
                             for (int i = 0; i < EPL; ++i) vn[i][l] = fma(v[i][k], tdot(rc, W[i]), vn[i][l]);
                         }
@@ -379,6 +475,136 @@ __global__ __launch_bounds__(kBlock) void k_forward(
         for (int l = 0; l < NPMAX; ++l) L += v[i][l] * prior0;
         if (ie[i] < ne) out[(size_t)ie[i] * ld_out + ic] = log(L);
     }
+}
+
+
+
+// Same recursion with the workgroup's whole coefficient block (and the step
+// program) staged in LDS by wide coalesced loads: transitions are then read
+// with in-order ds_read_b128 broadcasts instead of scalar loads, so there is no
+// scalar-cache miss on the critical path.  Used when the block fits kFwdLds.
+template <int NPMAX, int DEG, int EPL>
+__global__ __launch_bounds__(kBlock) void k_forward_lds(
+    const double *__restrict__ R, size_t ldR, const uint32_t *__restrict__ prog, uint32_t nprog,
+    uint32_t np0, double prior0, const double *__restrict__ evals, uint32_t ne,
+    double *__restrict__ out, uint32_t ld_out, unsigned long long *__restrict__ stamps)
+{
+    constexpr int RS = DEG + 1;
+    constexpr int RSP = (DEG + 2) & ~1;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    MDP_RSTAMP(stamps, 6);
+    MDP_STAMP(stamps, 0);
+    double *Rl = lds;
+    uint32_t *pl = (uint32_t *)(lds + ldR);
+    const uint32_t ic = blockIdx.x;
+    {
+        const double2 *src = (const double2 *)(R + (size_t)ic * ldR);
+        double2 *dst = (double2 *)Rl;
+        const uint32_t n2 = (uint32_t)(ldR / 2);
+        for (uint32_t i0 = threadIdx.x; i0 < n2; i0 += 4 * kBlock) {  // 4 loads in flight per lane
+            const uint32_t i1 = i0 + kBlock, i2 = i0 + 2 * kBlock, i3 = i0 + 3 * kBlock;
+            const double2 t0 = src[i0];
+            const double2 t1 = src[i1 < n2 ? i1 : i0];
+            const double2 t2 = src[i2 < n2 ? i2 : i0];
+            const double2 t3 = src[i3 < n2 ? i3 : i0];
+            dst[i0] = t0;
+            if (i1 < n2) dst[i1] = t1;
+            if (i2 < n2) dst[i2] = t2;
+            if (i3 < n2) dst[i3] = t3;
+        }
+        for (uint32_t i = threadIdx.x; i <= nprog; i += kBlock) pl[i] = prog[i];
+    }
+    uint32_t ie[EPL];
+    double W[EPL][RS];
+    double v[EPL][NPMAX];
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+        ie[i] = blockIdx.y * (kBlock * EPL) + i * kBlock + threadIdx.x;
+        const double e = ie[i] < ne ? evals[ie[i]] : 0.0;
+        const double x = e > 1.0 ? 1.0 : e;
+        const double y = 1.0 - x;
+        double yp[RS];
+        yp[0] = 1.0;
+#pragma unroll
+        for (int r = 1; r < RS; ++r) yp[r] = yp[r - 1] * y;
+        double xp = 1.0;
+#pragma unroll
+        for (int r = DEG; r >= 0; --r) {
+            W[i][r] = xp * yp[r];
+            xp *= x;
+        }
+#pragma unroll
+        for (int k = 0; k < NPMAX; ++k) v[i][k] = (uint32_t)k < np0 ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    MDP_STAMP(stamps, 1);
+    const double *rp = Rl;
+    unsigned long long cyc_run = 0, cyc_gen = 0;  // diagnostic accounting only
+    for (uint32_t pi = 0; pi < nprog; ++pi) {
+        const uint32_t op = pl[pi];
+        const unsigned long long t_op = stamps ? __builtin_amdgcn_s_memtime() : 0ull;
+        if ((op & 1u) == 0) {
+            uint32_t cnt = op >> 1;
+            for (; cnt >= 2; cnt -= 2, rp += 2 * RSP) {
+                double ra[RS], rb[RS];
+                tload_l(ra, rp);
+                tload_l(rb, rp + RSP);
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * tdot(ra, W[i]);
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * tdot(rb, W[i]);
+            }
+            if (cnt) {
+                double ra[RS];
+                tload_l(ra, rp);
+                rp += RSP;
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * tdot(ra, W[i]);
+            }
+        } else {
+            const uint32_t npp = (op >> 8) & 0xffu, npc = (op >> 16) & 0xffu;
+            double vn[EPL][NPMAX];
+#pragma unroll
+            for (int l = 0; l < NPMAX; ++l) {
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) vn[i][l] = 0.0;
+                if ((uint32_t)l < npc) {
+#pragma unroll
+                    for (int k = 0; k < NPMAX; ++k) {
+                        if ((uint32_t)k < npp) {
+                            double rc[RS];
+                            tload_l(rc, rp);
+                            rp += RSP;
+#pragma unroll
+                            for (int i = 0; i < EPL; ++i) vn[i][l] = fma(v[i][k], tdot(rc, W[i]), vn[i][l]);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < EPL; ++i)
+#pragma unroll
+                for (int l = 0; l < NPMAX; ++l) v[i][l] = vn[i][l];
+        }
+        if (stamps) {
+            const unsigned long long dt = __builtin_amdgcn_s_memtime() - t_op;
+            if (op & 1u) cyc_gen += dt;
+            else cyc_run += dt;
+        }
+    }
+    if (stamps && threadIdx.x == 0) {
+        stamps[(size_t)(blockIdx.x + gridDim.x * blockIdx.y) * kStampSlots + 3] = cyc_run;
+        stamps[(size_t)(blockIdx.x + gridDim.x * blockIdx.y) * kStampSlots + 4] = cyc_gen;
+    }
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+        double L = 0.0;
+#pragma unroll
+        for (int l = 0; l < NPMAX; ++l) L += v[i][l] * prior0;
+        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + ic] = log(L);
+    }
+    MDP_STAMP(stamps, 2);
+    MDP_RSTAMP(stamps, 7);
 }
 
 // ---------------------------------------------------------------------------
@@ -428,12 +654,17 @@ struct DevCtx {
     double *S = nullptr;
     uint32_t *var_cols = nullptr, *row_col = nullptr;
     uint32_t *pairA = nullptr, *pairB = nullptr, *pairOff = nullptr;
-    uint32_t *use_pair = nullptr, *prog = nullptr, *items = nullptr;
+    uint32_t *udesc = nullptr, *prog = nullptr, *pairPart0 = nullptr, *partP = nullptr, *partK0 = nullptr;
     double *e = nullptr, *c = nullptr;
     size_t cap_e = 0, cap_c = 0;
     uint32_t ne = 0, nc = 0;
-    double *ZPV = nullptr, *R = nullptr, *out = nullptr;
-    size_t cap_zpv = 0, cap_r = 0, cap_out = 0;
+    double *ZPV = nullptr, *R = nullptr, *out = nullptr, *gpart = nullptr;
+    size_t cap_zpv = 0, cap_r = 0, cap_out = 0, cap_gpart = 0;
+    unsigned long long *stamps[3] = {nullptr, nullptr, nullptr};  // k_zpv, k_coefs, k_forward
+    size_t cap_st[3] = {0, 0, 0};
+    size_t nst[3] = {0, 0, 0};
+    hipModule_t jit_mod = nullptr;   // problem-specialised forward kernel
+    hipFunction_t jit_fn = nullptr;
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     size_t ev_used = 0;          // event sets recorded since the last collect
 };
@@ -446,10 +677,17 @@ struct mdp_engine {
     uint32_t deg = 0;         // homogeneous transition degree D
     uint32_t maxA = 0;        // max |A| over uses
     int epl = kEPL;           // k_forward points per lane (MDP_EPL overrides: 1, 2, 4)
+    bool fwd_lds = false;     // coefficient block staged in LDS (k_forward_lds)
+    size_t fwd_lds_bytes = 0;
     bool lds_zpv = true;      // k_coefs stages Z/PV in LDS
+    bool lds_part = true;     // k_coefs keeps subset partial sums in LDS
+    bool diag = false;        // MDP_DIAG: record phase stamps
+    bool jit = false;         // forward kernel specialised with hipRTC (spom_jit.cpp)
+    std::vector<char> jit_code;
+    std::string jit_log;
     size_t coef_lds = 0;      // k_coefs dynamic LDS bytes
     double prior0 = 1.0;
-    std::vector<uint32_t> np, pairA, pairB, pairOff, use_pair, prog, items;
+    std::vector<uint32_t> np, pairA, pairB, pairOff, use_pair, prog, udesc, pairPart0, partP, partK0;
     std::vector<DevCtx> devs;
     int profiling = 0;
     double last_ms[3] = {0, 0, 0};  // mean per run over the last collected runs
@@ -459,7 +697,7 @@ struct mdp_engine {
 
 namespace {
 
-constexpr int kDegBuckets[] = {2, 4, 6, 8, 12, 16, 24};
+constexpr int kDegBuckets[] = {4, 8, 16, 24};
 
 int select_variant(mdp_engine *eng)
 {
@@ -540,24 +778,21 @@ int build_plan(mdp_engine *eng, const mdp_problem *p)
         off += (uint32_t)__builtin_popcount(A0[i] & B0[i]) + 1u;
     }
     for (uint32_t u : use0) eng->use_pair.push_back(rank[u]);
-    // k_coefs work items (pair, m), heaviest (largest C(|X|, m)) first
-    {
-        std::vector<std::pair<double, uint32_t>> w;
-        for (uint32_t pi = 0; pi < eng->pairA.size(); ++pi) {
-            const uint32_t nX = (uint32_t)__builtin_popcount(eng->pairA[pi] & eng->pairB[pi]);
-            double cnk = 1.0;
-            for (uint32_t m = 0; m <= nX; ++m) {
-                w.emplace_back(-cnk, (pi << 5) | m);
-                cnk = cnk * (double)(nX - m) / (double)(m + 1);
-            }
+    // k_coefs subset parts (pair, first subset index), and per-use descriptors
+    for (uint32_t pi = 0; pi < eng->pairA.size(); ++pi) {
+        const uint32_t nX = (uint32_t)__builtin_popcount(eng->pairA[pi] & eng->pairB[pi]);
+        eng->pairPart0.push_back((uint32_t)eng->partP.size());
+        for (uint32_t k0 = 0; k0 < (1u << nX); k0 += kSubPart) {
+            eng->partP.push_back(pi);
+            eng->partK0.push_back(k0);
         }
-        std::stable_sort(w.begin(), w.end(),
-                         [](const std::pair<double, uint32_t> &a, const std::pair<double, uint32_t> &b) {
-                             return a.first < b.first;
-                         });
-        for (auto &x : w) eng->items.push_back(x.second);
-        if (eng->pairA.size() >= (1u << 27))
-            return mdp_set_error(MDP_EUNSUPPORTED, "too many transition pairs");
+    }
+    eng->pairPart0.push_back((uint32_t)eng->partP.size());
+    if (off > kOffMask) return mdp_set_error(MDP_EUNSUPPORTED, "too many transition coefficients");
+    for (uint32_t pi : eng->use_pair) {
+        const uint32_t A = eng->pairA[pi], B = eng->pairB[pi];
+        const uint32_t nA = (uint32_t)__builtin_popcount(A), nX = (uint32_t)__builtin_popcount(A & B);
+        eng->udesc.push_back(eng->pairOff[pi] | (nX << kOffBits) | (nA << 27));
     }
     eng->npairs = (uint32_t)eng->pairA.size();
     eng->nuses = (uint32_t)eng->use_pair.size();
@@ -579,14 +814,20 @@ int build_plan(mdp_engine *eng, const mdp_problem *p)
         }
     }
     eng->prog.push_back(0u);  // pad: the forward kernel reads one word ahead
-    // k_coefs LDS plan
+    // k_coefs LDS plan: [Z/PV block] [part partials] [Q] [binomials]; the
+    // partials spill to a global scratch when they do not fit
     const size_t zbytes = (size_t)(eng->nvar + 1) * eng->nstates * sizeof(double);
-    const size_t qbytes = (size_t)eng->ncoef * sizeof(double);
-    if (zbytes + qbytes <= kLdsBudget) {
-        eng->lds_zpv = true;
-        eng->coef_lds = zbytes + qbytes;
-    } else if (qbytes <= kLdsBudget) {
+    const size_t pbytes = (size_t)eng->partP.size() * (eng->nvar + 1) * sizeof(double);
+    const size_t qbytes = ((size_t)eng->ncoef + (size_t)(kMaxDeg + 1) * (kMaxDeg + 1)) * sizeof(double);
+    if (zbytes + pbytes + qbytes <= kLdsBudget) {
+        eng->lds_zpv = eng->lds_part = true;
+        eng->coef_lds = zbytes + pbytes + qbytes;
+    } else if (pbytes + qbytes <= kLdsBudget) {
         eng->lds_zpv = false;
+        eng->lds_part = true;
+        eng->coef_lds = pbytes + qbytes;
+    } else if (qbytes <= kLdsBudget) {
+        eng->lds_zpv = eng->lds_part = false;
         eng->coef_lds = qbytes;
     } else {
         return mdp_set_error(MDP_EUNSUPPORTED, "%u transition coefficients exceed the LDS budget",
@@ -623,8 +864,10 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
     if ((rc = dev_upload(&dM, M))) return rc;
     if ((rc = dev_upload(&d.var_cols, var)) || (rc = dev_upload(&d.row_col, row_col)) ||
         (rc = dev_upload(&d.pairA, eng->pairA)) || (rc = dev_upload(&d.pairB, eng->pairB)) ||
-        (rc = dev_upload(&d.pairOff, eng->pairOff)) || (rc = dev_upload(&d.use_pair, eng->use_pair)) ||
-        (rc = dev_upload(&d.prog, eng->prog)) || (rc = dev_upload(&d.items, eng->items)) ||
+        (rc = dev_upload(&d.pairOff, eng->pairOff)) || (rc = dev_upload(&d.udesc, eng->udesc)) ||
+        (rc = dev_upload(&d.pairPart0, eng->pairPart0)) || (rc = dev_upload(&d.partP, eng->partP)) ||
+        (rc = dev_upload(&d.partK0, eng->partK0)) ||
+        (rc = dev_upload(&d.prog, eng->prog)) ||
         (rc = dev_alloc(&d.S, (size_t)p->n * eng->nstates))) {
         (void)hipFree(dM);
         return rc;
@@ -635,10 +878,17 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(d.stream));
     (void)hipFree(dM);
+    if (eng->jit) {
+        HIP_TRY(hipModuleLoadData(&d.jit_mod, eng->jit_code.data()));
+        HIP_TRY(hipModuleGetFunction(&d.jit_fn, d.jit_mod, "mdp_fwd_jit"));
+    }
     if (eng->coef_lds > 64 * 1024) {
-        const void *fns[] = {(const void *)k_coefs<true, 8>,   (const void *)k_coefs<true, 16>,
-                             (const void *)k_coefs<true, 24>,  (const void *)k_coefs<false, 8>,
-                             (const void *)k_coefs<false, 16>, (const void *)k_coefs<false, 24>};
+        const void *fns[] = {
+            (const void *)k_coefs<true, true, 8>,   (const void *)k_coefs<true, true, 16>,
+            (const void *)k_coefs<true, true, 24>,  (const void *)k_coefs<false, true, 8>,
+            (const void *)k_coefs<false, true, 16>, (const void *)k_coefs<false, true, 24>,
+            (const void *)k_coefs<false, false, 8>, (const void *)k_coefs<false, false, 16>,
+            (const void *)k_coefs<false, false, 24>};
         for (const void *fn : fns)
             HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)eng->coef_lds));
@@ -649,17 +899,19 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
 void free_device(DevCtx &d)
 {
     (void)hipSetDevice(d.device);
-    void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.use_pair, d.prog, d.items,
-                    d.e, d.c, d.ZPV, d.R, d.out};
+    void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog, d.pairPart0, d.partP, d.partK0,
+                    d.e, d.c, d.ZPV, d.R, d.out, d.gpart, d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
     for (hipEvent_t ev : d.ev) (void)hipEventDestroy(ev);
+    if (d.jit_mod) (void)hipModuleUnload(d.jit_mod);
     if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
-// per-c coefficient stride: every forward use plus two zero transitions of
-// prefetch padding
-size_t ldR_of(const mdp_engine *eng) { return ((size_t)eng->nuses + 2) * (eng->deg + 1); }
+// per-c coefficient stride: every forward use (deg+1 coefficients padded to
+// an even count) plus two zero transitions of prefetch padding
+size_t rsp_of(const mdp_engine *eng) { return (eng->deg + 2) & ~1u; }
+size_t ldR_of(const mdp_engine *eng) { return ((size_t)eng->nuses + 2) * rsp_of(eng); }
 
 int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const double *c,
                  uint32_t nc)
@@ -670,6 +922,18 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         (rc = dev_reserve(&d.ZPV, &d.cap_zpv, (size_t)nc * (eng->nvar + 1) * eng->nstates)) ||
         (rc = dev_reserve(&d.R, &d.cap_r, (size_t)nc * ldR_of(eng))))
         return rc;
+    if (!eng->lds_part &&
+        (rc = dev_reserve(&d.gpart, &d.cap_gpart, (size_t)nc * eng->partP.size() * (eng->nvar + 1))))
+        return rc;
+    if (eng->diag) {
+        d.nst[0] = (size_t)((eng->nstates + kZpvJ - 1) / kZpvJ) * ((nc + kZpvCT - 1) / kZpvCT);
+        d.nst[1] = nc;
+        d.nst[2] = (size_t)nc * ((ne + kBlock - 1) / kBlock);
+        for (int k = 0; k < 3; ++k) {
+            if ((rc = dev_reserve(&d.stamps[k], &d.cap_st[k], d.nst[k] * kStampSlots))) return rc;
+            HIP_TRY(hipMemset(d.stamps[k], 0, d.cap_st[k] * sizeof(unsigned long long)));
+        }
+    }
     if (ne) HIP_TRY(hipMemcpy(d.e, e, ne * sizeof(double), hipMemcpyHostToDevice));
     if (nc) HIP_TRY(hipMemcpy(d.c, c, nc * sizeof(double), hipMemcpyHostToDevice));
     d.ne = ne;
@@ -681,8 +945,14 @@ template <int NP, int DEG, int EPL>
 void launch_fwd_epl(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
 {
     dim3 grid(d.nc, (d.ne + kBlock * EPL - 1) / (kBlock * EPL));
-    hipLaunchKernelGGL((k_forward<NP, DEG, EPL>), grid, dim3(kBlock), 0, s, d.R, ldR_of(eng), d.prog,
-                       (uint32_t)eng->prog.size() - 1, eng->np[0], eng->prior0, d.e, d.ne, out, ld);
+    const uint32_t nprog = (uint32_t)eng->prog.size() - 1;
+    if (eng->fwd_lds)
+        hipLaunchKernelGGL((k_forward_lds<NP, DEG, EPL>), grid, dim3(kBlock), eng->fwd_lds_bytes, s,
+                           d.R, ldR_of(eng), d.prog, nprog, eng->np[0], eng->prior0, d.e, d.ne, out, ld,
+                           d.stamps[2]);
+    else
+        hipLaunchKernelGGL((k_forward<NP, DEG, EPL>), grid, dim3(kBlock), 0, s, d.R, ldR_of(eng),
+                           d.prog, nprog, eng->np[0], eng->prior0, d.e, d.ne, out, ld);
 }
 
 template <int NP, int DEG>
@@ -699,11 +969,8 @@ template <int NP>
 int launch_fwd_deg(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
 {
     switch (eng->deg) {
-    case 2: launch_fwd<NP, 2>(eng, d, out, ld, s); break;
     case 4: launch_fwd<NP, 4>(eng, d, out, ld, s); break;
-    case 6: launch_fwd<NP, 6>(eng, d, out, ld, s); break;
     case 8: launch_fwd<NP, 8>(eng, d, out, ld, s); break;
-    case 12: launch_fwd<NP, 12>(eng, d, out, ld, s); break;
     case 16: launch_fwd<NP, 16>(eng, d, out, ld, s); break;
     case 24: launch_fwd<NP, 24>(eng, d, out, ld, s); break;
     default: return mdp_set_error(MDP_EUNSUPPORTED, "no forward kernel for degree %u", eng->deg);
@@ -714,6 +981,16 @@ int launch_fwd_deg(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
 int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
 {
     int rc;
+    if (eng->jit && d.jit_fn) {
+        const double *R = d.R;
+        double prior0 = eng->prior0;
+        const double *ev = d.e;
+        uint32_t ne = d.ne;
+        void *args[] = {(void *)&R, (void *)&prior0, (void *)&ev, (void *)&ne, (void *)&out, (void *)&ld};
+        const unsigned gy = (d.ne + kBlock * eng->epl - 1) / (kBlock * eng->epl);
+        HIP_TRY(hipModuleLaunchKernel(d.jit_fn, d.nc, gy, 1, kBlock, 1, 1, 0, s, args, nullptr));
+        return MDP_OK;
+    }
     switch (eng->variant / 100) {
     case 1: rc = launch_fwd_deg<1>(eng, d, out, ld, s); break;
     case 2: rc = launch_fwd_deg<2>(eng, d, out, ld, s); break;
@@ -727,26 +1004,29 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
     return MDP_OK;
 }
 
-template <bool LDS, int NV>
+template <bool LDSZ, bool LDSP, int NV>
 void launch_coefs_nv(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_coefs<LDS, NV>), dim3(d.nc), dim3(kBlock), eng->coef_lds, s, d.ZPV,
-                       eng->nstates, eng->nvar, d.pairA, d.pairB, d.pairOff, d.items,
-                       (uint32_t)eng->items.size(), d.use_pair, eng->nuses, eng->deg, d.R, ldR_of(eng));
+    hipLaunchKernelGGL((k_coefs<LDSZ, LDSP, NV>), dim3(d.nc), dim3(kBlock), eng->coef_lds, s, d.ZPV,
+                       eng->nstates, eng->nvar, d.pairA, d.pairB, d.pairOff, d.pairPart0, eng->npairs,
+                       d.partP, d.partK0, (uint32_t)eng->partP.size(), eng->ncoef, d.udesc,
+                       eng->nuses, eng->deg, d.R, ldR_of(eng), d.gpart, d.stamps[1]);
+}
+
+template <bool LDSZ, bool LDSP>
+void launch_coefs_lds(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
+{
+    const uint32_t nv = eng->nvar;
+    if (nv <= 8) launch_coefs_nv<LDSZ, LDSP, 8>(eng, d, s);
+    else if (nv <= 16) launch_coefs_nv<LDSZ, LDSP, 16>(eng, d, s);
+    else launch_coefs_nv<LDSZ, LDSP, 24>(eng, d, s);
 }
 
 int launch_coefs(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
 {
-    const uint32_t nv = eng->nvar;
-    if (eng->lds_zpv) {
-        if (nv <= 8) launch_coefs_nv<true, 8>(eng, d, s);
-        else if (nv <= 16) launch_coefs_nv<true, 16>(eng, d, s);
-        else launch_coefs_nv<true, 24>(eng, d, s);
-    } else {
-        if (nv <= 8) launch_coefs_nv<false, 8>(eng, d, s);
-        else if (nv <= 16) launch_coefs_nv<false, 16>(eng, d, s);
-        else launch_coefs_nv<false, 24>(eng, d, s);
-    }
+    if (eng->lds_zpv) launch_coefs_lds<true, true>(eng, d, s);
+    else if (eng->lds_part) launch_coefs_lds<false, true>(eng, d, s);
+    else launch_coefs_lds<false, false>(eng, d, s);
     HIP_TRY(hipGetLastError());
     return MDP_OK;
 }
@@ -774,7 +1054,7 @@ int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
     {
         dim3 grid((eng->nstates + kZpvJ - 1) / kZpvJ, (d.nc + kZpvCT - 1) / kZpvCT);
         hipLaunchKernelGGL(k_zpv, grid, dim3(kBlock), 0, s, d.S, eng->nstates, eng->n - eng->nvar,
-                           eng->nvar, d.c, d.nc, d.ZPV);
+                           eng->nvar, d.c, d.nc, d.ZPV, d.stamps[0]);
         HIP_TRY(hipGetLastError());
     }
     if (prof) HIP_TRY(hipEventRecord(ev[kEvZpv], s));
@@ -830,9 +1110,31 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
         delete eng;
         return rc;
     }
+    eng->fwd_lds_bytes = ldR_of(eng) * sizeof(double) + (eng->prog.size() + 1) * sizeof(uint32_t);
+    eng->fwd_lds = eng->fwd_lds_bytes <= kFwdLds;
+    if (const char *ev = getenv("MDP_FWD"))
+        if (!strcmp(ev, "scalar")) eng->fwd_lds = false;
     if (const char *ev = getenv("MDP_EPL")) {
         const int v = atoi(ev);
         if (v == 1 || v == 2 || v == 4) eng->epl = v;
+    }
+    if (const char *ev = getenv("MDP_DIAG")) eng->diag = atoi(ev) != 0;
+    {
+        const char *jv = getenv("MDP_JIT");
+        const bool want = !(jv && !strcmp(jv, "0")) && !eng->diag;
+        if (want && eng->nuses > 0 && eng->nuses <= kJitMaxUses &&
+            ldR_of(eng) * sizeof(double) <= kJitMaxLds) {
+            MdpJitPlan plan;
+            plan.np = eng->np;
+            plan.deg = eng->deg;
+            plan.ldR = ldR_of(eng);
+            plan.epl = eng->epl;
+            if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
+            const std::string src = mdp_jit_forward_source(plan);
+            if (mdp_jit_compile(src, eng->jit_code, eng->jit_log) == 0) eng->jit = true;
+            else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the generic kernel:\n%s\n",
+                         eng->jit_log.c_str());
+        }
     }
     std::vector<int> ids;
     if (n_devices == 0) {
@@ -920,6 +1222,65 @@ int mdp_loglik_grid(mdp_engine *eng, const double *e, uint32_t ne, const double 
     return MDP_OK;
 }
 
+int mdp_engine_diag_report(mdp_engine *eng, char *buf, size_t len)
+{
+    if (!eng || !buf || !len) return mdp_set_error(MDP_EINVAL, "null argument");
+    buf[0] = 0;
+    if (!eng->diag || eng->devs.empty()) return 0;
+    DevCtx &d = eng->devs[0];
+    HIP_TRY(hipSetDevice(d.device));
+    HIP_TRY(hipDeviceSynchronize());
+    static const char *names[3] = {"k_zpv", "k_coefs", "k_forward_lds"};
+    static const int slots[3] = {3, 5, 3};
+    size_t used = 0;
+    for (int k = 0; k < 3; ++k) {
+        if (!d.stamps[k] || !d.nst[k]) continue;
+        std::vector<unsigned long long> h(d.nst[k] * kStampSlots);
+        HIP_TRY(hipMemcpy(h.data(), d.stamps[k], h.size() * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull, t1 = 0, rs0 = ~0ull, rs1 = 0, re1 = 0;
+        double rdur = 0.0;
+        std::vector<double> mean(slots[k], 0.0);
+        size_t nb = 0;
+        for (size_t b = 0; b < d.nst[k]; ++b) {
+            const unsigned long long *st = &h[b * kStampSlots];
+            if (!st[0] || !st[slots[k] - 1] || st[slots[k] - 1] < st[0]) continue;
+            ++nb;
+            rs0 = std::min(rs0, st[6]);
+            rs1 = std::max(rs1, st[6]);
+            re1 = std::max(re1, st[7]);
+            rdur += (double)(st[7] - st[6]);
+            t0 = std::min(t0, st[0]);
+            t1 = std::max(t1, st[slots[k] - 1]);
+            for (int q = 1; q < slots[k]; ++q) mean[q] += (double)(st[q] - st[q - 1]);
+        }
+        int w = snprintf(buf + used, len - used,
+                         "%s: blocks=%zu wall_us=%.2f last_start_us=%.2f mean_block_us=%.2f cycles:",
+                         names[k], nb, nb ? (re1 - rs0) * 0.01 : 0.0, nb ? (rs1 - rs0) * 0.01 : 0.0,
+                         nb ? rdur / nb * 0.01 : 0.0);
+        if (w > 0) used = std::min(len - 1, used + (size_t)w);
+        for (int q = 1; q < slots[k]; ++q) {
+            w = snprintf(buf + used, len - used, " ph%d=%.0f", q, nb ? mean[q] / nb : 0.0);
+            if (w > 0) used = std::min(len - 1, used + (size_t)w);
+        }
+        if (k == 2 && nb) {  // forward: cycles summed over run ops / general ops (wave 0)
+            double cr = 0, cg = 0;
+            for (size_t b = 0; b < d.nst[k]; ++b) {
+                const unsigned long long *st = &h[b * kStampSlots];
+                if (!st[0] || !st[2]) continue;
+                cr += (double)st[3];
+                cg += (double)st[4];
+            }
+            w = snprintf(buf + used, len - used, " run_ops=%.0f general_ops=%.0f", cr / nb, cg / nb);
+            if (w > 0) used = std::min(len - 1, used + (size_t)w);
+        }
+        w = snprintf(buf + used, len - used, "\n");
+        if (w > 0) used = std::min(len - 1, used + (size_t)w);
+        HIP_TRY(hipMemset(d.stamps[k], 0, h.size() * sizeof(unsigned long long)));
+    }
+    return (int)used;
+}
+
 int mdp_engine_set_profiling(mdp_engine *eng, int enable)
 {
     if (!eng) return mdp_set_error(MDP_EINVAL, "null engine");
@@ -952,7 +1313,7 @@ int mdp_engine_get_info(const mdp_engine *eng, mdp_engine_info *info)
     info->nuses = eng->nuses;
     info->ncoef = eng->ncoef;
     info->npmax = eng->npmax;
-    info->variant = eng->variant;
+    info->variant = eng->variant + (eng->jit ? 10000u : 0u);
     return MDP_OK;
 }
 

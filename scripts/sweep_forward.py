@@ -1,12 +1,20 @@
-"""Time k_zpv / k_coefs / k_forward variants (MDP_EPL) on configs 2 and 3.
-Usage (GPU box): python scripts/sweep_forward.py [--steps K]"""
+"""Time the engine's kernels under environment variants on configs 2 and 3.
+
+Usage (GPU box):
+  python scripts/sweep_forward.py [--steps K] [--configs 2,3] [--diag]
+         [--variants 'MDP_JIT=1,MDP_EPL=2;MDP_JIT=0,MDP_EPL=2']
+Each variant is a comma-separated list of environment assignments applied
+before the engine is created.  Prints one JSON line per (config, variant).
+"""
 import argparse
 import json
 import os
 import sys
 import tempfile
+import time
 from pathlib import Path
 
+import numpy as np
 import torch
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -14,23 +22,39 @@ sys.path.insert(0, str(ROOT))
 import midaspom_amd as mdp  # noqa: E402
 from midaspom_amd import synth  # noqa: E402
 
+DEFAULT_VARIANTS = ";".join([
+    "MDP_JIT=1,MDP_EPL=2,MDP_JIT_WINDOW=4",
+    "MDP_JIT=1,MDP_EPL=2,MDP_JIT_WINDOW=8",
+    "MDP_JIT=1,MDP_EPL=1,MDP_JIT_WINDOW=8",
+    "MDP_JIT=1,MDP_EPL=4,MDP_JIT_WINDOW=8",
+    "MDP_JIT=0,MDP_EPL=2",
+])
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=30)
-ap.add_argument("--epl", default="1,2,4")
 ap.add_argument("--configs", default="2,3")
+ap.add_argument("--variants", default=DEFAULT_VARIANTS)
+ap.add_argument("--diag", action="store_true")
 args = ap.parse_args()
 torch.cuda.set_device(0)
 tmp = Path(tempfile.mkdtemp())
-res = []
+KEYS = ("MDP_JIT", "MDP_EPL", "MDP_JIT_WINDOW", "MDP_FWD", "MDP_DIAG")
 for cfgid in [int(x) for x in args.configs.split(",")]:
     gen, s = (synth.CONFIG2, 512) if cfgid == 2 else (synth.CONFIG3, 1024)
     f = synth.write(tmp / f"c{cfgid}.txt", **gen)
     model = mdp.Model.load(f)
     g, _ = mdp.grid(s)
     ref = None
-    for epl in [int(x) for x in args.epl.split(",")]:
-        os.environ["MDP_EPL"] = str(epl)
+    for var in [v for v in args.variants.split(";") if v]:
+        for k in KEYS:
+            os.environ.pop(k, None)
+        env = dict(kv.split("=") for kv in var.split(","))
+        if args.diag:
+            env["MDP_DIAG"] = "1"
+        os.environ.update(env)
+        t0 = time.perf_counter()
         eng = mdp.Engine(model, devices=[0])
+        t_create = time.perf_counter() - t0
         eng.set_grid(g, g)
         out = torch.empty((s, s), dtype=torch.float64, device="cuda")
         st = torch.cuda.current_stream().cuda_stream
@@ -38,17 +62,27 @@ for cfgid in [int(x) for x in args.configs.split(",")]:
             eng.run(out.data_ptr(), s, st)
         torch.cuda.synchronize()
         eng.set_profiling(True)
+        t0 = time.perf_counter()
         for _ in range(args.steps):
             eng.run(out.data_ptr(), s, st)
         torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / args.steps
         ms = eng.kernel_ms()
         w = eng.work(s, s)
         o = out.cpu().numpy()
         if ref is None:
             ref = o
-        same = bool(((o == ref) | (torch.isnan(torch.from_numpy(o)).numpy())).all())
-        r = {"config": cfgid, "epl": epl, **{k: round(v * 1e3, 2) for k, v in ms.items()},
+        fin = np.isfinite(ref) & np.isfinite(o)
+        r = {"config": cfgid, "variant": var, "create_s": round(t_create, 3),
+             **{k: round(v * 1e3, 2) for k, v in ms.items()},
+             "step_us": round(wall * 1e6, 1),
              "fwd_tflops": round(w["flop_impl"] / (ms["k_forward"] * 1e-3) / 1e12, 2),
-             "bitwise_same_as_first": same, "info": eng.info()}
+             "same_inf": bool(np.array_equal(np.isinf(ref), np.isinf(o))),
+             "max_dlog_vs_first": float(np.abs(o[fin] - ref[fin]).max()) if fin.any() else 0.0,
+             "info": eng.info()}
         print(json.dumps(r), flush=True)
+        if args.diag:
+            eng.run(out.data_ptr(), s, st)
+            torch.cuda.synchronize()
+            print(eng.diag_report(), flush=True)
         eng.close()
