@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_coefs(
     uint32_t npairs, const uint32_t *__restrict__ partP, const uint32_t *__restrict__ partK0,
     uint32_t nparts, uint32_t ncoef, const uint32_t *__restrict__ udesc, uint32_t nuses,
     uint32_t deg, double *__restrict__ R, size_t ldR, double *__restrict__ gpart,
-    unsigned long long *__restrict__ stamps)
+    double *__restrict__ Qg, size_t ldQ, unsigned long long *__restrict__ stamps)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     MDP_RSTAMP(stamps, 6);
@@ -297,6 +297,13 @@ __global__ __launch_bounds__(kBlock) void k_coefs(
     }
     __syncthreads();
     MDP_STAMP(stamps, 3);
+    if (Qg) {  // problem-specialised forward kernel: it evaluates from Q directly
+        double *qd = Qg + (size_t)ic * ldQ;
+        for (uint32_t i = threadIdx.x; i < ldQ; i += kBlock) qd[i] = i < ncoef ? Qs[i] : 0.0;
+        MDP_STAMP(stamps, 4);
+        MDP_RSTAMP(stamps, 7);
+        return;
+    }
     const uint32_t rsp = (deg + 2) & ~1u;
     double *Rc = R + (size_t)ic * ldR;
     for (uint32_t it = nuses * rsp + threadIdx.x; it < (nuses + 2) * rsp; it += kBlock) Rc[it] = 0.0;
@@ -658,8 +665,8 @@ struct DevCtx {
     double *e = nullptr, *c = nullptr;
     size_t cap_e = 0, cap_c = 0;
     uint32_t ne = 0, nc = 0;
-    double *ZPV = nullptr, *R = nullptr, *out = nullptr, *gpart = nullptr;
-    size_t cap_zpv = 0, cap_r = 0, cap_out = 0, cap_gpart = 0;
+    double *ZPV = nullptr, *R = nullptr, *out = nullptr, *gpart = nullptr, *Qg = nullptr;
+    size_t cap_zpv = 0, cap_r = 0, cap_out = 0, cap_gpart = 0, cap_qg = 0;
     unsigned long long *stamps[3] = {nullptr, nullptr, nullptr};  // k_zpv, k_coefs, k_forward
     size_t cap_st[3] = {0, 0, 0};
     size_t nst[3] = {0, 0, 0};
@@ -683,6 +690,8 @@ struct mdp_engine {
     bool lds_part = true;     // k_coefs keeps subset partial sums in LDS
     bool diag = false;        // MDP_DIAG: record phase stamps
     bool jit = false;         // forward kernel specialised with hipRTC (spom_jit.cpp)
+    int jit_epl = 1;          // its grid points per lane
+    size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
     std::vector<char> jit_code;
     std::string jit_log;
     size_t coef_lds = 0;      // k_coefs dynamic LDS bytes
@@ -900,7 +909,7 @@ void free_device(DevCtx &d)
 {
     (void)hipSetDevice(d.device);
     void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog, d.pairPart0, d.partP, d.partK0,
-                    d.e, d.c, d.ZPV, d.R, d.out, d.gpart, d.stamps[0], d.stamps[1], d.stamps[2]};
+                    d.e, d.c, d.ZPV, d.R, d.out, d.gpart, d.Qg, d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
     for (hipEvent_t ev : d.ev) (void)hipEventDestroy(ev);
@@ -922,6 +931,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         (rc = dev_reserve(&d.ZPV, &d.cap_zpv, (size_t)nc * (eng->nvar + 1) * eng->nstates)) ||
         (rc = dev_reserve(&d.R, &d.cap_r, (size_t)nc * ldR_of(eng))))
         return rc;
+    if (eng->jit && (rc = dev_reserve(&d.Qg, &d.cap_qg, (size_t)nc * eng->ldQ))) return rc;
     if (!eng->lds_part &&
         (rc = dev_reserve(&d.gpart, &d.cap_gpart, (size_t)nc * eng->partP.size() * (eng->nvar + 1))))
         return rc;
@@ -982,12 +992,13 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
 {
     int rc;
     if (eng->jit && d.jit_fn) {
-        const double *R = d.R;
+        const double *Q = d.Qg;
         double prior0 = eng->prior0;
         const double *ev = d.e;
-        uint32_t ne = d.ne;
-        void *args[] = {(void *)&R, (void *)&prior0, (void *)&ev, (void *)&ne, (void *)&out, (void *)&ld};
-        const unsigned gy = (d.ne + kBlock * eng->epl - 1) / (kBlock * eng->epl);
+        uint32_t ne = d.ne, one = 1;
+        void *args[] = {(void *)&Q,   (void *)&prior0, (void *)&ev, (void *)&ne,
+                        (void *)&out, (void *)&ld,     (void *)&one};
+        const unsigned gy = (d.ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
         HIP_TRY(hipModuleLaunchKernel(d.jit_fn, d.nc, gy, 1, kBlock, 1, 1, 0, s, args, nullptr));
         return MDP_OK;
     }
@@ -1010,7 +1021,8 @@ void launch_coefs_nv(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
     hipLaunchKernelGGL((k_coefs<LDSZ, LDSP, NV>), dim3(d.nc), dim3(kBlock), eng->coef_lds, s, d.ZPV,
                        eng->nstates, eng->nvar, d.pairA, d.pairB, d.pairOff, d.pairPart0, eng->npairs,
                        d.partP, d.partK0, (uint32_t)eng->partP.size(), eng->ncoef, d.udesc,
-                       eng->nuses, eng->deg, d.R, ldR_of(eng), d.gpart, d.stamps[1]);
+                       eng->nuses, eng->deg, d.R, ldR_of(eng), d.gpart, eng->jit ? d.Qg : nullptr,
+                       eng->ldQ, d.stamps[1]);
 }
 
 template <bool LDSZ, bool LDSP>
@@ -1122,15 +1134,23 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
     {
         const char *jv = getenv("MDP_JIT");
         const bool want = !(jv && !strcmp(jv, "0")) && !eng->diag;
+        eng->ldQ = ((size_t)eng->ncoef + 1) & ~(size_t)1;
         if (want && eng->nuses > 0 && eng->nuses <= kJitMaxUses &&
-            ldR_of(eng) * sizeof(double) <= kJitMaxLds) {
+            eng->ldQ * sizeof(double) <= kJitMaxLds) {
             MdpJitPlan plan;
             plan.np = eng->np;
-            plan.deg = eng->deg;
-            plan.ldR = ldR_of(eng);
-            plan.epl = eng->epl;
+            plan.udesc = eng->udesc;
+            plan.ldQ = eng->ldQ;
+            if (const char *ev = getenv("MDP_EPL")) plan.epl = atoi(ev);
             if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
             const std::string src = mdp_jit_forward_source(plan);
+            eng->jit_epl = plan.epl;
+            if (getenv("MDP_JIT_DUMP")) {
+                if (FILE *f = fopen(getenv("MDP_JIT_DUMP"), "w")) {
+                    fputs(src.c_str(), f);
+                    fclose(f);
+                }
+            }
             if (mdp_jit_compile(src, eng->jit_code, eng->jit_log) == 0) eng->jit = true;
             else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the generic kernel:\n%s\n",
                          eng->jit_log.c_str());
@@ -1328,6 +1348,10 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     const double D = (double)eng->deg;
     double per_pt = (double)eng->nuses * (2.0 * (D + 1.0) + 2.0) + 3.0 * (D + 1.0) +
                     2.0 * (double)eng->npmax;
+    if (eng->jit) {  // direct form: (nX+1)-term dot product per use, then the v update
+        per_pt = 2.0 * (double)eng->npmax;
+        for (uint32_t dsc : eng->udesc) per_pt += 2.0 * (double)(((dsc >> kOffBits) & 31u) + 1u) + 2.0;
+    }
     if (flop_impl) *flop_impl = per_pt * pts;
     // SURVEY.md §8(d) F_alg (dense-in-j formulation)
     double fwd = 0;
@@ -1337,7 +1361,8 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     if (flop_survey) *flop_survey = falg * pts;
     // compulsory bytes of k_forward: its coefficient stream once per c, the
     // e values, the output
-    if (bytes_min) *bytes_min = 8.0 * ((double)nc * ldR_of(eng) + (double)ne + pts);
+    if (bytes_min)
+        *bytes_min = 8.0 * ((double)nc * (eng->jit ? eng->ldQ : ldR_of(eng)) + (double)ne + pts);
     return MDP_OK;
 }
 

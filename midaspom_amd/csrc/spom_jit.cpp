@@ -30,28 +30,6 @@ namespace {
 const char *kPrelude = R"SRC(
 typedef unsigned int u32;
 #define KBLOCK 256
-template <int RS>
-__device__ __forceinline__ double tdot(const double *p, const double (&w)[RS])
-{
-    // coefficient block at a 16-byte aligned LDS address: ds_read_b128 pairs
-    double c[RS];
-    const double2 *p2 = (const double2 *)p;
-#pragma unroll
-    for (int r = 0; r + 1 < RS; r += 2) {
-        const double2 q = p2[r / 2];
-        c[r] = q.x;
-        c[r + 1] = q.y;
-    }
-    if (RS & 1) c[RS - 1] = p[RS - 1];
-    double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-    for (int r = 0; r + 1 < RS; r += 2) {
-        a0 = fma(c[r], w[r], a0);
-        a1 = fma(c[r + 1], w[r + 1], a1);
-    }
-    if (RS & 1) a0 = fma(c[RS - 1], w[RS - 1], a0);
-    return a0 + a1;
-}
 )SRC";
 
 uint64_t fnv1a(const std::string &s)
@@ -111,89 +89,98 @@ std::map<uint64_t, std::vector<char>> g_code;  // in-process code-object cache
 
 }  // namespace
 
-std::string mdp_jit_forward_source(const MdpJitPlan &pl)
+std::string mdp_jit_forward_source(MdpJitPlan &pl)
 {
-    const int RS = (int)pl.deg + 1;
-    const int RSP = ((int)pl.deg + 2) & ~1;
-    const int EPL = pl.epl;
+    // weight table: every (|A|, m) a transition needs, W = x^{|A|-m} y^m
+    std::map<std::pair<uint32_t, uint32_t>, int> widx;
+    uint32_t dmax = 0;
+    for (uint32_t d : pl.udesc) {
+        const uint32_t nX = (d >> 22) & 31u, nA = d >> 27;
+        dmax = nA > dmax ? nA : dmax;
+        for (uint32_t m = 0; m <= nX; ++m) widx.emplace(std::make_pair(nA, m), 0);
+    }
+    int nw = 0;
+    for (auto &kv : widx) kv.second = nw++;
+    const int EPL = pl.epl > 0 ? pl.epl : (nw <= 64 ? 2 : 1);
+    pl.epl = EPL;
     const uint32_t np0 = pl.np[0];
     uint32_t npmax = 1;
     for (uint32_t x : pl.np) npmax = x > npmax ? x : npmax;
     std::ostringstream o;
     o << kPrelude;
-    o << "#define RS " << RS << "\n#define RSP " << RSP << "\n#define EPL " << EPL << "\n#define LDR "
-      << pl.ldR << "\n#define NPMAX " << npmax << "\n";
+    o << "#define EPL " << EPL << "\n#define LDQ " << pl.ldQ << "\n#define NPMAX " << npmax
+      << "\n#define DMAX " << dmax << "\n#define NW " << (nw ? nw : 1) << "\n";
     o << "extern \"C\" __global__ __launch_bounds__(KBLOCK) void mdp_fwd_jit(\n"
-         "    const double *__restrict__ R, double prior0, const double *__restrict__ evals, u32 ne,\n"
+         "    const double *__restrict__ Q, double prior0, const double *__restrict__ evals, u32 ne,\n"
          "    double *__restrict__ out, u32 ld_out, u32 one)\n{\n"
-         "    __shared__ __attribute__((aligned(16))) double Rl[LDR];\n"
+         "    __shared__ __attribute__((aligned(16))) double Ql[LDQ];\n"
          "    const u32 ic = blockIdx.x;\n"
          "    {\n"
-         "        const double2 *src = (const double2 *)(R + (size_t)ic * LDR);\n"
-         "        double2 *dst = (double2 *)Rl;\n"
-         "        for (u32 i0 = threadIdx.x; i0 < LDR / 2; i0 += 4 * KBLOCK) {\n"
-         "            // four loads in flight per lane; clamped indexes keep them unconditional\n"
-         "            const u32 i1 = i0 + KBLOCK, i2 = i0 + 2 * KBLOCK, i3 = i0 + 3 * KBLOCK;\n"
+         "        const double2 *src = (const double2 *)(Q + (size_t)ic * LDQ);\n"
+         "        double2 *dst = (double2 *)Ql;\n"
+         "        for (u32 i0 = threadIdx.x; i0 < LDQ / 2; i0 += 2 * KBLOCK) {\n"
+         "            const u32 i1 = i0 + KBLOCK;\n"
          "            const double2 t0 = src[i0];\n"
-         "            const double2 t1 = src[i1 < LDR / 2 ? i1 : i0];\n"
-         "            const double2 t2 = src[i2 < LDR / 2 ? i2 : i0];\n"
-         "            const double2 t3 = src[i3 < LDR / 2 ? i3 : i0];\n"
+         "            const double2 t1 = src[i1 < LDQ / 2 ? i1 : i0];\n"
          "            dst[i0] = t0;\n"
-         "            if (i1 < LDR / 2) dst[i1] = t1;\n"
-         "            if (i2 < LDR / 2) dst[i2] = t2;\n"
-         "            if (i3 < LDR / 2) dst[i3] = t3;\n"
+         "            if (i1 < LDQ / 2) dst[i1] = t1;\n"
          "        }\n"
          "    }\n"
-         "    u32 ie[EPL];\n    double W[EPL][RS];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n"
+         "    u32 ie[EPL];\n    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n"
          "#pragma unroll\n"
          "    for (int i = 0; i < EPL; ++i) {\n"
          "        ie[i] = blockIdx.y * (KBLOCK * EPL) + i * KBLOCK + threadIdx.x;\n"
          "        const double e = ie[i] < ne ? evals[ie[i]] : 0.0;\n"
          "        const double x = e > 1.0 ? 1.0 : e;\n"
          "        const double y = 1.0 - x;\n"
-         "        double yp[RS];\n        yp[0] = 1.0;\n"
-         "#pragma unroll\n        for (int r = 1; r < RS; ++r) yp[r] = yp[r - 1] * y;\n"
-         "        double xp = 1.0;\n"
-         "#pragma unroll\n        for (int r = RS - 1; r >= 0; --r) { W[i][r] = xp * yp[r]; xp *= x; }\n"
-         "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < "
-      << np0 << " ? 1.0 : 0.0;\n"
-                "    }\n"
-                "    __syncthreads();\n";
-    // one block per year transition, uses in (l, k) order as the plan's R.
-    // A sched_barrier every `window` transitions bounds how far the scheduler
-    // hoists LDS reads (unbounded, straight-line code spills hundreds of VGPRs).
-    const int window = pl.window > 0 ? pl.window : 4;
-    size_t u = 0, since = 0;
-    // Regions are separate basic blocks (an opaque always-true kernel
-    // argument guards each), which instruction selection cannot merge.
-    // each guard value passes through an opaque scalar move, so no two
-    // regions can be proven equivalent and merged
-    const char *guard = "    { u32 g_; asm volatile(\"s_mov_b32 %0, %1\" : \"=s\"(g_) : \"s\"(one)); if (g_) {\n";
+         "        double xp[DMAX + 1], yp[DMAX + 1];\n        xp[0] = 1.0;\n        yp[0] = 1.0;\n"
+         "#pragma unroll\n        for (int r = 1; r <= DMAX; ++r) { xp[r] = xp[r - 1] * x; yp[r] = yp[r - 1] * y; }\n";
+    for (auto &kv : widx)
+        o << "        W[i][" << kv.second << "] = xp[" << (kv.first.first - kv.first.second) << "] * yp["
+          << kv.first.second << "];\n";
+    o << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < " << np0
+      << " ? 1.0 : 0.0;\n"
+         "    }\n"
+         "    __syncthreads();\n";
+    // P = sum_m Q[off+m] W[|A|][m] as an expression for point i
+    auto pexpr = [&](uint32_t d) {
+        const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u, nA = d >> 27;
+        std::string e = "Ql[" + std::to_string(off) + "] * W[i][" +
+                        std::to_string(widx[std::make_pair(nA, 0u)]) + "]";
+        for (uint32_t m = 1; m <= nX; ++m)
+            e = "fma(Ql[" + std::to_string(off + m) + "], W[i][" +
+                std::to_string(widx[std::make_pair(nA, m)]) + "], " + e + ")";
+        return e;
+    };
+    // Regions are separate basic blocks: each guard value passes through an
+    // opaque scalar move, so instruction selection can neither merge regions
+    // nor hoist every transition's reads to the top (which spills).
+    const int window = pl.window > 0 ? pl.window : 8;
+    const char *guard =
+        "    { u32 g_; asm volatile(\"s_mov_b32 %0, %1\" : \"=s\"(g_) : \"s\"(one)); if (g_) {\n";
     o << guard;
-    auto fence = [&](size_t uses) {
-        since += uses;
-        if ((int)since >= window) {
+    int since = 0;
+    auto fence = [&]() {
+        if (++since >= window) {
             o << "    }}\n" << guard;
             since = 0;
         }
     };
+    size_t u = 0;
     for (size_t t = 1; t < pl.np.size(); ++t) {
         const uint32_t npp = pl.np[t - 1], npc = pl.np[t];
         if (npp == 1 && npc == 1) {
-            o << "    for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * tdot<RS>(Rl + " << u * RSP
-              << ", W[i]);\n";
-            ++u;
-            fence(1);
+            o << "    for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * (" << pexpr(pl.udesc[u++]) << ");\n";
+            fence();
             continue;
         }
-        // general year: n[.][l] = sum_k v[.][k] P[k][l] (ascending k), one
-        // statement per transition so a region boundary may fall inside
+        // general year: n[.][l] = sum_k v[.][k] P[k][l] in ascending k
         for (uint32_t l = 0; l < npc; ++l)
-            for (uint32_t k = 0; k < npp; ++k, ++u) {
-                o << "    for (int i = 0; i < EPL; ++i) n[i][" << l << "] = fma(v[i][" << k
-                  << "], tdot<RS>(Rl + " << u * RSP << ", W[i]), " << (k ? "n[i][" + std::to_string(l) + "]" : std::string("0.0"))
+            for (uint32_t k = 0; k < npp; ++k) {
+                o << "    for (int i = 0; i < EPL; ++i) n[i][" << l << "] = fma(v[i][" << k << "], "
+                  << pexpr(pl.udesc[u++]) << ", " << (k ? "n[i][" + std::to_string(l) + "]" : std::string("0.0"))
                   << ");\n";
-                fence(1);
+                fence();
             }
         o << "    for (int i = 0; i < EPL; ++i) {\n";
         for (uint32_t l = 0; l < npmax; ++l) {
@@ -210,6 +197,7 @@ std::string mdp_jit_forward_source(const MdpJitPlan &pl)
          "        for (int l = 0; l < NPMAX; ++l) L += v[i][l] * prior0;\n"
          "        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
          "    }\n}\n";
+    o << "// EPL_CHOSEN " << EPL << "\n";
     return o.str();
 }
 

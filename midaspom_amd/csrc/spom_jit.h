@@ -7,15 +7,15 @@
 #include <vector>
 
 struct MdpJitPlan {
-    std::vector<uint32_t> np;  // possible states per year
-    uint32_t deg = 0;          // homogeneous transition degree D
-    size_t ldR = 0;            // per-c coefficient block (doubles, stride RSP per use)
-    int epl = 2;               // grid points per lane
-    int window = 4;            // transitions per scheduling region
+    std::vector<uint32_t> np;     // possible states per year
+    std::vector<uint32_t> udesc;  // per forward use: Q offset | nX << 22 | nA << 27
+    size_t ldQ = 0;               // per-c coefficient block (doubles, even)
+    int epl = 0;                  // grid points per lane (0: 2 unless the weight table is large)
+    int window = 8;               // transitions per scheduling region
 };
 
-// HIP source of `mdp_fwd_jit` for this plan.
-std::string mdp_jit_forward_source(const MdpJitPlan &plan);
+// HIP source of `mdp_fwd_jit` for this plan; sets plan.epl when it was 0.
+std::string mdp_jit_forward_source(MdpJitPlan &plan);
 
 // Compile (or fetch from the memory / disk cache) a gfx950 code object.
 // Returns 0 on success; on failure `log` holds the compiler output.
