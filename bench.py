@@ -136,7 +136,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    eng.set_profiling(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -145,6 +144,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    # Kernel durations: the same K steps again, every kernel launched with its
+    # own start/stop HIP events (hipExtLaunchKernel).  Kept out of the timed
+    # region above because the event completion signals cost the stream
+    # several microseconds between kernels; the per-kernel durations agree
+    # with rocprofv3 --kernel-trace (profiles/).
+    eng.set_profiling(True)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
     kms = eng.kernel_ms()
     eng.set_profiling(False)
     if world > 1:
@@ -185,7 +193,9 @@ def main():
             "traffic": None,
             "flop_per_launch": work["flop_impl"],
             "flop_per_launch_survey_dense": work["flop_survey"],
-            "survey_dense_equiv_tflops": work["flop_survey"] / (fwd_ms * 1e-3) / 1e12,
+            # SURVEY §8(d) F_alg over the whole step: exceeds the FP64 peak
+            # because the factorised path never performs most of F_alg
+            "falg_step_equiv_tflops": work["flop_survey"] / (dt / args.steps) / 1e12,
             "uses_per_point": info["nuses"],
         },
     }

@@ -33,7 +33,7 @@ extern "C" {
 #define MDP_ENODEV (-5)       /* no usable GPU                             */
 #define MDP_EUNSUPPORTED (-6) /* problem outside the engine's limits       */
 
-#define MDP_ABI_VERSION 1
+#define MDP_ABI_VERSION 2
 
 /* ------------------------------------------------------------------ */
 /* Host model: parse + state enumeration (the reference's L2 layer)    */
@@ -123,13 +123,16 @@ int mdp_engine_set_grid(mdp_engine *engine, const double *e, uint32_t ne, const 
                         uint32_t nc);
 int mdp_engine_run(mdp_engine *engine, double *d_out, uint32_t ld_out, void *stream);
 
-/* Kernel timing: when enabled, each run records HIP events around its
- * kernels on the launch stream.  mdp_engine_kernel_ms fills up to max_k
- * durations (ms) of the last run, in launch order, and returns the count;
- * names via mdp_engine_kernel_name. */
+/* Kernel timing: when enabled, every kernel of a run is launched with its own
+ * start/stop events (stamped from the dispatch, no extra packets on the
+ * stream).  mdp_engine_kernel_ms fills up to max_k mean durations (ms) over
+ * the runs since the previous call, in launch order, and returns the count;
+ * mdp_engine_kernel_name gives the slot's kernel ("" for a slot the engine's
+ * path does not launch: the direct path runs k_colonise + k_forward, the
+ * generic path k_zpv + k_coefs + k_forward). */
 int mdp_engine_set_profiling(mdp_engine *engine, int enable);
 int mdp_engine_kernel_ms(mdp_engine *engine, double *ms, int max_k);
-const char *mdp_engine_kernel_name(int k);
+const char *mdp_engine_kernel_name(const mdp_engine *engine, int k);
 
 /* Diagnostics (MDP_DIAG=1 in the environment at engine creation): text
  * report of per-workgroup s_memtime phase durations (shader cycles) of the

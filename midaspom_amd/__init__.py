@@ -182,7 +182,8 @@ class Engine:
     def kernel_ms(self) -> dict:
         buf = (ctypes.c_double * 8)()
         k = check(lib().mdp_engine_kernel_ms(self._h, buf, 8))
-        return {lib().mdp_engine_kernel_name(i).decode(): buf[i] for i in range(k)}
+        names = [lib().mdp_engine_kernel_name(self._h, i).decode() for i in range(k)]
+        return {nm: buf[i] for i, nm in enumerate(names) if nm}
 
     def diag_report(self) -> str:
         """Phase-stamp report of the last run (engine created with MDP_DIAG=1)."""

@@ -27,6 +27,7 @@
 //   k_forward  one lane / (e,c) point x EPL: forward recursion over the years,
 //              c wave-uniform, R streamed through the scalar cache.
 // Once per engine: k_colsum builds S.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -53,13 +54,14 @@ constexpr int kEPL = 2;         // k_forward: default grid points (e values) per
 constexpr int kMaxDeg = 24;
 constexpr int kStampSlots = 8;      // diagnostic stamps per workgroup
 constexpr uint32_t kSubPart = 16;   // k_coefs: subsets per work part
+constexpr uint32_t kColItems = 8;   // k_colonise: items per task (rows with more are split)
 constexpr uint32_t kOffBits = 22;   // coefficient offset bits in a use descriptor
 constexpr uint32_t kOffMask = (1u << kOffBits) - 1u;
 constexpr unsigned kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), other counters untouched
 constexpr size_t kLdsBudget = 120 * 1024;  // dynamic LDS of k_coefs
 constexpr size_t kFwdLds = 48 * 1024;      // max coefficient block staged by k_forward_lds
 constexpr uint32_t kJitMaxUses = 2048;     // larger programs use the generic kernels
-constexpr size_t kJitMaxLds = 48 * 1024;
+constexpr size_t kJitMaxLds = 64 * 1024;   // Pc row + Q block of the direct path
 
 __constant__ double c_binom[kMaxDeg + 1][kMaxDeg + 1];
 
@@ -87,6 +89,19 @@ __constant__ double c_binom[kMaxDeg + 1][kMaxDeg + 1];
             return mdp_set_error(MDP_EHIP, "%s failed: %s (%s:%d)", #expr,               \
                                  hipGetErrorString(e_), __FILE__, __LINE__);              \
     } while (0)
+
+// Kernel timing: while an engine is profiled, every launch of a run carries
+// its own start/stop events (hipExtLaunchKernel), which the runtime stamps
+// from the dispatch itself -- no marker packets between the kernels, so the
+// timed run is the production run and the durations agree with rocprofv3.
+struct KernelEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+thread_local KernelEvents t_kev;
+
+#define MDP_LAUNCH(kernel, grid, block, shmem, stream, ...)                                     \
+    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)(shmem), stream, t_kev.start, t_kev.stop, \
+                          0u, __VA_ARGS__)
 
 // ---------------------------------------------------------------------------
 // kernels
@@ -194,6 +209,107 @@ __global__ __launch_bounds__(kBlock) void k_zpv(
     MDP_RSTAMP(stamps, 7);
 }
 
+// Colonisation factors of the direct (problem-specialised) path.  Lanes run
+// over 64 c values; each wave takes one task = (hidden state j that some
+// transition needs, up to kColItems of the states b its row feeds):
+//   Z_j(c)    = prod over always-zero columns k of (1 - min(1, c S[j][k]))
+//   Pc[j][b]  = Z_j prod_{var b' not in j} (B_b' ? pC_jb' : 1 - pC_jb')
+// jtab[task] = {j, zs offset, zs length, first item}; the next entry's first
+// item ends the task (tasks are in item order; rows split into several tasks
+// share their zs row).  A workgroup (4 tasks):
+//  1. stages its zs rows and item masks in LDS (coalesced, one round trip);
+//  2. every lane multiplies its row from LDS broadcasts;
+//  3. writes its Pc values to an LDS tile [c][item] ...
+//  4. ... which the workgroup stores as contiguous row segments of Pc[c][item]
+//     (direct per-lane stores would scatter 8-byte writes over 64 rows).
+// Columns whose factor rounds to exactly 1.0 for every c of the grid are left
+// out of zs (rows padded to a multiple of 8 with zeros, which also give 1.0),
+// so the product equals the full one.
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_colonise(
+    const double *__restrict__ cvals, uint32_t nc, uint32_t nvar, const uint4 *__restrict__ jtab,
+    uint32_t ntask, const double *__restrict__ zs, const double *__restrict__ sv,
+    const uint32_t *__restrict__ itemB, double *__restrict__ Pc, uint32_t ldP,
+    unsigned long long *__restrict__ stamps)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    MDP_RSTAMP(stamps, 6);
+    MDP_STAMP(stamps, 0);
+    constexpr uint32_t kTasks = kBlock / 64;
+    const uint32_t t0 = blockIdx.y * kTasks, t1 = min(t0 + kTasks, ntask);
+    const uint4 r0 = jtab[t0], rl = jtab[t1 - 1], r1 = jtab[t1];
+    const uint32_t zn = rl.y + rl.z - r0.y;  // multiple of 8
+    const uint32_t ni = r1.w - r0.w, tw = ni | 1u;  // tile row stride: odd, no bank conflicts
+    uint32_t *bl = (uint32_t *)(lds + zn);
+    double *tile = lds + zn + ((ni + 1) >> 1);
+    {
+        const double2 *src = (const double2 *)(zs + r0.y);
+        double2 *dst = (double2 *)lds;
+#pragma unroll 4
+        for (uint32_t i = threadIdx.x; i < zn / 2; i += kBlock) dst[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < ni; i += kBlock) bl[i] = itemB[r0.w + i];
+    }
+    const uint32_t task = t0 + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ic = blockIdx.x * 64 + lane;
+    const double c = ic < nc ? cvals[ic] : 0.0;
+    const bool active = task < t1;
+    const uint4 jt = jtab[active ? task : t0];
+    const uint32_t item1 = active ? jtab[task + 1].w : jt.w;
+    double svv[NV];  // rows padded to NV with zeros
+#pragma unroll
+    for (int b = 0; b < NV; ++b) svv[b] = sv[(size_t)(active ? task : t0) * NV + b];
+    __syncthreads();
+    MDP_STAMP(stamps, 1);
+    const double *z8 = lds + (jt.y - r0.y);
+    // 1 - min(1, c s) = max(0, fma(-c, s, 1)); the clamp to 0 happens for some
+    // column iff it happens for the row's largest s (zs[0], c >= 0), and then
+    // Z = 0.  So the loop multiplies the unclamped factors and the clamp is
+    // one test at the end (v_max_f64 issues at a fraction of the FMA rate).
+    double z = 1.0;
+#pragma unroll 2
+    for (uint32_t k = 0; k < jt.z; k += 8) {
+        double f[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) f[u] = fma(-c, z8[k + u], 1.0);
+#pragma unroll
+        for (int w = 1; w < 8; w *= 2)
+#pragma unroll
+            for (int u = 0; u + w < 8; u += 2 * w) f[u] *= f[u + w];
+        z *= f[0];
+    }
+    if (jt.z && !(fma(-c, z8[0], 1.0) > 0.0)) z = 0.0;
+    MDP_STAMP(stamps, 2);
+    // per var column: the factor for B_b = 1 (pC) and B_b = 0 (1 - pC); both
+    // 1.0 for columns inside j (and past nvar)
+    double f1[NV], f0[NV];
+#pragma unroll
+    for (int b = 0; b < NV; ++b) {
+        const bool inj = (uint32_t)b >= nvar || ((jt.x >> (nvar - 1 - b)) & 1u);
+        double pc = c * svv[b];
+        pc = pc > 1.0 ? 1.0 : pc;
+        f1[b] = inj ? 1.0 : pc;
+        f0[b] = inj ? 1.0 : 1.0 - pc;
+    }
+    for (uint32_t it = jt.w; it < item1; ++it) {
+        const uint32_t B = bl[it - r0.w];
+        double p = z;
+#pragma unroll
+        for (int b = 0; b < NV; ++b)
+            if ((uint32_t)b < nvar) p *= ((B >> (nvar - 1 - b)) & 1u) ? f1[b] : f0[b];
+        tile[lane * tw + (it - r0.w)] = p;
+    }
+    __syncthreads();
+    const uint32_t rows = min(64u, nc - blockIdx.x * 64);
+    double *dst = Pc + (size_t)blockIdx.x * 64 * ldP + r0.w;
+    for (uint32_t i = threadIdx.x; i < rows * ni; i += kBlock) {
+        const uint32_t r = i / ni, k = i - r * ni;
+        dst[(size_t)r * ldP + k] = tile[r * tw + k];
+    }
+    MDP_STAMP(stamps, 3);
+    MDP_RSTAMP(stamps, 7);
+}
+
 // One workgroup per c value.
 //  1. stage this c's Z/PV block (LDS_ZPV) and the binomial table in LDS;
 //  2. subset products: lane per part (pair p, 16 consecutive subset indexes k
@@ -211,7 +327,7 @@ __global__ __launch_bounds__(kBlock) void k_coefs(
     uint32_t npairs, const uint32_t *__restrict__ partP, const uint32_t *__restrict__ partK0,
     uint32_t nparts, uint32_t ncoef, const uint32_t *__restrict__ udesc, uint32_t nuses,
     uint32_t deg, double *__restrict__ R, size_t ldR, double *__restrict__ gpart,
-    double *__restrict__ Qg, size_t ldQ, unsigned long long *__restrict__ stamps)
+    unsigned long long *__restrict__ stamps)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     MDP_RSTAMP(stamps, 6);
@@ -297,13 +413,6 @@ __global__ __launch_bounds__(kBlock) void k_coefs(
     }
     __syncthreads();
     MDP_STAMP(stamps, 3);
-    if (Qg) {  // problem-specialised forward kernel: it evaluates from Q directly
-        double *qd = Qg + (size_t)ic * ldQ;
-        for (uint32_t i = threadIdx.x; i < ldQ; i += kBlock) qd[i] = i < ncoef ? Qs[i] : 0.0;
-        MDP_STAMP(stamps, 4);
-        MDP_RSTAMP(stamps, 7);
-        return;
-    }
     const uint32_t rsp = (deg + 2) & ~1u;
     double *Rc = R + (size_t)ic * ldR;
     for (uint32_t it = nuses * rsp + threadIdx.x; it < (nuses + 2) * rsp; it += kBlock) Rc[it] = 0.0;
@@ -652,8 +761,9 @@ int dev_reserve(T **p, size_t *cap, size_t count)
     return MDP_OK;
 }
 
-enum { kEvBegin = 0, kEvZpv, kEvCoefs, kEvForward, kNumEv };
-const char *const kKernelNames[] = {"k_zpv", "k_coefs", "k_forward"};
+constexpr int kNumEv = 6;  // start/stop per kernel: k_zpv, k_coefs, k_forward
+const char *const kKernelNames[2][3] = {{"k_zpv", "k_coefs", "k_forward"},
+                                        {"k_colonise", "", "k_forward"}};
 
 struct DevCtx {
     int device = 0;
@@ -665,11 +775,18 @@ struct DevCtx {
     double *e = nullptr, *c = nullptr;
     size_t cap_e = 0, cap_c = 0;
     uint32_t ne = 0, nc = 0;
-    double *ZPV = nullptr, *R = nullptr, *out = nullptr, *gpart = nullptr, *Qg = nullptr;
-    size_t cap_zpv = 0, cap_r = 0, cap_out = 0, cap_gpart = 0, cap_qg = 0;
+    double *ZPV = nullptr, *R = nullptr, *out = nullptr, *gpart = nullptr;
+    size_t cap_zpv = 0, cap_r = 0, cap_out = 0, cap_gpart = 0;
     unsigned long long *stamps[3] = {nullptr, nullptr, nullptr};  // k_zpv, k_coefs, k_forward
     size_t cap_st[3] = {0, 0, 0};
     size_t nst[3] = {0, 0, 0};
+    // direct path: colonisation tables (jtab / zs depend on the grid's c range)
+    uint4 *jtab = nullptr;
+    double *zs = nullptr, *sv = nullptr, *Pc = nullptr;
+    uint32_t *itemB = nullptr, *qstart = nullptr, *qitem = nullptr;
+    size_t cap_jtab = 0, cap_zs = 0, cap_pc = 0;
+    size_t col_lds = 0;     // k_colonise dynamic LDS: largest workgroup's S rows + item masks
+    double zs_cmax = -1.0;  // c bound the uploaded zs was pruned for (-1: none yet)
     hipModule_t jit_mod = nullptr;   // problem-specialised forward kernel
     hipFunction_t jit_fn = nullptr;
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
@@ -693,6 +810,14 @@ struct mdp_engine {
     int jit_epl = 1;          // its grid points per lane
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
     std::vector<char> jit_code;
+    // direct path (jit): k_colonise computes Pc[j][b] for the needed (j, b)
+    // items, the forward kernel assembles Q from them
+    uint32_t nj = 0, nitems = 0, ncoef_d = 0;
+    size_t ldP = 0;
+    std::vector<uint32_t> cj_bits, cj_item0, itemB, qstart, qitem, udesc_d, var_cols;
+    std::vector<uint32_t> task_js, task_item0;  // k_colonise tasks: j slot, first item (+ end)
+    std::vector<uint8_t> isvar;
+    std::vector<double> Sj;  // [nj][n] colonisation sums of every column for each needed j
     std::string jit_log;
     size_t coef_lds = 0;      // k_coefs dynamic LDS bytes
     double prior0 = 1.0;
@@ -845,6 +970,179 @@ int build_plan(mdp_engine *eng, const mdp_problem *p)
     return MDP_OK;
 }
 
+// Direct-path plan.  Transitions that share X = A & B and the target state B
+// share Q; each (X, B) group needs Pc[j][B] for every j <= X.  Items are the
+// distinct (j, B), numbered by j ascending then B ascending; qstart / qitem
+// list, for every Q entry (group, m), its items with |j| = m in ascending j.
+int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
+{
+    std::map<uint64_t, uint32_t> group;  // (X, B) -> Q offset
+    std::vector<std::pair<uint32_t, uint32_t>> groups;
+    std::vector<uint32_t> pair_group(eng->pairA.size());
+    uint32_t off = 0;
+    std::vector<uint32_t> goff;
+    for (size_t pi = 0; pi < eng->pairA.size(); ++pi) {
+        const uint32_t B = eng->pairB[pi], X = eng->pairA[pi] & B;
+        const uint64_t key = ((uint64_t)X << 32) | B;
+        auto it = group.find(key);
+        if (it == group.end()) {
+            it = group.emplace(key, (uint32_t)groups.size()).first;
+            groups.push_back({X, B});
+            goff.push_back(off);
+            off += (uint32_t)__builtin_popcount(X) + 1u;
+        }
+        pair_group[pi] = it->second;
+    }
+    if (off > kOffMask) return mdp_set_error(MDP_EUNSUPPORTED, "too many transition coefficients");
+    eng->ncoef_d = off;
+    std::map<uint32_t, std::vector<uint32_t>> jb;  // j -> states B (sorted, unique)
+    auto for_subsets = [](uint32_t X, auto &&fn) {  // ascending j <= X
+        const uint32_t nX = (uint32_t)__builtin_popcount(X);
+        for (uint32_t k = 0; k < (1u << nX); ++k) {
+            uint32_t j = 0, xs = X;
+            for (uint32_t i = 0; i < nX; ++i) {
+                const uint32_t low = xs & (0u - xs);
+                if ((k >> i) & 1u) j |= low;
+                xs ^= low;
+            }
+            fn(j);
+        }
+    };
+    for (auto &g : groups) for_subsets(g.first, [&](uint32_t j) { jb[j].push_back(g.second); });
+    std::map<uint64_t, uint32_t> item;  // (j, B) -> item
+    eng->cj_bits.clear();
+    eng->cj_item0.clear();
+    eng->itemB.clear();
+    for (auto &kv : jb) {
+        auto &v = kv.second;
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        eng->cj_bits.push_back(kv.first);
+        eng->cj_item0.push_back((uint32_t)eng->itemB.size());
+        for (uint32_t B : v) {
+            item.emplace(((uint64_t)kv.first << 32) | B, (uint32_t)eng->itemB.size());
+            eng->itemB.push_back(B);
+        }
+    }
+    eng->cj_item0.push_back((uint32_t)eng->itemB.size());
+    eng->nj = (uint32_t)eng->cj_bits.size();
+    eng->task_js.clear();
+    eng->task_item0.clear();
+    for (uint32_t js = 0; js < eng->nj; ++js)
+        for (uint32_t i = eng->cj_item0[js]; i < eng->cj_item0[js + 1]; i += kColItems) {
+            eng->task_js.push_back(js);
+            eng->task_item0.push_back(i);
+        }
+    eng->task_item0.push_back((uint32_t)eng->itemB.size());
+    eng->nitems = (uint32_t)eng->itemB.size();
+    eng->ldP = ((size_t)eng->nitems + 1) & ~(size_t)1;
+    eng->qstart.assign(1, 0u);
+    eng->qitem.clear();
+    for (auto &g : groups) {
+        const uint32_t nX = (uint32_t)__builtin_popcount(g.first);
+        for (uint32_t m = 0; m <= nX; ++m) {
+            for_subsets(g.first, [&](uint32_t j) {
+                if ((uint32_t)__builtin_popcount(j) == m)
+                    eng->qitem.push_back(item.at(((uint64_t)j << 32) | g.second));
+            });
+            eng->qstart.push_back((uint32_t)eng->qitem.size());
+        }
+    }
+    eng->udesc_d.clear();
+    for (uint32_t pi : eng->use_pair) {
+        const uint32_t A = eng->pairA[pi], B = eng->pairB[pi];
+        const uint32_t nA = (uint32_t)__builtin_popcount(A), nX = (uint32_t)__builtin_popcount(A & B);
+        eng->udesc_d.push_back(goff[pair_group[pi]] | (nX << kOffBits) | (nA << 27));
+    }
+    // colonisation sums S[j][k] = sum over var columns l in j (ascending),
+    // l != k, of M[l][k] -- the reference's per-point sum (:350-357) with its
+    // zero terms dropped, in its order
+    const uint32_t n = p->n, nvar = p->nvar;
+    eng->var_cols.assign(p->var_cols, p->var_cols + nvar);
+    eng->isvar.assign(n, 0);
+    for (uint32_t b = 0; b < nvar; ++b) eng->isvar[p->var_cols[b]] = 1;
+    eng->Sj.assign((size_t)eng->nj * n, 0.0);
+    for (uint32_t js = 0; js < eng->nj; ++js) {
+        const uint32_t j = eng->cj_bits[js];
+        for (uint32_t k = 0; k < n; ++k) {
+            double acc = 0.0;
+            for (uint32_t b = 0; b < nvar; ++b) {
+                const uint32_t col = p->var_cols[b];
+                if (((j >> (nvar - 1 - b)) & 1u) && col != k) acc += p->M[(size_t)col * n + k];
+            }
+            eng->Sj[(size_t)js * n + k] = acc;
+        }
+    }
+    return MDP_OK;
+}
+
+uint32_t colonise_nv(uint32_t nvar) { return nvar <= 8 ? 8u : nvar <= 16 ? 16u : 24u; }
+constexpr size_t kColLdsMax = 160 * 1024;
+
+// k_colonise LDS per workgroup (tasks [t0, t0 + 4)): zs rows, item masks and
+// the [64][items | 1] output tile; zlen per j slot
+size_t colonise_lds(const mdp_engine *eng, const std::vector<uint32_t> &zlen)
+{
+    size_t mx = 0;
+    const uint32_t nt = (uint32_t)eng->task_js.size();
+    for (uint32_t t0 = 0; t0 < nt; t0 += kBlock / 64) {
+        const uint32_t t1 = std::min<uint32_t>(t0 + kBlock / 64, nt);
+        size_t z = 0;
+        for (uint32_t t = t0; t < t1; ++t)
+            if (t == t0 || eng->task_js[t] != eng->task_js[t - 1]) z += zlen[eng->task_js[t]];
+        const size_t ni = eng->task_item0[t1] - eng->task_item0[t0];
+        mx = std::max(mx, (z + (ni + 1) / 2 + 64 * (ni | 1)) * sizeof(double));
+    }
+    return mx;
+}
+
+// zs / jtab for a grid whose |c| <= cmax: a column's factor
+// max(0, fma(-c, s, 1)) is exactly 1.0 when |c s| <= 2^-55, so it is dropped
+int upload_colonise_tables(const mdp_engine *eng, DevCtx &d, double cmax)
+{
+    std::vector<double> zs;
+    std::vector<uint32_t> zoff(eng->nj), zlen(eng->nj);
+    const uint32_t n = eng->n;
+    for (uint32_t js = 0; js < eng->nj; ++js) {
+        const size_t z0 = zs.size();
+        size_t imax = z0;
+        for (uint32_t k = 0; k < n; ++k) {
+            if (eng->isvar[k]) continue;
+            const double sv = eng->Sj[(size_t)js * n + k];
+            if (cmax * sv <= 0x1p-55) continue;  // false for NaN / inf: kept
+            if (zs.size() > z0 && sv > zs[imax]) imax = zs.size();
+            zs.push_back(sv);
+        }
+        // the clamp test reads the row's largest value first: rotate it to the
+        // front (the product order changes, each factor stays the same)
+        if (zs.size() > z0) std::swap(zs[z0], zs[imax]);
+        while ((zs.size() - z0) % 8) zs.push_back(0.0);
+        zoff[js] = (uint32_t)z0;
+        zlen[js] = (uint32_t)(zs.size() - z0);
+    }
+    std::vector<uint4> jtab;
+    for (size_t t = 0; t < eng->task_js.size(); ++t) {
+        const uint32_t js = eng->task_js[t];
+        jtab.push_back(make_uint4(eng->cj_bits[js], zoff[js], zlen[js], eng->task_item0[t]));
+    }
+    jtab.push_back(make_uint4(0u, (uint32_t)zs.size(), 0u, eng->nitems));
+    d.col_lds = colonise_lds(eng, zlen);
+    if (d.col_lds > kColLdsMax)
+        return mdp_set_error(MDP_EUNSUPPORTED, "colonisation rows need %zu B of LDS", d.col_lds);
+    if (d.col_lds > 64 * 1024)  // opt in to exactly what the launch uses
+        for (const void *fn : {(const void *)k_colonise<8>, (const void *)k_colonise<16>,
+                               (const void *)k_colonise<24>})
+            HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.col_lds));
+    zs.push_back(0.0);
+    int rc;
+    if ((rc = dev_reserve(&d.zs, &d.cap_zs, zs.size())) || (rc = dev_reserve(&d.jtab, &d.cap_jtab, jtab.size())))
+        return rc;
+    HIP_TRY(hipMemcpy(d.zs, zs.data(), zs.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d.jtab, jtab.data(), jtab.size() * sizeof(uint4), hipMemcpyHostToDevice));
+    d.zs_cmax = cmax;
+    return MDP_OK;
+}
+
 int upload_binomials()  // into the current device's constant bank
 {
     double h[kMaxDeg + 1][kMaxDeg + 1] = {};
@@ -888,6 +1186,18 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
     HIP_TRY(hipStreamSynchronize(d.stream));
     (void)hipFree(dM);
     if (eng->jit) {
+        const uint32_t nvp = colonise_nv(eng->nvar);
+        const size_t nt = eng->task_js.size();
+        std::vector<double> sv(nt * nvp + 1, 0.0);
+        for (size_t t = 0; t < nt; ++t)
+            for (uint32_t b = 0; b < eng->nvar; ++b)
+                sv[t * nvp + b] = eng->Sj[(size_t)eng->task_js[t] * eng->n + eng->var_cols[b]];
+        std::vector<uint32_t> itemB = eng->itemB, qitem = eng->qitem;
+        itemB.push_back(0u);
+        qitem.push_back(0u);
+        if ((rc = dev_upload(&d.sv, sv)) || (rc = dev_upload(&d.itemB, itemB)) ||
+            (rc = dev_upload(&d.qstart, eng->qstart)) || (rc = dev_upload(&d.qitem, qitem)))
+            return rc;
         HIP_TRY(hipModuleLoadData(&d.jit_mod, eng->jit_code.data()));
         HIP_TRY(hipModuleGetFunction(&d.jit_fn, d.jit_mod, "mdp_fwd_jit"));
     }
@@ -908,8 +1218,10 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
 void free_device(DevCtx &d)
 {
     (void)hipSetDevice(d.device);
-    void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog, d.pairPart0, d.partP, d.partK0,
-                    d.e, d.c, d.ZPV, d.R, d.out, d.gpart, d.Qg, d.stamps[0], d.stamps[1], d.stamps[2]};
+    void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog,
+                    d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
+                    d.jtab, d.zs, d.sv, d.Pc, d.itemB, d.qstart, d.qitem,
+                    d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
     for (hipEvent_t ev : d.ev) (void)hipEventDestroy(ev);
@@ -927,18 +1239,24 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
 {
     HIP_TRY(hipSetDevice(d.device));
     int rc;
-    if ((rc = dev_reserve(&d.e, &d.cap_e, ne)) || (rc = dev_reserve(&d.c, &d.cap_c, nc)) ||
-        (rc = dev_reserve(&d.ZPV, &d.cap_zpv, (size_t)nc * (eng->nvar + 1) * eng->nstates)) ||
-        (rc = dev_reserve(&d.R, &d.cap_r, (size_t)nc * ldR_of(eng))))
+    if ((rc = dev_reserve(&d.e, &d.cap_e, ne)) || (rc = dev_reserve(&d.c, &d.cap_c, nc))) return rc;
+    if (eng->jit) {
+        double cmax = 0.0;
+        for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
+        if ((rc = dev_reserve(&d.Pc, &d.cap_pc, (size_t)nc * eng->ldP))) return rc;
+        if (!(d.zs_cmax == cmax) && (rc = upload_colonise_tables(eng, d, cmax))) return rc;
+    } else if ((rc = dev_reserve(&d.ZPV, &d.cap_zpv, (size_t)nc * (eng->nvar + 1) * eng->nstates)) ||
+               (rc = dev_reserve(&d.R, &d.cap_r, (size_t)nc * ldR_of(eng)))) {
         return rc;
-    if (eng->jit && (rc = dev_reserve(&d.Qg, &d.cap_qg, (size_t)nc * eng->ldQ))) return rc;
-    if (!eng->lds_part &&
+    }
+    if (!eng->jit && !eng->lds_part &&
         (rc = dev_reserve(&d.gpart, &d.cap_gpart, (size_t)nc * eng->partP.size() * (eng->nvar + 1))))
         return rc;
     if (eng->diag) {
-        d.nst[0] = (size_t)((eng->nstates + kZpvJ - 1) / kZpvJ) * ((nc + kZpvCT - 1) / kZpvCT);
+        d.nst[0] = eng->jit ? (size_t)((nc + 63) / 64) * ((eng->task_js.size() + kBlock / 64 - 1) / (kBlock / 64))
+                            : (size_t)((eng->nstates + kZpvJ - 1) / kZpvJ) * ((nc + kZpvCT - 1) / kZpvCT);
         d.nst[1] = nc;
-        d.nst[2] = (size_t)nc * ((ne + kBlock - 1) / kBlock);
+        d.nst[2] = (size_t)nc * ((ne + kBlock - 1) / kBlock);  // >= the JIT grid (EPL >= 1)
         for (int k = 0; k < 3; ++k) {
             if ((rc = dev_reserve(&d.stamps[k], &d.cap_st[k], d.nst[k] * kStampSlots))) return rc;
             HIP_TRY(hipMemset(d.stamps[k], 0, d.cap_st[k] * sizeof(unsigned long long)));
@@ -957,11 +1275,11 @@ void launch_fwd_epl(const mdp_engine *eng, const DevCtx &d, double *out, uint32_
     dim3 grid(d.nc, (d.ne + kBlock * EPL - 1) / (kBlock * EPL));
     const uint32_t nprog = (uint32_t)eng->prog.size() - 1;
     if (eng->fwd_lds)
-        hipLaunchKernelGGL((k_forward_lds<NP, DEG, EPL>), grid, dim3(kBlock), eng->fwd_lds_bytes, s,
+        MDP_LAUNCH((k_forward_lds<NP, DEG, EPL>), grid, dim3(kBlock), eng->fwd_lds_bytes, s,
                            d.R, ldR_of(eng), d.prog, nprog, eng->np[0], eng->prior0, d.e, d.ne, out, ld,
                            d.stamps[2]);
     else
-        hipLaunchKernelGGL((k_forward<NP, DEG, EPL>), grid, dim3(kBlock), 0, s, d.R, ldR_of(eng),
+        MDP_LAUNCH((k_forward<NP, DEG, EPL>), grid, dim3(kBlock), 0, s, d.R, ldR_of(eng),
                            d.prog, nprog, eng->np[0], eng->prior0, d.e, d.ne, out, ld);
 }
 
@@ -991,15 +1309,21 @@ int launch_fwd_deg(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
 int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
 {
     int rc;
-    if (eng->jit && d.jit_fn) {
-        const double *Q = d.Qg;
+    if (eng->jit) {
+        const double *Pc = d.Pc;
+        const uint32_t *qs = d.qstart, *qi = d.qitem;
         double prior0 = eng->prior0;
         const double *ev = d.e;
-        uint32_t ne = d.ne, one = 1;
-        void *args[] = {(void *)&Q,   (void *)&prior0, (void *)&ev, (void *)&ne,
-                        (void *)&out, (void *)&ld,     (void *)&one};
-        const unsigned gy = (d.ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
-        HIP_TRY(hipModuleLaunchKernel(d.jit_fn, d.nc, gy, 1, kBlock, 1, 1, 0, s, args, nullptr));
+        uint32_t ne = d.ne, nc = d.nc, one = 1;
+        unsigned long long *st = d.stamps[2];
+        void *args[] = {(void *)&Pc, (void *)&qs,  (void *)&qi, (void *)&prior0, (void *)&ev, (void *)&ne,
+                        (void *)&nc, (void *)&out, (void *)&ld, (void *)&one,    (void *)&st};
+        const uint64_t gy = (d.ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
+        const uint64_t nb = gy * d.nc;
+        if (nb * kBlock > 0xffffffffull)
+            return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
+        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn, (uint32_t)(nb * kBlock), 1, 1, kBlock, 1, 1, 0, s, args,
+                                         nullptr, t_kev.start, t_kev.stop, 0));
         return MDP_OK;
     }
     switch (eng->variant / 100) {
@@ -1018,11 +1342,10 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
 template <bool LDSZ, bool LDSP, int NV>
 void launch_coefs_nv(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_coefs<LDSZ, LDSP, NV>), dim3(d.nc), dim3(kBlock), eng->coef_lds, s, d.ZPV,
+    MDP_LAUNCH((k_coefs<LDSZ, LDSP, NV>), dim3(d.nc), dim3(kBlock), eng->coef_lds, s, d.ZPV,
                        eng->nstates, eng->nvar, d.pairA, d.pairB, d.pairOff, d.pairPart0, eng->npairs,
                        d.partP, d.partK0, (uint32_t)eng->partP.size(), eng->ncoef, d.udesc,
-                       eng->nuses, eng->deg, d.R, ldR_of(eng), d.gpart, eng->jit ? d.Qg : nullptr,
-                       eng->ldQ, d.stamps[1]);
+                       eng->nuses, eng->deg, d.R, ldR_of(eng), d.gpart, d.stamps[1]);
 }
 
 template <bool LDSZ, bool LDSP>
@@ -1061,23 +1384,55 @@ int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
         }
         ev = &d.ev[d.ev_used * kNumEv];
         ++d.ev_used;
-        HIP_TRY(hipEventRecord(ev[kEvBegin], s));
+    }
+    auto timed = [&](int k) { t_kev = prof ? KernelEvents{ev[2 * k], ev[2 * k + 1]} : KernelEvents{}; };
+    struct Reset {
+        ~Reset() { t_kev = KernelEvents{}; }
+    } reset;
+    if (eng->jit) {  // direct path: colonisation factors, then the specialised forward kernel
+        timed(0);
+        const uint32_t ntask = (uint32_t)eng->task_js.size();
+        if (ntask) {
+            const dim3 grid((d.nc + 63) / 64, (ntask + kBlock / 64 - 1) / (kBlock / 64));
+            if (eng->nvar <= 8)
+                MDP_LAUNCH(k_colonise<8>, grid, dim3(kBlock), d.col_lds, s, d.c, d.nc, eng->nvar, d.jtab, ntask,
+                           d.zs, d.sv, d.itemB, d.Pc, (uint32_t)eng->ldP, d.stamps[0]);
+            else if (eng->nvar <= 16)
+                MDP_LAUNCH(k_colonise<16>, grid, dim3(kBlock), d.col_lds, s, d.c, d.nc, eng->nvar, d.jtab, ntask,
+                           d.zs, d.sv, d.itemB, d.Pc, (uint32_t)eng->ldP, d.stamps[0]);
+            else
+                MDP_LAUNCH(k_colonise<24>, grid, dim3(kBlock), d.col_lds, s, d.c, d.nc, eng->nvar, d.jtab, ntask,
+                           d.zs, d.sv, d.itemB, d.Pc, (uint32_t)eng->ldP, d.stamps[0]);
+            HIP_TRY(hipGetLastError());
+        } else if (prof) {
+            HIP_TRY(hipEventRecord(ev[0], s));
+            HIP_TRY(hipEventRecord(ev[1], s));
+        }
+        if (prof) {  // no separate coefficient kernel
+            HIP_TRY(hipEventRecord(ev[2], s));
+            HIP_TRY(hipEventRecord(ev[3], s));
+        }
+        timed(2);
+        return launch_forward(eng, d, out, ld, s);
     }
     {
+        timed(0);
         dim3 grid((eng->nstates + kZpvJ - 1) / kZpvJ, (d.nc + kZpvCT - 1) / kZpvCT);
-        hipLaunchKernelGGL(k_zpv, grid, dim3(kBlock), 0, s, d.S, eng->nstates, eng->n - eng->nvar,
-                           eng->nvar, d.c, d.nc, d.ZPV, d.stamps[0]);
+        MDP_LAUNCH(k_zpv, grid, dim3(kBlock), 0, s, d.S, eng->nstates, eng->n - eng->nvar,
+                   eng->nvar, d.c, d.nc, d.ZPV, d.stamps[0]);
         HIP_TRY(hipGetLastError());
     }
-    if (prof) HIP_TRY(hipEventRecord(ev[kEvZpv], s));
     if (eng->nuses) {
+        timed(1);
         int rc = launch_coefs(eng, d, s);
         if (rc) return rc;
+    } else if (prof) {  // no coefficient kernel: zero-length interval
+        HIP_TRY(hipEventRecord(ev[2], s));
+        HIP_TRY(hipEventRecord(ev[3], s));
     }
-    if (prof) HIP_TRY(hipEventRecord(ev[kEvCoefs], s));
+    timed(2);
     int rc = launch_forward(eng, d, out, ld, s);
     if (rc) return rc;
-    if (prof) HIP_TRY(hipEventRecord(ev[kEvForward], s));
     return MDP_OK;
 }
 
@@ -1086,12 +1441,12 @@ int collect_times(mdp_engine *eng, DevCtx &d)
 {
     if (d.ev_used == 0) return MDP_OK;
     HIP_TRY(hipSetDevice(d.device));
-    HIP_TRY(hipEventSynchronize(d.ev[(d.ev_used - 1) * kNumEv + kEvForward]));
+    HIP_TRY(hipEventSynchronize(d.ev[(d.ev_used - 1) * kNumEv + kNumEv - 1]));
     double sum[3] = {0, 0, 0};
     for (size_t r = 0; r < d.ev_used; ++r)
         for (int k = 0; k < 3; ++k) {
             float ms = 0;
-            HIP_TRY(hipEventElapsedTime(&ms, d.ev[r * kNumEv + k], d.ev[r * kNumEv + k + 1]));
+            HIP_TRY(hipEventElapsedTime(&ms, d.ev[r * kNumEv + 2 * k], d.ev[r * kNumEv + 2 * k + 1]));
             sum[k] += ms;
         }
     for (int k = 0; k < 3; ++k) eng->last_ms[k] = sum[k] / (double)d.ev_used;
@@ -1133,14 +1488,25 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
     if (const char *ev = getenv("MDP_DIAG")) eng->diag = atoi(ev) != 0;
     {
         const char *jv = getenv("MDP_JIT");
-        const bool want = !(jv && !strcmp(jv, "0")) && !eng->diag;
-        eng->ldQ = ((size_t)eng->ncoef + 1) & ~(size_t)1;
-        if (want && eng->nuses > 0 && eng->nuses <= kJitMaxUses &&
-            eng->ldQ * sizeof(double) <= kJitMaxLds) {
+        const bool want = !(jv && !strcmp(jv, "0"));
+        bool want_jit = want && build_direct_plan(eng, p) == MDP_OK;
+        if (want_jit) {  // colonisation rows without pruning must fit the LDS
+            const uint32_t z = ((eng->n - eng->nvar) + 7u) & ~7u;
+            want_jit = colonise_lds(eng, std::vector<uint32_t>(eng->nj, z)) <= kColLdsMax;
+        }
+        eng->ldQ = ((size_t)eng->ncoef_d + 1) & ~(size_t)1;
+        if (want_jit && eng->nuses > 0 && eng->nuses <= kJitMaxUses &&
+            (eng->ldQ + eng->ldP) * sizeof(double) + (eng->ncoef_d + 1 + eng->qitem.size()) * 4 <=
+                kJitMaxLds) {
             MdpJitPlan plan;
             plan.np = eng->np;
-            plan.udesc = eng->udesc;
+            plan.udesc = eng->udesc_d;
             plan.ldQ = eng->ldQ;
+            plan.ncoef = eng->ncoef_d;
+            plan.ldP = eng->ldP;
+            plan.nqi = eng->qitem.size();
+            plan.diag = eng->diag;
+            if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
             if (const char *ev = getenv("MDP_EPL")) plan.epl = atoi(ev);
             if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
             const std::string src = mdp_jit_forward_source(plan);
@@ -1250,11 +1616,17 @@ int mdp_engine_diag_report(mdp_engine *eng, char *buf, size_t len)
     DevCtx &d = eng->devs[0];
     HIP_TRY(hipSetDevice(d.device));
     HIP_TRY(hipDeviceSynchronize());
-    static const char *names[3] = {"k_zpv", "k_coefs", "k_forward_lds"};
-    static const int slots[3] = {3, 5, 3};
+    const char *names[3] = {"k_zpv", "k_coefs", "k_forward_lds"};
+    int slots[3] = {3, 5, 3};
+    if (eng->jit) {  // direct path: k_colonise and the hipRTC forward kernel
+        names[0] = "k_colonise";
+        names[2] = "k_forward(jit)";
+        slots[0] = slots[2] = 4;
+        slots[1] = 0;
+    }
     size_t used = 0;
     for (int k = 0; k < 3; ++k) {
-        if (!d.stamps[k] || !d.nst[k]) continue;
+        if (!d.stamps[k] || !d.nst[k] || !slots[k]) continue;
         std::vector<unsigned long long> h(d.nst[k] * kStampSlots);
         HIP_TRY(hipMemcpy(h.data(), d.stamps[k], h.size() * sizeof(unsigned long long),
                           hipMemcpyDeviceToHost));
@@ -1283,7 +1655,7 @@ int mdp_engine_diag_report(mdp_engine *eng, char *buf, size_t len)
             w = snprintf(buf + used, len - used, " ph%d=%.0f", q, nb ? mean[q] / nb : 0.0);
             if (w > 0) used = std::min(len - 1, used + (size_t)w);
         }
-        if (k == 2 && nb) {  // forward: cycles summed over run ops / general ops (wave 0)
+        if (k == 2 && nb && !eng->jit) {  // forward: cycles summed over run ops / general ops (wave 0)
             double cr = 0, cg = 0;
             for (size_t b = 0; b < d.nst[k]; ++b) {
                 const unsigned long long *st = &h[b * kStampSlots];
@@ -1320,9 +1692,9 @@ int mdp_engine_kernel_ms(mdp_engine *eng, double *ms, int max_k)
     return k;
 }
 
-const char *mdp_engine_kernel_name(int k)
+const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
-    return (k >= 0 && k < 3) ? kKernelNames[k] : "";
+    return (eng && k >= 0 && k < 3) ? kKernelNames[eng->jit ? 1 : 0][k] : "";
 }
 
 int mdp_engine_get_info(const mdp_engine *eng, mdp_engine_info *info)
@@ -1362,7 +1734,7 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     // compulsory bytes of k_forward: its coefficient stream once per c, the
     // e values, the output
     if (bytes_min)
-        *bytes_min = 8.0 * ((double)nc * (eng->jit ? eng->ldQ : ldR_of(eng)) + (double)ne + pts);
+        *bytes_min = 8.0 * ((double)nc * (eng->jit ? eng->ldP : ldR_of(eng)) + (double)ne + pts);
     return MDP_OK;
 }
 

@@ -110,26 +110,58 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     o << kPrelude;
     o << "#define EPL " << EPL << "\n#define LDQ " << pl.ldQ << "\n#define NPMAX " << npmax
       << "\n#define DMAX " << dmax << "\n#define NW " << (nw ? nw : 1) << "\n";
+    o << "#define LDP " << pl.ldP << "\n#define NCOEF " << pl.ncoef << "\n#define NQI " << (pl.nqi ? pl.nqi : 1)
+      << "\n";
+    // diagnostic phase stamps: s_memtime (slots 0-3) and s_memrealtime (6, 7)
+    auto stamp = [&](int slot) {
+        if (!pl.diag) return std::string();
+        return std::string("    if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * 8 + ") +
+               std::to_string(slot) + "] = " +
+               (slot >= 6 ? "__builtin_amdgcn_s_memrealtime();\n" : "__builtin_amdgcn_s_memtime();\n");
+    };
     o << "extern \"C\" __global__ __launch_bounds__(KBLOCK) void mdp_fwd_jit(\n"
-         "    const double *__restrict__ Q, double prior0, const double *__restrict__ evals, u32 ne,\n"
-         "    double *__restrict__ out, u32 ld_out, u32 one)\n{\n"
+         "    const double *__restrict__ Pc, const u32 *__restrict__ qstart, const u32 *__restrict__ qitem,\n"
+         "    double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
+         "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps)\n{\n"
+         "    __shared__ __attribute__((aligned(16))) double Pl[LDP];\n"
          "    __shared__ __attribute__((aligned(16))) double Ql[LDQ];\n"
-         "    const u32 ic = blockIdx.x;\n"
+         "    __shared__ u32 Qs[NCOEF + 1];\n"
+         "    __shared__ u32 Qi[NQI];\n"
+         // XCD-aware order: the dispatcher deals blocks round-robin over the 8
+         // XCDs, so consecutive logical blocks (adjacent c columns of the
+         // output rows) are given to one XCD and its L2 assembles whole lines
+         << stamp(6) << stamp(0) <<
+         "    const u32 nb = gridDim.x, full = nb & ~7u;\n"
+      << (pl.xcd ? "    const u32 lb = blockIdx.x < full ? (blockIdx.x & 7u) * (full >> 3) + (blockIdx.x >> 3) : blockIdx.x;\n"
+                 : "    const u32 lb = blockIdx.x + 0 * full;\n") <<
+         "    const u32 ic = lb % nc, by = lb / nc;\n"
          "    {\n"
-         "        const double2 *src = (const double2 *)(Q + (size_t)ic * LDQ);\n"
-         "        double2 *dst = (double2 *)Ql;\n"
-         "        for (u32 i0 = threadIdx.x; i0 < LDQ / 2; i0 += 2 * KBLOCK) {\n"
+         "        const double2 *src = (const double2 *)(Pc + (size_t)ic * LDP);\n"
+         "        double2 *dst = (double2 *)Pl;\n"
+         "        for (u32 i0 = threadIdx.x; i0 < LDP / 2; i0 += 2 * KBLOCK) {\n"
          "            const u32 i1 = i0 + KBLOCK;\n"
          "            const double2 t0 = src[i0];\n"
-         "            const double2 t1 = src[i1 < LDQ / 2 ? i1 : i0];\n"
+         "            const double2 t1 = src[i1 < LDP / 2 ? i1 : i0];\n"
          "            dst[i0] = t0;\n"
-         "            if (i1 < LDQ / 2) dst[i1] = t1;\n"
+         "            if (i1 < LDP / 2) dst[i1] = t1;\n"
          "        }\n"
+         "        for (u32 i = threadIdx.x; i <= NCOEF; i += KBLOCK) Qs[i] = qstart[i];\n"
+         "        for (u32 i = threadIdx.x; i < NQI; i += KBLOCK) Qi[i] = qitem[i];\n"
+         "    }\n"
+         "    __syncthreads();\n"
+         << stamp(1) <<
+         // Q_ab[m] = sum over the pair's hidden states j (|j| = m, ascending)
+         // of Pc[j][b]: fixed order, deterministic
+         "    for (u32 q = threadIdx.x; q < LDQ; q += KBLOCK) {\n"
+         "        double a = 0.0;\n"
+         "        if (q < NCOEF)\n"
+         "            for (u32 i = Qs[q], i1 = Qs[q + 1]; i < i1; ++i) a += Pl[Qi[i]];\n"
+         "        Ql[q] = a;\n"
          "    }\n"
          "    u32 ie[EPL];\n    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n"
          "#pragma unroll\n"
          "    for (int i = 0; i < EPL; ++i) {\n"
-         "        ie[i] = blockIdx.y * (KBLOCK * EPL) + i * KBLOCK + threadIdx.x;\n"
+         "        ie[i] = by * (KBLOCK * EPL) + i * KBLOCK + threadIdx.x;\n"
          "        const double e = ie[i] < ne ? evals[ie[i]] : 0.0;\n"
          "        const double x = e > 1.0 ? 1.0 : e;\n"
          "        const double y = 1.0 - x;\n"
@@ -141,7 +173,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     o << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < " << np0
       << " ? 1.0 : 0.0;\n"
          "    }\n"
-         "    __syncthreads();\n";
+         "    __syncthreads();\n"
+      << stamp(2);
     // P = sum_m Q[off+m] W[|A|][m] as an expression for point i
     auto pexpr = [&](uint32_t d) {
         const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u, nA = d >> 27;
@@ -189,14 +222,15 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         }
         o << "    }\n";
     }
-    o << "    }}\n";
+    o << "    }}\n" << stamp(3);
     o << "#pragma unroll\n"
          "    for (int i = 0; i < EPL; ++i) {\n"
          "        double L = 0.0;\n"
          "#pragma unroll\n"
          "        for (int l = 0; l < NPMAX; ++l) L += v[i][l] * prior0;\n"
          "        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
-         "    }\n}\n";
+         "    }\n"
+      << stamp(7) << "}\n";
     o << "// EPL_CHOSEN " << EPL << "\n";
     return o.str();
 }

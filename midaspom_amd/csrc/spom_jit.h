@@ -9,9 +9,14 @@
 struct MdpJitPlan {
     std::vector<uint32_t> np;     // possible states per year
     std::vector<uint32_t> udesc;  // per forward use: Q offset | nX << 22 | nA << 27
-    size_t ldQ = 0;               // per-c coefficient block (doubles, even)
+    size_t ldQ = 0;               // Q block in LDS (doubles, even)
+    size_t ncoef = 0;             // Q entries assembled from the colonisation factors
+    size_t ldP = 0;               // per-c colonisation-factor row Pc[c][item] (doubles, even)
+    size_t nqi = 0;               // length of the Q-assembly item list (qitem)
     int epl = 0;                  // grid points per lane (0: 2 unless the weight table is large)
     int window = 8;               // transitions per scheduling region
+    bool diag = false;            // record s_memtime phase stamps (MDP_DIAG)
+    bool xcd = true;              // XCD-aware block order
 };
 
 // HIP source of `mdp_fwd_jit` for this plan; sets plan.epl when it was 0.

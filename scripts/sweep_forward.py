@@ -23,10 +23,9 @@ import midaspom_amd as mdp  # noqa: E402
 from midaspom_amd import synth  # noqa: E402
 
 DEFAULT_VARIANTS = ";".join([
-    "MDP_JIT=1,MDP_JIT_WINDOW=8",
+    "MDP_JIT=1",
+    "MDP_JIT=1,MDP_EPL=1",
     "MDP_JIT=1,MDP_JIT_WINDOW=16",
-    "MDP_JIT=1,MDP_JIT_WINDOW=4",
-    "MDP_JIT=1,MDP_EPL=2,MDP_JIT_WINDOW=8",
     "MDP_JIT=0,MDP_EPL=2",
 ])
 

@@ -123,8 +123,19 @@ def test_q5_impossible_transition(tmp_path):
 # ---------------------------------------------------------------------------
 # fuzzing: random problems covering every forward-kernel variant
 # ---------------------------------------------------------------------------
+@pytest.fixture(params=["direct", "generic"])
+def engine_path(request, monkeypatch):
+    """Both engine paths: the direct one (k_colonise + hipRTC-specialised
+    forward kernel, the default) and the generic kernels (MDP_JIT=0)."""
+    if request.param == "generic":
+        monkeypatch.setenv("MDP_JIT", "0")
+    else:
+        monkeypatch.delenv("MDP_JIT", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("seed", range(24))
-def test_random_problems(seed):
+def test_random_problems(seed, engine_path):
     rng = np.random.default_rng(1000 + seed)
     n = int(rng.integers(2, 48))
     nvar = int(rng.integers(1, min(n, 10) + 1))
@@ -144,7 +155,7 @@ def test_random_problems(seed):
     assert_loglik_close(got, ref)
 
 
-def test_single_year_and_constant_series():
+def test_single_year_and_constant_series(engine_path):
     for obs in (np.array([[1, 0, -1, 1]]), np.array([[0, 1, 1]] * 6), np.array([[1], [1], [0], [1]])):
         model = mdp.Model.from_obs(obs)
         g, _ = mdp.grid(7)
@@ -217,8 +228,25 @@ def test_device_run_matches_host_path(golden):
         torch.cuda.synchronize()
         ms = eng.kernel_ms()
     assert np.array_equal(out[:, :96].cpu().numpy(), host)
-    assert set(ms) == {"k_zpv", "k_coefs", "k_forward"}
+    assert set(ms) in ({"k_colonise", "k_forward"}, {"k_zpv", "k_coefs", "k_forward"})
     assert all(v > 0 for v in ms.values())
+
+
+@pytest.mark.parametrize("fname,s", [("config2_64x50.txt", 256), ("config3_256x200.txt", 128)])
+def test_direct_and_generic_paths_agree(golden, monkeypatch, fname, s):
+    model = mdp.Model.load(golden / fname)
+    g, _ = mdp.grid(s, 0.0, 1.0)
+    c, _ = mdp.grid(s + 1, 0.0, 1.5)
+    monkeypatch.delenv("MDP_JIT", raising=False)
+    with mdp.Engine(model) as eng:
+        assert eng.info()["variant"] >= 10000  # the direct path is the default
+        a = eng.loglik_grid(g, c)
+        assert set(eng.kernel_ms()) <= {"k_colonise", "k_forward"}
+    monkeypatch.setenv("MDP_JIT", "0")
+    with mdp.Engine(model) as eng:
+        assert eng.info()["variant"] < 10000
+        b = eng.loglik_grid(g, c)
+    assert_loglik_close(a, b, atol=1e-11)
 
 
 def test_explicit_device_list(golden):
