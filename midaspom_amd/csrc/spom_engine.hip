@@ -310,6 +310,44 @@ __global__ __launch_bounds__(kBlock) void k_colonise(
     MDP_RSTAMP(stamps, 7);
 }
 
+// Q rows of the direct path: Q[c][q] = sum of the items qitem[qstart[q] ..
+// qstart[q + 1]) of the Pc row (ascending j within each (pair, m) entry:
+// fixed order, deterministic).  A workgroup stages the CSR lists once and
+// assembles kQsumC consecutive c rows from LDS copies of their Pc rows.
+constexpr uint32_t kQsumC = 2;
+__global__ __launch_bounds__(kBlock) void k_qsum(const double *__restrict__ Pc, uint32_t ldP,
+                                                 const uint32_t *__restrict__ qstart,
+                                                 const uint32_t *__restrict__ qitem, uint32_t ncoef,
+                                                 uint32_t nqi, double *__restrict__ Q, uint32_t ldQ,
+                                                 uint32_t nc)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double *Pl = lds;  // [kQsumC][ldP]
+    uint32_t *Qs = (uint32_t *)(lds + (size_t)kQsumC * ldP);
+    uint32_t *Qi = Qs + ncoef + 1;
+    const uint32_t c0 = blockIdx.x * kQsumC, rows = min(kQsumC, nc - c0);
+    {
+        const double2 *src = (const double2 *)(Pc + (size_t)c0 * ldP);
+        double2 *dst = (double2 *)Pl;
+        const uint32_t n2 = rows * ldP / 2;
+#pragma unroll 4
+        for (uint32_t i = threadIdx.x; i < n2; i += kBlock) dst[i] = src[i];
+    }
+    for (uint32_t i = threadIdx.x; i <= ncoef; i += kBlock) Qs[i] = qstart[i];
+    for (uint32_t i = threadIdx.x; i < nqi; i += kBlock) Qi[i] = qitem[i];
+    __syncthreads();
+    for (uint32_t r = 0; r < rows; ++r) {
+        const double *pr = Pl + (size_t)r * ldP;
+        double *qr = Q + (size_t)(c0 + r) * ldQ;
+        for (uint32_t q = threadIdx.x; q < ldQ; q += kBlock) {
+            double a = 0.0;
+            if (q < ncoef)
+                for (uint32_t i = Qs[q], i1 = Qs[q + 1]; i < i1; ++i) a += pr[Qi[i]];
+            qr[q] = a;
+        }
+    }
+}
+
 // One workgroup per c value.
 //  1. stage this c's Z/PV block (LDS_ZPV) and the binomial table in LDS;
 //  2. subset products: lane per part (pair p, 16 consecutive subset indexes k
@@ -763,7 +801,7 @@ int dev_reserve(T **p, size_t *cap, size_t count)
 
 constexpr int kNumEv = 6;  // start/stop per kernel: k_zpv, k_coefs, k_forward
 const char *const kKernelNames[2][3] = {{"k_zpv", "k_coefs", "k_forward"},
-                                        {"k_colonise", "", "k_forward"}};
+                                        {"k_colonise", "k_qsum", "k_forward"}};
 
 struct DevCtx {
     int device = 0;
@@ -782,13 +820,14 @@ struct DevCtx {
     size_t nst[3] = {0, 0, 0};
     // direct path: colonisation tables (jtab / zs depend on the grid's c range)
     uint4 *jtab = nullptr;
-    double *zs = nullptr, *sv = nullptr, *Pc = nullptr;
+    double *zs = nullptr, *sv = nullptr, *Pc = nullptr, *Qrow = nullptr;
     uint32_t *itemB = nullptr, *qstart = nullptr, *qitem = nullptr;
-    size_t cap_jtab = 0, cap_zs = 0, cap_pc = 0;
+    size_t cap_jtab = 0, cap_zs = 0, cap_pc = 0, cap_qrow = 0;
     size_t col_lds = 0;     // k_colonise dynamic LDS: largest workgroup's S rows + item masks
     double zs_cmax = -1.0;  // c bound the uploaded zs was pruned for (-1: none yet)
-    hipModule_t jit_mod = nullptr;   // problem-specialised forward kernel
-    hipFunction_t jit_fn = nullptr;
+    hipModule_t jit_mod[2] = {nullptr, nullptr};  // problem-specialised forward kernel [qsum]
+    hipFunction_t jit_fn[2] = {nullptr, nullptr};
+    bool use_qsum = false;  // this grid's direct path runs k_qsum (several e blocks per c)
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     size_t ev_used = 0;          // event sets recorded since the last collect
 };
@@ -809,10 +848,14 @@ struct mdp_engine {
     bool jit = false;         // forward kernel specialised with hipRTC (spom_jit.cpp)
     int jit_epl = 1;          // its grid points per lane
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
-    std::vector<char> jit_code;
+    std::vector<char> jit_code[2];  // forward kernel code objects [qsum], compiled on demand
+    MdpJitPlan jit_plan;
+    int qsum_mode = -1;  // MDP_QSUM: -1 auto (k_qsum when a c column spans several e blocks), 0, 1
     // direct path (jit): k_colonise computes Pc[j][b] for the needed (j, b)
     // items, the forward kernel assembles Q from them
     uint32_t nj = 0, nitems = 0, ncoef_d = 0;
+    bool qsum_ok = true;  // k_qsum fits the LDS
+    size_t qsum_lds = 0;
     size_t ldP = 0;
     std::vector<uint32_t> cj_bits, cj_item0, itemB, qstart, qitem, udesc_d, var_cols;
     std::vector<uint32_t> task_js, task_item0;  // k_colonise tasks: j slot, first item (+ end)
@@ -1143,6 +1186,38 @@ int upload_colonise_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     return MDP_OK;
 }
 
+// Compile (hipRTC, cached) the forward kernel variant `qsum` of the engine's plan.
+int jit_build(mdp_engine *eng, bool qsum)
+{
+    if (!eng->jit_code[qsum].empty()) return MDP_OK;
+    MdpJitPlan plan = eng->jit_plan;
+    plan.qsum = qsum;
+    const std::string src = mdp_jit_forward_source(plan);
+    eng->jit_epl = plan.epl;
+    if (const char *dump = getenv("MDP_JIT_DUMP")) {
+        if (FILE *f = fopen(dump, "w")) {
+            fputs(src.c_str(), f);
+            fclose(f);
+        }
+    }
+    if (mdp_jit_compile(src, eng->jit_code[qsum], eng->jit_log) != 0)
+        return mdp_set_error(MDP_EHIP, "hipRTC compilation of the forward kernel failed: %s",
+                             eng->jit_log.c_str());
+    return MDP_OK;
+}
+
+// Load the forward kernel variant into the device (compiling it if needed).
+int jit_load(mdp_engine *eng, DevCtx &d, bool qsum)
+{
+    if (d.jit_fn[qsum]) return MDP_OK;
+    int rc = jit_build(eng, qsum);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(d.device));
+    HIP_TRY(hipModuleLoadData(&d.jit_mod[qsum], eng->jit_code[qsum].data()));
+    HIP_TRY(hipModuleGetFunction(&d.jit_fn[qsum], d.jit_mod[qsum], "mdp_fwd_jit"));
+    return MDP_OK;
+}
+
 int upload_binomials()  // into the current device's constant bank
 {
     double h[kMaxDeg + 1][kMaxDeg + 1] = {};
@@ -1198,8 +1273,10 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
         if ((rc = dev_upload(&d.sv, sv)) || (rc = dev_upload(&d.itemB, itemB)) ||
             (rc = dev_upload(&d.qstart, eng->qstart)) || (rc = dev_upload(&d.qitem, qitem)))
             return rc;
-        HIP_TRY(hipModuleLoadData(&d.jit_mod, eng->jit_code.data()));
-        HIP_TRY(hipModuleGetFunction(&d.jit_fn, d.jit_mod, "mdp_fwd_jit"));
+        if (eng->qsum_lds > 64 * 1024)
+            HIP_TRY(hipFuncSetAttribute((const void *)k_qsum, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)eng->qsum_lds));
+        if ((rc = jit_load(eng, d, eng->qsum_mode == 1))) return rc;
     }
     if (eng->coef_lds > 64 * 1024) {
         const void *fns[] = {
@@ -1220,12 +1297,13 @@ void free_device(DevCtx &d)
     (void)hipSetDevice(d.device);
     void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog,
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
-                    d.jtab, d.zs, d.sv, d.Pc, d.itemB, d.qstart, d.qitem,
+                    d.jtab, d.zs, d.sv, d.Pc, d.Qrow, d.itemB, d.qstart, d.qitem,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
     for (hipEvent_t ev : d.ev) (void)hipEventDestroy(ev);
-    if (d.jit_mod) (void)hipModuleUnload(d.jit_mod);
+    for (hipModule_t m : d.jit_mod)
+        if (m) (void)hipModuleUnload(m);
     if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -1244,6 +1322,10 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         double cmax = 0.0;
         for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
         if ((rc = dev_reserve(&d.Pc, &d.cap_pc, (size_t)nc * eng->ldP))) return rc;
+        const uint32_t gy = (ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
+        d.use_qsum = eng->qsum_mode == 1 || (eng->qsum_mode == -1 && gy > 1);
+        if ((rc = jit_load(eng, d, d.use_qsum))) return rc;
+        if (d.use_qsum && (rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ))) return rc;
         if (!(d.zs_cmax == cmax) && (rc = upload_colonise_tables(eng, d, cmax))) return rc;
     } else if ((rc = dev_reserve(&d.ZPV, &d.cap_zpv, (size_t)nc * (eng->nvar + 1) * eng->nstates)) ||
                (rc = dev_reserve(&d.R, &d.cap_r, (size_t)nc * ldR_of(eng)))) {
@@ -1310,7 +1392,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
 {
     int rc;
     if (eng->jit) {
-        const double *Pc = d.Pc;
+        const double *Pc = d.use_qsum ? d.Qrow : d.Pc;
         const uint32_t *qs = d.qstart, *qi = d.qitem;
         double prior0 = eng->prior0;
         const double *ev = d.e;
@@ -1322,7 +1404,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
         const uint64_t nb = gy * d.nc;
         if (nb * kBlock > 0xffffffffull)
             return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
-        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn, (uint32_t)(nb * kBlock), 1, 1, kBlock, 1, 1, 0, s, args,
+        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.use_qsum], (uint32_t)(nb * kBlock), 1, 1, kBlock, 1, 1, 0, s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));
         return MDP_OK;
     }
@@ -1408,7 +1490,13 @@ int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
             HIP_TRY(hipEventRecord(ev[0], s));
             HIP_TRY(hipEventRecord(ev[1], s));
         }
-        if (prof) {  // no separate coefficient kernel
+        if (d.use_qsum && eng->nitems) {
+            timed(1);
+            MDP_LAUNCH(k_qsum, dim3((d.nc + kQsumC - 1) / kQsumC), dim3(kBlock), eng->qsum_lds, s, d.Pc,
+                       (uint32_t)eng->ldP, d.qstart, d.qitem, eng->ncoef_d, (uint32_t)eng->qitem.size(),
+                       d.Qrow, (uint32_t)eng->ldQ, d.nc);
+            HIP_TRY(hipGetLastError());
+        } else if (prof) {  // no separate coefficient kernel
             HIP_TRY(hipEventRecord(ev[2], s));
             HIP_TRY(hipEventRecord(ev[3], s));
         }
@@ -1498,7 +1586,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
         if (want_jit && eng->nuses > 0 && eng->nuses <= kJitMaxUses &&
             (eng->ldQ + eng->ldP) * sizeof(double) + (eng->ncoef_d + 1 + eng->qitem.size()) * 4 <=
                 kJitMaxLds) {
-            MdpJitPlan plan;
+            MdpJitPlan &plan = eng->jit_plan;
             plan.np = eng->np;
             plan.udesc = eng->udesc_d;
             plan.ldQ = eng->ldQ;
@@ -1506,18 +1594,16 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             plan.ldP = eng->ldP;
             plan.nqi = eng->qitem.size();
             plan.diag = eng->diag;
+            if (const char *qv = getenv("MDP_QSUM")) eng->qsum_mode = atoi(qv) != 0;
+            eng->qsum_lds = kQsumC * eng->ldP * sizeof(double) + (eng->ncoef_d + 1 + eng->qitem.size()) * 4;
+            eng->qsum_ok = eng->qsum_lds <= kColLdsMax;
+            if (!eng->qsum_ok) eng->qsum_mode = 0;
+            if (const char *cv = getenv("MDP_JIT_SLOTS")) plan.slots = atoi(cv);
             if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
             if (const char *ev = getenv("MDP_EPL")) plan.epl = atoi(ev);
             if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
-            const std::string src = mdp_jit_forward_source(plan);
-            eng->jit_epl = plan.epl;
-            if (getenv("MDP_JIT_DUMP")) {
-                if (FILE *f = fopen(getenv("MDP_JIT_DUMP"), "w")) {
-                    fputs(src.c_str(), f);
-                    fclose(f);
-                }
-            }
-            if (mdp_jit_compile(src, eng->jit_code, eng->jit_log) == 0) eng->jit = true;
+            // compile the variant a small grid uses now (the other on demand)
+            if (jit_build(eng, eng->qsum_mode == 1) == MDP_OK) eng->jit = true;
             else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the generic kernel:\n%s\n",
                          eng->jit_log.c_str());
         }
@@ -1694,7 +1780,9 @@ int mdp_engine_kernel_ms(mdp_engine *eng, double *ms, int max_k)
 
 const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
-    return (eng && k >= 0 && k < 3) ? kKernelNames[eng->jit ? 1 : 0][k] : "";
+    if (!eng || k < 0 || k >= 3) return "";
+    if (eng->jit && k == 1 && (eng->devs.empty() || !eng->devs[0].use_qsum)) return "";
+    return kKernelNames[eng->jit ? 1 : 0][k];
 }
 
 int mdp_engine_get_info(const mdp_engine *eng, mdp_engine_info *info)

@@ -19,6 +19,7 @@
 #include <map>
 #include <mutex>
 #include <sstream>
+#include <cstdint>
 #include <string>
 #include <sys/stat.h>
 #include <vector>
@@ -123,41 +124,51 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    const double *__restrict__ Pc, const u32 *__restrict__ qstart, const u32 *__restrict__ qitem,\n"
          "    double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
          "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps)\n{\n"
-         "    __shared__ __attribute__((aligned(16))) double Pl[LDP];\n"
          "    __shared__ __attribute__((aligned(16))) double Ql[LDQ];\n"
-         "    __shared__ u32 Qs[NCOEF + 1];\n"
-         "    __shared__ u32 Qi[NQI];\n"
+      << stamp(6) << stamp(0) <<
          // XCD-aware order: the dispatcher deals blocks round-robin over the 8
          // XCDs, so consecutive logical blocks (adjacent c columns of the
          // output rows) are given to one XCD and its L2 assembles whole lines
-         << stamp(6) << stamp(0) <<
          "    const u32 nb = gridDim.x, full = nb & ~7u;\n"
       << (pl.xcd ? "    const u32 lb = blockIdx.x < full ? (blockIdx.x & 7u) * (full >> 3) + (blockIdx.x >> 3) : blockIdx.x;\n"
                  : "    const u32 lb = blockIdx.x + 0 * full;\n") <<
-         "    const u32 ic = lb % nc, by = lb / nc;\n"
-         "    {\n"
-         "        const double2 *src = (const double2 *)(Pc + (size_t)ic * LDP);\n"
-         "        double2 *dst = (double2 *)Pl;\n"
-         "        for (u32 i0 = threadIdx.x; i0 < LDP / 2; i0 += 2 * KBLOCK) {\n"
-         "            const u32 i1 = i0 + KBLOCK;\n"
-         "            const double2 t0 = src[i0];\n"
-         "            const double2 t1 = src[i1 < LDP / 2 ? i1 : i0];\n"
-         "            dst[i0] = t0;\n"
-         "            if (i1 < LDP / 2) dst[i1] = t1;\n"
-         "        }\n"
-         "        for (u32 i = threadIdx.x; i <= NCOEF; i += KBLOCK) Qs[i] = qstart[i];\n"
-         "        for (u32 i = threadIdx.x; i < NQI; i += KBLOCK) Qi[i] = qitem[i];\n"
-         "    }\n"
-         "    __syncthreads();\n"
-         << stamp(1) <<
-         // Q_ab[m] = sum over the pair's hidden states j (|j| = m, ascending)
-         // of Pc[j][b]: fixed order, deterministic
-         "    for (u32 q = threadIdx.x; q < LDQ; q += KBLOCK) {\n"
-         "        double a = 0.0;\n"
-         "        if (q < NCOEF)\n"
-         "            for (u32 i = Qs[q], i1 = Qs[q + 1]; i < i1; ++i) a += Pl[Qi[i]];\n"
-         "        Ql[q] = a;\n"
-         "    }\n"
+         "    const u32 ic = lb % nc, by = lb / nc;\n";
+    // stage n doubles from src (16-byte aligned, n even) into the LDS array dst
+    auto stage = [&](const char *dst, const char *src, const char *n) {
+        o << "    {\n"
+             "        const double2 *src_ = (const double2 *)(" << src << ");\n"
+             "        double2 *dst_ = (double2 *)" << dst << ";\n"
+             "        for (u32 i0 = threadIdx.x; i0 < " << n << " / 2; i0 += 2 * KBLOCK) {\n"
+             "            const u32 i1 = i0 + KBLOCK;\n"
+             "            const double2 t0 = src_[i0];\n"
+             "            const double2 t1 = src_[i1 < " << n << " / 2 ? i1 : i0];\n"
+             "            dst_[i0] = t0;\n"
+             "            if (i1 < " << n << " / 2) dst_[i1] = t1;\n"
+             "        }\n"
+             "    }\n";
+    };
+    if (pl.qsum) {  // Q rows from k_qsum (the first pointer argument)
+        stage("Ql", "Pc + (size_t)ic * LDQ", "LDQ");
+        o << stamp(1);
+    } else {
+        o << "    __shared__ __attribute__((aligned(16))) double Pl[LDP];\n"
+             "    __shared__ u32 Qs[NCOEF + 1];\n"
+             "    __shared__ u32 Qi[NQI];\n";
+        stage("Pl", "Pc + (size_t)ic * LDP", "LDP");
+        o << "    for (u32 i = threadIdx.x; i <= NCOEF; i += KBLOCK) Qs[i] = qstart[i];\n"
+             "    for (u32 i = threadIdx.x; i < NQI; i += KBLOCK) Qi[i] = qitem[i];\n"
+             "    __syncthreads();\n"
+          << stamp(1) <<
+             // Q_ab[m] = sum over the pair's hidden states j (|j| = m,
+             // ascending) of Pc[j][b]: fixed order, deterministic
+             "    for (u32 q = threadIdx.x; q < LDQ; q += KBLOCK) {\n"
+             "        double a = 0.0;\n"
+             "        if (q < NCOEF)\n"
+             "            for (u32 i = Qs[q], i1 = Qs[q + 1]; i < i1; ++i) a += Pl[Qi[i]];\n"
+             "        Ql[q] = a;\n"
+             "    }\n";
+    }
+    o <<
          "    u32 ie[EPL];\n    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n"
          "#pragma unroll\n"
          "    for (int i = 0; i < EPL; ++i) {\n"
@@ -191,6 +202,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     const int window = pl.window > 0 ? pl.window : 8;
     const char *guard =
         "    { u32 g_; asm volatile(\"s_mov_b32 %0, %1\" : \"=s\"(g_) : \"s\"(one)); if (g_) {\n";
+    if (pl.slots > 0) o << "    double pc[EPL][" << pl.slots << "];\n";
     o << guard;
     int since = 0;
     auto fence = [&]() {
@@ -199,20 +211,61 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             since = 0;
         }
     };
+    // Transition cache: a use whose pair (same descriptor = same P) recurs
+    // within kHorizon uses keeps its P in one of pl.slots registers; later
+    // uses read it.  Slots are evicted farthest-next-use first.  The P values
+    // are computed exactly as inline, so results do not change.
+    const size_t nu = pl.udesc.size();
+    const int nslot = pl.slots > 0 ? pl.slots : 0;
+    const size_t kHorizon = 64;
+    std::vector<size_t> next_use(nu, SIZE_MAX);
+    {
+        std::map<uint32_t, size_t> last;
+        for (size_t i = nu; i-- > 0;) {
+            auto it = last.find(pl.udesc[i]);
+            if (it != last.end()) next_use[i] = it->second;
+            last[pl.udesc[i]] = i;
+        }
+    }
+    std::vector<uint32_t> slot_key(nslot, 0);
+    std::vector<size_t> slot_next(nslot, SIZE_MAX);  // SIZE_MAX: free / dead
+    // returns the expression for use u, emitting "pc[i][s] = P;" first when
+    // the use fills a slot (inside the caller's per-point loop)
+    auto use_expr = [&](size_t u, std::string &pre) -> std::string {
+        const uint32_t d = pl.udesc[u];
+        for (int sl = 0; sl < nslot; ++sl)
+            if (slot_next[sl] == u && slot_key[sl] == d) {
+                slot_next[sl] = next_use[u];
+                return "pc[i][" + std::to_string(sl) + "]";
+            }
+        const std::string e = pexpr(d);
+        if (nslot == 0 || next_use[u] == SIZE_MAX || next_use[u] - u > kHorizon) return "(" + e + ")";
+        int best = 0;
+        for (int sl = 1; sl < nslot; ++sl)
+            if (slot_next[sl] > slot_next[best]) best = sl;
+        if (slot_next[best] != SIZE_MAX && slot_next[best] <= next_use[u]) return "(" + e + ")";
+        slot_key[best] = d;
+        slot_next[best] = next_use[u];
+        pre = "pc[i][" + std::to_string(best) + "] = " + e + "; ";
+        return "pc[i][" + std::to_string(best) + "]";
+    };
     size_t u = 0;
     for (size_t t = 1; t < pl.np.size(); ++t) {
         const uint32_t npp = pl.np[t - 1], npc = pl.np[t];
         if (npp == 1 && npc == 1) {
-            o << "    for (int i = 0; i < EPL; ++i) v[i][0] = v[i][0] * (" << pexpr(pl.udesc[u++]) << ");\n";
+            std::string pre;
+            const std::string e = use_expr(u++, pre);
+            o << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
             fence();
             continue;
         }
         // general year: n[.][l] = sum_k v[.][k] P[k][l] in ascending k
         for (uint32_t l = 0; l < npc; ++l)
             for (uint32_t k = 0; k < npp; ++k) {
-                o << "    for (int i = 0; i < EPL; ++i) n[i][" << l << "] = fma(v[i][" << k << "], "
-                  << pexpr(pl.udesc[u++]) << ", " << (k ? "n[i][" + std::to_string(l) + "]" : std::string("0.0"))
-                  << ");\n";
+                std::string pre;
+                const std::string e = use_expr(u++, pre);
+                o << "    for (int i = 0; i < EPL; ++i) { " << pre << "n[i][" << l << "] = fma(v[i][" << k << "], "
+                  << e << ", " << (k ? "n[i][" + std::to_string(l) + "]" : std::string("0.0")) << "); }\n";
                 fence();
             }
         o << "    for (int i = 0; i < EPL; ++i) {\n";

@@ -17,6 +17,8 @@ struct MdpJitPlan {
     int window = 8;               // transitions per scheduling region
     bool diag = false;            // record s_memtime phase stamps (MDP_DIAG)
     bool xcd = true;              // XCD-aware block order
+    bool qsum = true;             // Q rows come from k_qsum (else assembled from Pc in LDS)
+    int slots = 8;                // registers caching transitions that recur (0: none)
 };
 
 // HIP source of `mdp_fwd_jit` for this plan; sets plan.epl when it was 0.

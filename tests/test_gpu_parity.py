@@ -123,14 +123,20 @@ def test_q5_impossible_transition(tmp_path):
 # ---------------------------------------------------------------------------
 # fuzzing: random problems covering every forward-kernel variant
 # ---------------------------------------------------------------------------
-@pytest.fixture(params=["direct", "generic"])
+@pytest.fixture(params=["direct", "direct-qsum", "direct-inline-q", "generic"])
 def engine_path(request, monkeypatch):
-    """Both engine paths: the direct one (k_colonise + hipRTC-specialised
-    forward kernel, the default) and the generic kernels (MDP_JIT=0)."""
+    """Every engine path: the direct one (k_colonise + the hipRTC-specialised
+    forward kernel, the default; k_qsum assembles Q when a c column spans
+    several e blocks), the direct one with k_qsum forced (MDP_QSUM=1) or
+    disabled (MDP_QSUM=0), and the generic kernels (MDP_JIT=0)."""
+    monkeypatch.delenv("MDP_JIT", raising=False)
+    monkeypatch.delenv("MDP_QSUM", raising=False)
     if request.param == "generic":
         monkeypatch.setenv("MDP_JIT", "0")
-    else:
-        monkeypatch.delenv("MDP_JIT", raising=False)
+    elif request.param == "direct-inline-q":
+        monkeypatch.setenv("MDP_QSUM", "0")
+    elif request.param == "direct-qsum":
+        monkeypatch.setenv("MDP_QSUM", "1")
     return request.param
 
 
@@ -228,7 +234,8 @@ def test_device_run_matches_host_path(golden):
         torch.cuda.synchronize()
         ms = eng.kernel_ms()
     assert np.array_equal(out[:, :96].cpu().numpy(), host)
-    assert set(ms) in ({"k_colonise", "k_forward"}, {"k_zpv", "k_coefs", "k_forward"})
+    assert set(ms) in ({"k_colonise", "k_qsum", "k_forward"}, {"k_colonise", "k_forward"},
+                       {"k_zpv", "k_coefs", "k_forward"})
     assert all(v > 0 for v in ms.values())
 
 
@@ -241,7 +248,7 @@ def test_direct_and_generic_paths_agree(golden, monkeypatch, fname, s):
     with mdp.Engine(model) as eng:
         assert eng.info()["variant"] >= 10000  # the direct path is the default
         a = eng.loglik_grid(g, c)
-        assert set(eng.kernel_ms()) <= {"k_colonise", "k_forward"}
+        assert set(eng.kernel_ms()) <= {"k_colonise", "k_qsum", "k_forward"}
     monkeypatch.setenv("MDP_JIT", "0")
     with mdp.Engine(model) as eng:
         assert eng.info()["variant"] < 10000
