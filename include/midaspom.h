@@ -128,7 +128,7 @@ int mdp_engine_run(mdp_engine *engine, double *d_out, uint32_t ld_out, void *str
  * stream).  mdp_engine_kernel_ms fills up to max_k mean durations (ms) over
  * the runs since the previous call, in launch order, and returns the count;
  * mdp_engine_kernel_name gives the slot's kernel ("" for a slot the engine's
- * path does not launch: the direct path runs k_colonise + k_forward, the
+ * path does not launch: the direct path runs k_qrows + k_forward, the
  * generic path k_zpv + k_coefs + k_forward). */
 int mdp_engine_set_profiling(mdp_engine *engine, int enable);
 int mdp_engine_kernel_ms(mdp_engine *engine, double *ms, int max_k);

@@ -54,7 +54,6 @@ constexpr int kEPL = 2;         // k_forward: default grid points (e values) per
 constexpr int kMaxDeg = 24;
 constexpr int kStampSlots = 8;      // diagnostic stamps per workgroup
 constexpr uint32_t kSubPart = 16;   // k_coefs: subsets per work part
-constexpr uint32_t kColItems = 8;   // k_colonise: items per task (rows with more are split)
 constexpr uint32_t kOffBits = 22;   // coefficient offset bits in a use descriptor
 constexpr uint32_t kOffMask = (1u << kOffBits) - 1u;
 constexpr unsigned kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), other counters untouched
@@ -209,143 +208,102 @@ __global__ __launch_bounds__(kBlock) void k_zpv(
     MDP_RSTAMP(stamps, 7);
 }
 
-// Colonisation factors of the direct (problem-specialised) path.  Lanes run
-// over 64 c values; each wave takes one task = (hidden state j that some
-// transition needs, up to kColItems of the states b its row feeds):
-//   Z_j(c)    = prod over always-zero columns k of (1 - min(1, c S[j][k]))
-//   Pc[j][b]  = Z_j prod_{var b' not in j} (B_b' ? pC_jb' : 1 - pC_jb')
-// jtab[task] = {j, zs offset, zs length, first item}; the next entry's first
-// item ends the task (tasks are in item order; rows split into several tasks
-// share their zs row).  A workgroup (4 tasks):
-//  1. stages its zs rows and item masks in LDS (coalesced, one round trip);
-//  2. every lane multiplies its row from LDS broadcasts;
-//  3. writes its Pc values to an LDS tile [c][item] ...
-//  4. ... which the workgroup stores as contiguous row segments of Pc[c][item]
-//     (direct per-lane stores would scatter 8-byte writes over 64 rows).
-// Columns whose factor rounds to exactly 1.0 for every c of the grid are left
-// out of zs (rows padded to a multiple of 8 with zeros, which also give 1.0),
-// so the product equals the full one.
+// Transition coefficients of the direct path, one workgroup per kQrowsMaxC
+// (or fewer) consecutive c values, every hidden state j some transition needs
+// ("rows", r) and every (j, b) item:
+//  1. threads over (c, r): Z_r(c) = prod over the always-zero columns k of
+//     1 - min(1, c S[j][k]) -- the row's pruned S values streamed from L2 as
+//     16-byte loads; the clamp to 0 is tested once against the row maximum
+//     (zs[0]); rows are padded to even length with zeros (factor 1.0);
+//  2. threads over (c, item): Pc[j][b] = Z_r prod_{var b' not in j}
+//     (B_b' ? pC : 1 - pC), pC = min(1, c S[j][b']) -- into LDS;
+//  3. threads over (c, q): Q[c][q] = sum of the q-th entry's items (CSR, in
+//     ascending j: fixed order) -- written as coalesced rows for the forward
+//     kernel.
+// Nothing but Q leaves the workgroup.  Columns whose factor rounds to exactly
+// 1.0 for every c of the grid are left out of zs, so the products equal the
+// full ones.
+constexpr int kQrowsBlock = 1024;
+constexpr uint32_t kQrowsMaxC = 4;
 template <int NV>
-__global__ __launch_bounds__(kBlock) void k_colonise(
-    const double *__restrict__ cvals, uint32_t nc, uint32_t nvar, const uint4 *__restrict__ jtab,
-    uint32_t ntask, const double *__restrict__ zs, const double *__restrict__ sv,
-    const uint32_t *__restrict__ itemB, double *__restrict__ Pc, uint32_t ldP,
+__global__ __launch_bounds__(kQrowsBlock) void k_qrows(
+    const double *__restrict__ cvals, uint32_t nc, uint32_t cb, uint32_t nvar, uint32_t nrows,
+    uint32_t kmax, const double *__restrict__ zs, const double *__restrict__ sv,
+    uint32_t nitems, const uint2 *__restrict__ items, uint32_t ncoef, const uint32_t *__restrict__ qstart,
+    uint32_t nqi, const uint32_t *__restrict__ qitem, double *__restrict__ Q, uint32_t ldQ,
     unsigned long long *__restrict__ stamps)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     MDP_RSTAMP(stamps, 6);
     MDP_STAMP(stamps, 0);
-    constexpr uint32_t kTasks = kBlock / 64;
-    const uint32_t t0 = blockIdx.y * kTasks, t1 = min(t0 + kTasks, ntask);
-    const uint4 r0 = jtab[t0], rl = jtab[t1 - 1], r1 = jtab[t1];
-    const uint32_t zn = rl.y + rl.z - r0.y;  // multiple of 8
-    const uint32_t ni = r1.w - r0.w, tw = ni | 1u;  // tile row stride: odd, no bank conflicts
-    uint32_t *bl = (uint32_t *)(lds + zn);
-    double *tile = lds + zn + ((ni + 1) >> 1);
-    {
-        const double2 *src = (const double2 *)(zs + r0.y);
-        double2 *dst = (double2 *)lds;
-#pragma unroll 4
-        for (uint32_t i = threadIdx.x; i < zn / 2; i += kBlock) dst[i] = src[i];
-        for (uint32_t i = threadIdx.x; i < ni; i += kBlock) bl[i] = itemB[r0.w + i];
-    }
-    const uint32_t task = t0 + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t ic = blockIdx.x * 64 + lane;
-    const double c = ic < nc ? cvals[ic] : 0.0;
-    const bool active = task < t1;
-    const uint4 jt = jtab[active ? task : t0];
-    const uint32_t item1 = active ? jtab[task + 1].w : jt.w;
-    double svv[NV];  // rows padded to NV with zeros
+    const uint32_t c0 = blockIdx.x * cb, ncb = min(cb, nc - c0);
+    double *Zl = lds;                                  // [cb][nrows]
+    double *Sv = Zl + (size_t)cb * nrows;              // [nrows][nvar]
+    double *Pl = Sv + (size_t)nrows * nvar;            // [cb][nitems]
+    uint2 *It = (uint2 *)(Pl + (size_t)cb * nitems);   // [nitems] {B, j}, row in the top bytes
+    uint32_t *Qs = (uint32_t *)(It + nitems);          // [ncoef + 1]
+    uint32_t *Qi = Qs + ncoef + 1;                     // [nqi]
+    for (uint32_t i = threadIdx.x; i < nrows * nvar; i += kQrowsBlock) Sv[i] = sv[i];
+    for (uint32_t i = threadIdx.x; i < nitems; i += kQrowsBlock) It[i] = items[i];
+    for (uint32_t i = threadIdx.x; i <= ncoef; i += kQrowsBlock) Qs[i] = qstart[i];
+    for (uint32_t i = threadIdx.x; i < nqi; i += kQrowsBlock) Qi[i] = qitem[i];
+    // 1. Z per (c, row)
+    for (uint32_t w = threadIdx.x; w < ncb * nrows; w += kQrowsBlock) {
+        const uint32_t cl = w % ncb, r = w / ncb;
+        const double c = cvals[c0 + cl];
+        // zs[k][row]: lanes over rows read consecutive addresses; eight
+        // loads in flight per step, four product chains
+        const double *zc0 = zs + r;
+        double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;
+        for (uint32_t k = 0; k < kmax; k += 8) {
+            double sk[8];
 #pragma unroll
-    for (int b = 0; b < NV; ++b) svv[b] = sv[(size_t)(active ? task : t0) * NV + b];
+            for (int u = 0; u < 8; ++u) sk[u] = zc0[(size_t)(k + u) * nrows];
+            za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
+            zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);
+            zc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);
+            zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
+        }
+        double z = (za * zb) * (zc * zd);
+        if (kmax && !(fma(-c, zc0[0], 1.0) > 0.0)) z = 0.0;
+        Zl[cl * nrows + r] = z;
+    }
     __syncthreads();
     MDP_STAMP(stamps, 1);
-    const double *z8 = lds + (jt.y - r0.y);
-    // 1 - min(1, c s) = max(0, fma(-c, s, 1)); the clamp to 0 happens for some
-    // column iff it happens for the row's largest s (zs[0], c >= 0), and then
-    // Z = 0.  So the loop multiplies the unclamped factors and the clamp is
-    // one test at the end (v_max_f64 issues at a fraction of the FMA rate).
-    double z = 1.0;
-#pragma unroll 2
-    for (uint32_t k = 0; k < jt.z; k += 8) {
-        double f[8];
+    // 2. Pc per (c, item)
+    for (uint32_t w = threadIdx.x; w < ncb * nitems; w += kQrowsBlock) {
+        const uint32_t cl = w % ncb, it = w / ncb;
+        const double c = cvals[c0 + cl];
+        const uint2 t = It[it];
+        const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;
+        double p = Zl[cl * nrows + r];
+        // branch-free: lanes hold different items; bits of j and past nvar
+        // contribute 1.0
 #pragma unroll
-        for (int u = 0; u < 8; ++u) f[u] = fma(-c, z8[k + u], 1.0);
-#pragma unroll
-        for (int w = 1; w < 8; w *= 2)
-#pragma unroll
-            for (int u = 0; u + w < 8; u += 2 * w) f[u] *= f[u + w];
-        z *= f[0];
-    }
-    if (jt.z && !(fma(-c, z8[0], 1.0) > 0.0)) z = 0.0;
-    MDP_STAMP(stamps, 2);
-    // per var column: the factor for B_b = 1 (pC) and B_b = 0 (1 - pC); both
-    // 1.0 for columns inside j (and past nvar)
-    double f1[NV], f0[NV];
-#pragma unroll
-    for (int b = 0; b < NV; ++b) {
-        const bool inj = (uint32_t)b >= nvar || ((jt.x >> (nvar - 1 - b)) & 1u);
-        double pc = c * svv[b];
-        pc = pc > 1.0 ? 1.0 : pc;
-        f1[b] = inj ? 1.0 : pc;
-        f0[b] = inj ? 1.0 : 1.0 - pc;
-    }
-    for (uint32_t it = jt.w; it < item1; ++it) {
-        const uint32_t B = bl[it - r0.w];
-        double p = z;
-#pragma unroll
-        for (int b = 0; b < NV; ++b)
-            if ((uint32_t)b < nvar) p *= ((B >> (nvar - 1 - b)) & 1u) ? f1[b] : f0[b];
-        tile[lane * tw + (it - r0.w)] = p;
+        for (int b = 0; b < NV; ++b) {
+            const bool live = (uint32_t)b < nvar;
+            const uint32_t bit = live ? nvar - 1 - (uint32_t)b : 0u;
+            double pc = c * Sv[r * nvar + (live ? (uint32_t)b : 0u)];
+            pc = pc > 1.0 ? 1.0 : pc;
+            const double f = ((B >> bit) & 1u) ? pc : 1.0 - pc;
+            p *= (!live || ((j >> bit) & 1u)) ? 1.0 : f;
+        }
+        Pl[cl * nitems + it] = p;
     }
     __syncthreads();
-    const uint32_t rows = min(64u, nc - blockIdx.x * 64);
-    double *dst = Pc + (size_t)blockIdx.x * 64 * ldP + r0.w;
-    for (uint32_t i = threadIdx.x; i < rows * ni; i += kBlock) {
-        const uint32_t r = i / ni, k = i - r * ni;
-        dst[(size_t)r * ldP + k] = tile[r * tw + k];
+    MDP_STAMP(stamps, 2);
+    // 3. Q rows
+    for (uint32_t w = threadIdx.x; w < ncb * ldQ; w += kQrowsBlock) {
+        const uint32_t cl = w / ldQ, q = w - cl * ldQ;
+        double a = 0.0;
+        if (q < ncoef) {
+            const double *pl = Pl + (size_t)cl * nitems;
+            for (uint32_t i = Qs[q], i1 = Qs[q + 1]; i < i1; ++i) a += pl[Qi[i]];
+        }
+        Q[(size_t)(c0 + cl) * ldQ + q] = a;
     }
     MDP_STAMP(stamps, 3);
     MDP_RSTAMP(stamps, 7);
-}
-
-// Q rows of the direct path: Q[c][q] = sum of the items qitem[qstart[q] ..
-// qstart[q + 1]) of the Pc row (ascending j within each (pair, m) entry:
-// fixed order, deterministic).  A workgroup stages the CSR lists once and
-// assembles kQsumC consecutive c rows from LDS copies of their Pc rows.
-constexpr uint32_t kQsumC = 2;
-__global__ __launch_bounds__(kBlock) void k_qsum(const double *__restrict__ Pc, uint32_t ldP,
-                                                 const uint32_t *__restrict__ qstart,
-                                                 const uint32_t *__restrict__ qitem, uint32_t ncoef,
-                                                 uint32_t nqi, double *__restrict__ Q, uint32_t ldQ,
-                                                 uint32_t nc)
-{
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    double *Pl = lds;  // [kQsumC][ldP]
-    uint32_t *Qs = (uint32_t *)(lds + (size_t)kQsumC * ldP);
-    uint32_t *Qi = Qs + ncoef + 1;
-    const uint32_t c0 = blockIdx.x * kQsumC, rows = min(kQsumC, nc - c0);
-    {
-        const double2 *src = (const double2 *)(Pc + (size_t)c0 * ldP);
-        double2 *dst = (double2 *)Pl;
-        const uint32_t n2 = rows * ldP / 2;
-#pragma unroll 4
-        for (uint32_t i = threadIdx.x; i < n2; i += kBlock) dst[i] = src[i];
-    }
-    for (uint32_t i = threadIdx.x; i <= ncoef; i += kBlock) Qs[i] = qstart[i];
-    for (uint32_t i = threadIdx.x; i < nqi; i += kBlock) Qi[i] = qitem[i];
-    __syncthreads();
-    for (uint32_t r = 0; r < rows; ++r) {
-        const double *pr = Pl + (size_t)r * ldP;
-        double *qr = Q + (size_t)(c0 + r) * ldQ;
-        for (uint32_t q = threadIdx.x; q < ldQ; q += kBlock) {
-            double a = 0.0;
-            if (q < ncoef)
-                for (uint32_t i = Qs[q], i1 = Qs[q + 1]; i < i1; ++i) a += pr[Qi[i]];
-            qr[q] = a;
-        }
-    }
 }
 
 // One workgroup per c value.
@@ -801,7 +759,7 @@ int dev_reserve(T **p, size_t *cap, size_t count)
 
 constexpr int kNumEv = 6;  // start/stop per kernel: k_zpv, k_coefs, k_forward
 const char *const kKernelNames[2][3] = {{"k_zpv", "k_coefs", "k_forward"},
-                                        {"k_colonise", "k_qsum", "k_forward"}};
+                                        {"k_qrows", "", "k_forward"}};
 
 struct DevCtx {
     int device = 0;
@@ -818,16 +776,21 @@ struct DevCtx {
     unsigned long long *stamps[3] = {nullptr, nullptr, nullptr};  // k_zpv, k_coefs, k_forward
     size_t cap_st[3] = {0, 0, 0};
     size_t nst[3] = {0, 0, 0};
-    // direct path: colonisation tables (jtab / zs depend on the grid's c range)
-    uint4 *jtab = nullptr;
-    double *zs = nullptr, *sv = nullptr, *Pc = nullptr, *Qrow = nullptr;
+    // direct path: k_qrows tables (zs depends on the grid's c range)
+    double *zs = nullptr, *sv = nullptr, *Qrow = nullptr;
+    uint2 *items = nullptr;  // per item {B | row << 24, j | (row >> 8) << 24}
     uint32_t *itemB = nullptr, *qstart = nullptr, *qitem = nullptr;
-    size_t cap_jtab = 0, cap_zs = 0, cap_pc = 0, cap_qrow = 0;
-    size_t col_lds = 0;     // k_colonise dynamic LDS: largest workgroup's S rows + item masks
+    size_t cap_zs = 0, cap_qrow = 0;
+    uint32_t zs_len = 0;    // doubles in zs = zs_kmax * nj
+    double *coltab = nullptr;  // fused kernel's column tables (plan offsets, zs last), 1 KiB padded
+    size_t cap_coltab = 0;
+    uint32_t ct_len = 0;       // doubles
+    uint32_t zs_kmax = 0;   // padded length of the longest pruned row
+    uint32_t qrows_cb = 1;  // c values per k_qrows workgroup for this grid
     double zs_cmax = -1.0;  // c bound the uploaded zs was pruned for (-1: none yet)
-    hipModule_t jit_mod[2] = {nullptr, nullptr};  // problem-specialised forward kernel [qsum]
+    hipModule_t jit_mod[2] = {nullptr, nullptr};  // problem-specialised forward kernel [fused]
     hipFunction_t jit_fn[2] = {nullptr, nullptr};
-    bool use_qsum = false;  // this grid's direct path runs k_qsum (several e blocks per c)
+    bool fused = false;  // this grid runs the fused forward kernel (no k_qrows)
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     size_t ev_used = 0;          // event sets recorded since the last collect
 };
@@ -847,18 +810,17 @@ struct mdp_engine {
     bool diag = false;        // MDP_DIAG: record phase stamps
     bool jit = false;         // forward kernel specialised with hipRTC (spom_jit.cpp)
     int jit_epl = 1;          // its grid points per lane
+    double jit_flops_pt = 0;  // its FP64 flops per grid point (counted by the generator)
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
-    std::vector<char> jit_code[2];  // forward kernel code objects [qsum], compiled on demand
+    std::vector<char> jit_code[2];  // forward kernel code objects [fused], compiled on demand
+    int fused_mode = -1;            // MDP_FUSED: -1 auto, 0, 1
     MdpJitPlan jit_plan;
-    int qsum_mode = -1;  // MDP_QSUM: -1 auto (k_qsum when a c column spans several e blocks), 0, 1
-    // direct path (jit): k_colonise computes Pc[j][b] for the needed (j, b)
+    // direct path (jit): k_qrows computes Pc[j][b] for the needed (j, b)
     // items, the forward kernel assembles Q from them
     uint32_t nj = 0, nitems = 0, ncoef_d = 0;
-    bool qsum_ok = true;  // k_qsum fits the LDS
-    size_t qsum_lds = 0;
     size_t ldP = 0;
     std::vector<uint32_t> cj_bits, cj_item0, itemB, qstart, qitem, udesc_d, var_cols;
-    std::vector<uint32_t> task_js, task_item0;  // k_colonise tasks: j slot, first item (+ end)
+    std::vector<uint32_t> itemRow;  // row (j slot) of each item
     std::vector<uint8_t> isvar;
     std::vector<double> Sj;  // [nj][n] colonisation sums of every column for each needed j
     std::string jit_log;
@@ -1069,14 +1031,10 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
     }
     eng->cj_item0.push_back((uint32_t)eng->itemB.size());
     eng->nj = (uint32_t)eng->cj_bits.size();
-    eng->task_js.clear();
-    eng->task_item0.clear();
+    if (eng->nj > 0xffffu) return mdp_set_error(MDP_EUNSUPPORTED, "%u hidden-state rows (direct path max 65535)", eng->nj);
+    eng->itemRow.assign(eng->itemB.size(), 0u);
     for (uint32_t js = 0; js < eng->nj; ++js)
-        for (uint32_t i = eng->cj_item0[js]; i < eng->cj_item0[js + 1]; i += kColItems) {
-            eng->task_js.push_back(js);
-            eng->task_item0.push_back(i);
-        }
-    eng->task_item0.push_back((uint32_t)eng->itemB.size());
+        for (uint32_t i = eng->cj_item0[js]; i < eng->cj_item0[js + 1]; ++i) eng->itemRow[i] = js;
     eng->nitems = (uint32_t)eng->itemB.size();
     eng->ldP = ((size_t)eng->nitems + 1) & ~(size_t)1;
     eng->qstart.assign(1, 0u);
@@ -1119,103 +1077,109 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
     return MDP_OK;
 }
 
-uint32_t colonise_nv(uint32_t nvar) { return nvar <= 8 ? 8u : nvar <= 16 ? 16u : 24u; }
-constexpr size_t kColLdsMax = 160 * 1024;
+constexpr size_t kQrowsLdsMax = 160 * 1024;
+constexpr size_t kFusedLdsMax = 64 * 1024;  // fused forward kernel: every table of one column
 
-// k_colonise LDS per workgroup (tasks [t0, t0 + 4)): zs rows, item masks and
-// the [64][items | 1] output tile; zlen per j slot
-size_t colonise_lds(const mdp_engine *eng, const std::vector<uint32_t> &zlen)
+// k_qrows LDS for cb c values per workgroup: Z, var-column S, Pc, Q CSR
+size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
 {
-    size_t mx = 0;
-    const uint32_t nt = (uint32_t)eng->task_js.size();
-    for (uint32_t t0 = 0; t0 < nt; t0 += kBlock / 64) {
-        const uint32_t t1 = std::min<uint32_t>(t0 + kBlock / 64, nt);
-        size_t z = 0;
-        for (uint32_t t = t0; t < t1; ++t)
-            if (t == t0 || eng->task_js[t] != eng->task_js[t - 1]) z += zlen[eng->task_js[t]];
-        const size_t ni = eng->task_item0[t1] - eng->task_item0[t0];
-        mx = std::max(mx, (z + (ni + 1) / 2 + 64 * (ni | 1)) * sizeof(double));
-    }
-    return mx;
+    return ((size_t)cb * eng->nj + (size_t)eng->nj * eng->nvar + (size_t)cb * eng->nitems) * sizeof(double) +
+           (size_t)eng->nitems * sizeof(uint2) + ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);
 }
 
-// zs / jtab for a grid whose |c| <= cmax: a column's factor
-// max(0, fma(-c, s, 1)) is exactly 1.0 when |c s| <= 2^-55, so it is dropped
-int upload_colonise_tables(const mdp_engine *eng, DevCtx &d, double cmax)
+// zs for a grid whose |c| <= cmax: a column's factor max(0, fma(-c, s, 1)) is
+// exactly 1.0 when |c s| <= 2^-55, so it is dropped.  The kept values of each
+// hidden-state row (largest first: the clamp test reads it) are stored
+// transposed, zs[k][row] with kmax = the longest row rounded up to 8 and zero
+// padding (factor 1.0), so lanes over rows read consecutive addresses.
+int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
 {
-    std::vector<double> zs;
-    std::vector<uint32_t> zoff(eng->nj), zlen(eng->nj);
-    const uint32_t n = eng->n;
-    for (uint32_t js = 0; js < eng->nj; ++js) {
-        const size_t z0 = zs.size();
-        size_t imax = z0;
+    const uint32_t n = eng->n, nj = eng->nj;
+    std::vector<std::vector<double>> rows(nj);
+    size_t kmax = 0;
+    for (uint32_t js = 0; js < nj; ++js) {
+        std::vector<double> &r = rows[js];
+        size_t imax = 0;
         for (uint32_t k = 0; k < n; ++k) {
             if (eng->isvar[k]) continue;
             const double sv = eng->Sj[(size_t)js * n + k];
             if (cmax * sv <= 0x1p-55) continue;  // false for NaN / inf: kept
-            if (zs.size() > z0 && sv > zs[imax]) imax = zs.size();
-            zs.push_back(sv);
+            if (!r.empty() && sv > r[imax]) imax = r.size();
+            r.push_back(sv);
         }
-        // the clamp test reads the row's largest value first: rotate it to the
-        // front (the product order changes, each factor stays the same)
-        if (zs.size() > z0) std::swap(zs[z0], zs[imax]);
-        while ((zs.size() - z0) % 8) zs.push_back(0.0);
-        zoff[js] = (uint32_t)z0;
-        zlen[js] = (uint32_t)(zs.size() - z0);
+        if (!r.empty()) std::swap(r[0], r[imax]);
+        kmax = std::max(kmax, r.size());
     }
-    std::vector<uint4> jtab;
-    for (size_t t = 0; t < eng->task_js.size(); ++t) {
-        const uint32_t js = eng->task_js[t];
-        jtab.push_back(make_uint4(eng->cj_bits[js], zoff[js], zlen[js], eng->task_item0[t]));
-    }
-    jtab.push_back(make_uint4(0u, (uint32_t)zs.size(), 0u, eng->nitems));
-    d.col_lds = colonise_lds(eng, zlen);
-    if (d.col_lds > kColLdsMax)
-        return mdp_set_error(MDP_EUNSUPPORTED, "colonisation rows need %zu B of LDS", d.col_lds);
-    if (d.col_lds > 64 * 1024)  // opt in to exactly what the launch uses
-        for (const void *fn : {(const void *)k_colonise<8>, (const void *)k_colonise<16>,
-                               (const void *)k_colonise<24>})
-            HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.col_lds));
-    zs.push_back(0.0);
+    kmax = (kmax + 7) & ~(size_t)7;
+    std::vector<double> zs(kmax * nj + 1, 0.0);
+    for (uint32_t js = 0; js < nj; ++js)
+        for (size_t k = 0; k < rows[js].size(); ++k) zs[k * nj + js] = rows[js][k];
     int rc;
-    if ((rc = dev_reserve(&d.zs, &d.cap_zs, zs.size())) || (rc = dev_reserve(&d.jtab, &d.cap_jtab, jtab.size())))
-        return rc;
+    if ((rc = dev_reserve(&d.zs, &d.cap_zs, zs.size()))) return rc;
     HIP_TRY(hipMemcpy(d.zs, zs.data(), zs.size() * sizeof(double), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d.jtab, jtab.data(), jtab.size() * sizeof(uint4), hipMemcpyHostToDevice));
     d.zs_cmax = cmax;
+    d.zs_len = (uint32_t)(kmax * nj);
+    d.zs_kmax = (uint32_t)kmax;
+    // the fused kernel's column tables: one contiguous image it copies to LDS
+    const MdpJitPlan &pl = eng->jit_plan;
+    const size_t ct = ((size_t)pl.off_zs + kmax * nj + 127) & ~(size_t)127;
+    std::vector<double> img(ct, 0.0);
+    for (uint32_t js = 0; js < nj; ++js)
+        for (uint32_t b = 0; b < eng->nvar; ++b)
+            img[(size_t)js * eng->nvar + b] = eng->Sj[(size_t)js * n + eng->var_cols[b]];
+    uint2 *it = (uint2 *)(img.data() + pl.off_it);
+    for (uint32_t i = 0; i < eng->nitems; ++i) {
+        const uint32_t r = eng->itemRow[i];
+        it[i] = make_uint2(eng->itemB[i] | ((r & 0xffu) << 24), eng->cj_bits[r] | ((r >> 8) << 24));
+    }
+    memcpy(img.data() + pl.off_qs, eng->qstart.data(), eng->qstart.size() * sizeof(uint32_t));
+    if (!eng->qitem.empty())
+        memcpy(img.data() + pl.off_qi, eng->qitem.data(), eng->qitem.size() * sizeof(uint32_t));
+    std::copy(zs.begin(), zs.begin() + kmax * nj, img.begin() + pl.off_zs);
+    if ((rc = dev_reserve(&d.coltab, &d.cap_coltab, ct))) return rc;
+    HIP_TRY(hipMemcpy(d.coltab, img.data(), ct * sizeof(double), hipMemcpyHostToDevice));
+    d.ct_len = (uint32_t)ct;
     return MDP_OK;
 }
 
-// Compile (hipRTC, cached) the forward kernel variant `qsum` of the engine's plan.
-int jit_build(mdp_engine *eng, bool qsum)
+// Compile (hipRTC, cached) the engine's forward kernel, fused or not.
+int jit_build(mdp_engine *eng, bool fused)
 {
-    if (!eng->jit_code[qsum].empty()) return MDP_OK;
+    if (!eng->jit_code[fused].empty()) return MDP_OK;
     MdpJitPlan plan = eng->jit_plan;
-    plan.qsum = qsum;
+    plan.fused = fused;
     const std::string src = mdp_jit_forward_source(plan);
     eng->jit_epl = plan.epl;
+    eng->jit_flops_pt = plan.flops_pt;
     if (const char *dump = getenv("MDP_JIT_DUMP")) {
         if (FILE *f = fopen(dump, "w")) {
             fputs(src.c_str(), f);
             fclose(f);
         }
     }
-    if (mdp_jit_compile(src, eng->jit_code[qsum], eng->jit_log) != 0)
+    if (mdp_jit_compile(src, eng->jit_code[fused], eng->jit_log) != 0)
         return mdp_set_error(MDP_EHIP, "hipRTC compilation of the forward kernel failed: %s",
                              eng->jit_log.c_str());
     return MDP_OK;
 }
 
-// Load the forward kernel variant into the device (compiling it if needed).
-int jit_load(mdp_engine *eng, DevCtx &d, bool qsum)
+// Load a forward kernel variant into the device (compiling it if needed).
+int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 {
-    if (d.jit_fn[qsum]) return MDP_OK;
-    int rc = jit_build(eng, qsum);
+    if (d.jit_fn[fused]) return MDP_OK;
+    int rc = jit_build(eng, fused);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(d.device));
-    HIP_TRY(hipModuleLoadData(&d.jit_mod[qsum], eng->jit_code[qsum].data()));
-    HIP_TRY(hipModuleGetFunction(&d.jit_fn[qsum], d.jit_mod[qsum], "mdp_fwd_jit"));
+    HIP_TRY(hipModuleLoadData(&d.jit_mod[fused], eng->jit_code[fused].data()));
+    HIP_TRY(hipModuleGetFunction(&d.jit_fn[fused], d.jit_mod[fused], "mdp_fwd_jit"));
     return MDP_OK;
+}
+
+// The fused forward kernel keeps its column's tables (ct_len doubles,
+// dynamic LDS), Z, Pc and Q in LDS.
+size_t fused_lds(const mdp_engine *eng, size_t ct_len)
+{
+    return (ct_len + eng->nj + eng->nitems + eng->ldQ) * sizeof(double);
 }
 
 int upload_binomials()  // into the current device's constant bank
@@ -1261,22 +1225,26 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
     HIP_TRY(hipStreamSynchronize(d.stream));
     (void)hipFree(dM);
     if (eng->jit) {
-        const uint32_t nvp = colonise_nv(eng->nvar);
-        const size_t nt = eng->task_js.size();
-        std::vector<double> sv(nt * nvp + 1, 0.0);
-        for (size_t t = 0; t < nt; ++t)
+        std::vector<double> sv((size_t)eng->nj * eng->nvar + 1, 0.0);
+        for (uint32_t js = 0; js < eng->nj; ++js)
             for (uint32_t b = 0; b < eng->nvar; ++b)
-                sv[t * nvp + b] = eng->Sj[(size_t)eng->task_js[t] * eng->n + eng->var_cols[b]];
-        std::vector<uint32_t> itemB = eng->itemB, qitem = eng->qitem;
-        itemB.push_back(0u);
+                sv[(size_t)js * eng->nvar + b] = eng->Sj[(size_t)js * eng->n + eng->var_cols[b]];
+        std::vector<uint2> items(eng->nitems + 1, make_uint2(0u, 0u));
+        for (uint32_t i = 0; i < eng->nitems; ++i) {
+            const uint32_t r = eng->itemRow[i];
+            items[i] = make_uint2(eng->itemB[i] | ((r & 0xffu) << 24), eng->cj_bits[r] | ((r >> 8) << 24));
+        }
+        std::vector<uint32_t> qitem = eng->qitem;
         qitem.push_back(0u);
-        if ((rc = dev_upload(&d.sv, sv)) || (rc = dev_upload(&d.itemB, itemB)) ||
+        if ((rc = dev_upload(&d.sv, sv)) || (rc = dev_upload(&d.items, items)) ||
             (rc = dev_upload(&d.qstart, eng->qstart)) || (rc = dev_upload(&d.qitem, qitem)))
             return rc;
-        if (eng->qsum_lds > 64 * 1024)
-            HIP_TRY(hipFuncSetAttribute((const void *)k_qsum, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)eng->qsum_lds));
-        if ((rc = jit_load(eng, d, eng->qsum_mode == 1))) return rc;
+        const size_t lds_max = qrows_lds(eng, kQrowsMaxC);
+        if (lds_max > 64 * 1024)
+            for (const void *fn : {(const void *)k_qrows<8>, (const void *)k_qrows<16>, (const void *)k_qrows<24>})
+                HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)std::min(lds_max, kQrowsLdsMax)));
+        if ((rc = jit_load(eng, d, eng->fused_mode == 1))) return rc;
     }
     if (eng->coef_lds > 64 * 1024) {
         const void *fns[] = {
@@ -1297,7 +1265,7 @@ void free_device(DevCtx &d)
     (void)hipSetDevice(d.device);
     void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog,
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
-                    d.jtab, d.zs, d.sv, d.Pc, d.Qrow, d.itemB, d.qstart, d.qitem,
+                    d.zs, d.sv, d.Qrow, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -1321,12 +1289,18 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     if (eng->jit) {
         double cmax = 0.0;
         for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
-        if ((rc = dev_reserve(&d.Pc, &d.cap_pc, (size_t)nc * eng->ldP))) return rc;
+        if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ))) return rc;
+        if (!(d.zs_cmax == cmax) && (rc = upload_qrows_tables(eng, d, cmax))) return rc;
+        // one e block per c column and a small per-c problem: the forward
+        // kernel computes its column's Q itself (one launch)
         const uint32_t gy = (ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
-        d.use_qsum = eng->qsum_mode == 1 || (eng->qsum_mode == -1 && gy > 1);
-        if ((rc = jit_load(eng, d, d.use_qsum))) return rc;
-        if (d.use_qsum && (rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ))) return rc;
-        if (!(d.zs_cmax == cmax) && (rc = upload_colonise_tables(eng, d, cmax))) return rc;
+        d.fused = fused_lds(eng, d.ct_len) <= kFusedLdsMax &&
+                  (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
+        if ((rc = jit_load(eng, d, d.fused))) return rc;
+        // c values per k_qrows workgroup: enough workgroups for every CU, within the LDS
+        uint32_t cb = std::max(1u, std::min(kQrowsMaxC, nc / 256u));
+        while (cb > 1 && qrows_lds(eng, cb) > kQrowsLdsMax) --cb;
+        d.qrows_cb = cb;
     } else if ((rc = dev_reserve(&d.ZPV, &d.cap_zpv, (size_t)nc * (eng->nvar + 1) * eng->nstates)) ||
                (rc = dev_reserve(&d.R, &d.cap_r, (size_t)nc * ldR_of(eng)))) {
         return rc;
@@ -1335,7 +1309,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         (rc = dev_reserve(&d.gpart, &d.cap_gpart, (size_t)nc * eng->partP.size() * (eng->nvar + 1))))
         return rc;
     if (eng->diag) {
-        d.nst[0] = eng->jit ? (size_t)((nc + 63) / 64) * ((eng->task_js.size() + kBlock / 64 - 1) / (kBlock / 64))
+        d.nst[0] = eng->jit ? (size_t)nc
                             : (size_t)((eng->nstates + kZpvJ - 1) / kZpvJ) * ((nc + kZpvCT - 1) / kZpvCT);
         d.nst[1] = nc;
         d.nst[2] = (size_t)nc * ((ne + kBlock - 1) / kBlock);  // >= the JIT grid (EPL >= 1)
@@ -1392,19 +1366,22 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
 {
     int rc;
     if (eng->jit) {
-        const double *Pc = d.use_qsum ? d.Qrow : d.Pc;
-        const uint32_t *qs = d.qstart, *qi = d.qitem;
+        const double *Qrow = d.Qrow;
         double prior0 = eng->prior0;
         const double *ev = d.e;
         uint32_t ne = d.ne, nc = d.nc, one = 1;
         unsigned long long *st = d.stamps[2];
-        void *args[] = {(void *)&Pc, (void *)&qs,  (void *)&qi, (void *)&prior0, (void *)&ev, (void *)&ne,
-                        (void *)&nc, (void *)&out, (void *)&ld, (void *)&one,    (void *)&st};
+        const double *cv = d.c, *ctab = d.coltab;
+        uint32_t ctl = d.ct_len, kmax = d.zs_kmax;
+        void *args[] = {(void *)&Qrow, (void *)&prior0, (void *)&ev,  (void *)&ne, (void *)&nc,
+                        (void *)&out,  (void *)&ld,     (void *)&one, (void *)&st, (void *)&cv,
+                        (void *)&ctab, (void *)&ctl,    (void *)&kmax};
         const uint64_t gy = (d.ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
         const uint64_t nb = gy * d.nc;
         if (nb * kBlock > 0xffffffffull)
             return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
-        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.use_qsum], (uint32_t)(nb * kBlock), 1, 1, kBlock, 1, 1, 0, s, args,
+        const uint32_t dyn = d.fused ? d.ct_len * (uint32_t)sizeof(double) : 0u;
+        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kBlock), 1, 1, kBlock, 1, 1, dyn, s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));
         return MDP_OK;
     }
@@ -1473,30 +1450,24 @@ int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
     } reset;
     if (eng->jit) {  // direct path: colonisation factors, then the specialised forward kernel
         timed(0);
-        const uint32_t ntask = (uint32_t)eng->task_js.size();
-        if (ntask) {
-            const dim3 grid((d.nc + 63) / 64, (ntask + kBlock / 64 - 1) / (kBlock / 64));
-            if (eng->nvar <= 8)
-                MDP_LAUNCH(k_colonise<8>, grid, dim3(kBlock), d.col_lds, s, d.c, d.nc, eng->nvar, d.jtab, ntask,
-                           d.zs, d.sv, d.itemB, d.Pc, (uint32_t)eng->ldP, d.stamps[0]);
-            else if (eng->nvar <= 16)
-                MDP_LAUNCH(k_colonise<16>, grid, dim3(kBlock), d.col_lds, s, d.c, d.nc, eng->nvar, d.jtab, ntask,
-                           d.zs, d.sv, d.itemB, d.Pc, (uint32_t)eng->ldP, d.stamps[0]);
-            else
-                MDP_LAUNCH(k_colonise<24>, grid, dim3(kBlock), d.col_lds, s, d.c, d.nc, eng->nvar, d.jtab, ntask,
-                           d.zs, d.sv, d.itemB, d.Pc, (uint32_t)eng->ldP, d.stamps[0]);
+        if (eng->nitems && !d.fused) {
+            const uint32_t cb = d.qrows_cb;
+            const dim3 grid((d.nc + cb - 1) / cb);
+            const size_t lds = qrows_lds(eng, cb);
+#define MDP_QROWS(NV)                                                                                  \
+    MDP_LAUNCH(k_qrows<NV>, grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj, d.zs_kmax, \
+               d.zs, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                               \
+               (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[0])
+            if (eng->nvar <= 8) MDP_QROWS(8);
+            else if (eng->nvar <= 16) MDP_QROWS(16);
+            else MDP_QROWS(24);
+#undef MDP_QROWS
             HIP_TRY(hipGetLastError());
         } else if (prof) {
             HIP_TRY(hipEventRecord(ev[0], s));
             HIP_TRY(hipEventRecord(ev[1], s));
         }
-        if (d.use_qsum && eng->nitems) {
-            timed(1);
-            MDP_LAUNCH(k_qsum, dim3((d.nc + kQsumC - 1) / kQsumC), dim3(kBlock), eng->qsum_lds, s, d.Pc,
-                       (uint32_t)eng->ldP, d.qstart, d.qitem, eng->ncoef_d, (uint32_t)eng->qitem.size(),
-                       d.Qrow, (uint32_t)eng->ldQ, d.nc);
-            HIP_TRY(hipGetLastError());
-        } else if (prof) {  // no separate coefficient kernel
+        if (prof) {  // no second kernel on this path
             HIP_TRY(hipEventRecord(ev[2], s));
             HIP_TRY(hipEventRecord(ev[3], s));
         }
@@ -1580,30 +1551,38 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
         bool want_jit = want && build_direct_plan(eng, p) == MDP_OK;
         if (want_jit) {  // colonisation rows without pruning must fit the LDS
             const uint32_t z = ((eng->n - eng->nvar) + 7u) & ~7u;
-            want_jit = colonise_lds(eng, std::vector<uint32_t>(eng->nj, z)) <= kColLdsMax;
+            (void)z;
+            want_jit = qrows_lds(eng, 1) <= kQrowsLdsMax;
         }
         eng->ldQ = ((size_t)eng->ncoef_d + 1) & ~(size_t)1;
         if (want_jit && eng->nuses > 0 && eng->nuses <= kJitMaxUses &&
-            (eng->ldQ + eng->ldP) * sizeof(double) + (eng->ncoef_d + 1 + eng->qitem.size()) * 4 <=
-                kJitMaxLds) {
+            eng->ldQ * sizeof(double) <= kJitMaxLds) {
             MdpJitPlan &plan = eng->jit_plan;
             plan.np = eng->np;
             plan.udesc = eng->udesc_d;
             plan.ldQ = eng->ldQ;
-            plan.ncoef = eng->ncoef_d;
-            plan.ldP = eng->ldP;
-            plan.nqi = eng->qitem.size();
             plan.diag = eng->diag;
-            if (const char *qv = getenv("MDP_QSUM")) eng->qsum_mode = atoi(qv) != 0;
-            eng->qsum_lds = kQsumC * eng->ldP * sizeof(double) + (eng->ncoef_d + 1 + eng->qitem.size()) * 4;
-            eng->qsum_ok = eng->qsum_lds <= kColLdsMax;
-            if (!eng->qsum_ok) eng->qsum_mode = 0;
             if (const char *cv = getenv("MDP_JIT_SLOTS")) plan.slots = atoi(cv);
             if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
             if (const char *ev = getenv("MDP_EPL")) plan.epl = atoi(ev);
             if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
             // compile the variant a small grid uses now (the other on demand)
-            if (jit_build(eng, eng->qsum_mode == 1) == MDP_OK) eng->jit = true;
+            if (const char *fv = getenv("MDP_FUSED")) eng->fused_mode = atoi(fv) != 0;
+            if (const char *gv = getenv("MDP_JIT_GLDS")) plan.glds = atoi(gv) != 0;
+            plan.nj = eng->nj;
+            plan.nvar = eng->nvar;
+            plan.nitems = eng->nitems;
+            plan.ncoef = eng->ncoef_d;
+            plan.nqi = (uint32_t)eng->qitem.size();
+            auto even = [](size_t v) { return (uint32_t)((v + 1) & ~(size_t)1); };
+            plan.off_it = even((size_t)eng->nj * eng->nvar);
+            plan.off_qs = even(plan.off_it + eng->nitems);
+            plan.off_qi = even(plan.off_qs + (eng->ncoef_d + 2) / 2);
+            plan.off_zs = even(plan.off_qi + (eng->qitem.size() + 1) / 2);
+            const size_t kmax_max = ((size_t)(eng->n - eng->nvar) + 7) & ~(size_t)7;
+            plan.ct_max = (uint32_t)std::min<size_t>(((plan.off_zs + kmax_max * eng->nj) + 127) & ~(size_t)127,
+                                                     kFusedLdsMax / sizeof(double));
+            if (jit_build(eng, eng->fused_mode == 1) == MDP_OK) eng->jit = true;
             else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the generic kernel:\n%s\n",
                          eng->jit_log.c_str());
         }
@@ -1704,10 +1683,11 @@ int mdp_engine_diag_report(mdp_engine *eng, char *buf, size_t len)
     HIP_TRY(hipDeviceSynchronize());
     const char *names[3] = {"k_zpv", "k_coefs", "k_forward_lds"};
     int slots[3] = {3, 5, 3};
-    if (eng->jit) {  // direct path: k_colonise and the hipRTC forward kernel
-        names[0] = "k_colonise";
+    if (eng->jit) {  // direct path: k_qrows and the hipRTC forward kernel
+        names[0] = "k_qrows";
         names[2] = "k_forward(jit)";
-        slots[0] = slots[2] = 4;
+        slots[0] = 4;
+        slots[2] = d.fused ? 6 : 4;
         slots[1] = 0;
     }
     size_t used = 0;
@@ -1722,15 +1702,20 @@ int mdp_engine_diag_report(mdp_engine *eng, char *buf, size_t len)
         size_t nb = 0;
         for (size_t b = 0; b < d.nst[k]; ++b) {
             const unsigned long long *st = &h[b * kStampSlots];
-            if (!st[0] || !st[slots[k] - 1] || st[slots[k] - 1] < st[0]) continue;
+            const int last = (k == 2 && eng->jit && d.fused) ? 3 : slots[k] - 1;
+            if (!st[0] || !st[last] || st[last] < st[0]) continue;
             ++nb;
             rs0 = std::min(rs0, st[6]);
             rs1 = std::max(rs1, st[6]);
             re1 = std::max(re1, st[7]);
             rdur += (double)(st[7] - st[6]);
             t0 = std::min(t0, st[0]);
-            t1 = std::max(t1, st[slots[k] - 1]);
-            for (int q = 1; q < slots[k]; ++q) mean[q] += (double)(st[q] - st[q - 1]);
+            t1 = std::max(t1, st[last]);
+            // the fused forward kernel stamps slots 4 and 5 between 0 and 1
+            const bool fz = k == 2 && eng->jit && eng->devs[0].fused && slots[k] == 6;
+            static const int seq_plain[6] = {0, 1, 2, 3, 4, 5}, seq_fused[6] = {0, 4, 5, 1, 2, 3};
+            const int *seq = fz ? seq_fused : seq_plain;
+            for (int q = 1; q < slots[k]; ++q) mean[q] += (double)(st[seq[q]] - st[seq[q - 1]]);
         }
         int w = snprintf(buf + used, len - used,
                          "%s: blocks=%zu wall_us=%.2f last_start_us=%.2f mean_block_us=%.2f cycles:",
@@ -1781,7 +1766,7 @@ int mdp_engine_kernel_ms(mdp_engine *eng, double *ms, int max_k)
 const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
     if (!eng || k < 0 || k >= 3) return "";
-    if (eng->jit && k == 1 && (eng->devs.empty() || !eng->devs[0].use_qsum)) return "";
+    if (eng->jit && k == 0 && (eng->devs.empty() || eng->devs[0].fused)) return "";  // fused: one kernel
     return kKernelNames[eng->jit ? 1 : 0][k];
 }
 
@@ -1808,10 +1793,7 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     const double D = (double)eng->deg;
     double per_pt = (double)eng->nuses * (2.0 * (D + 1.0) + 2.0) + 3.0 * (D + 1.0) +
                     2.0 * (double)eng->npmax;
-    if (eng->jit) {  // direct form: (nX+1)-term dot product per use, then the v update
-        per_pt = 2.0 * (double)eng->npmax;
-        for (uint32_t dsc : eng->udesc) per_pt += 2.0 * (double)(((dsc >> kOffBits) & 31u) + 1u) + 2.0;
-    }
+    if (eng->jit) per_pt = eng->jit_flops_pt;  // the generated code's own count
     if (flop_impl) *flop_impl = per_pt * pts;
     // SURVEY.md §8(d) F_alg (dense-in-j formulation)
     double fwd = 0;
@@ -1822,7 +1804,7 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     // compulsory bytes of k_forward: its coefficient stream once per c, the
     // e values, the output
     if (bytes_min)
-        *bytes_min = 8.0 * ((double)nc * (eng->jit ? eng->ldP : ldR_of(eng)) + (double)ne + pts);
+        *bytes_min = 8.0 * ((double)nc * (eng->jit ? eng->ldQ : ldR_of(eng)) + (double)ne + pts);
     return MDP_OK;
 }
 

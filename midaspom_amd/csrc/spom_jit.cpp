@@ -111,8 +111,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     o << kPrelude;
     o << "#define EPL " << EPL << "\n#define LDQ " << pl.ldQ << "\n#define NPMAX " << npmax
       << "\n#define DMAX " << dmax << "\n#define NW " << (nw ? nw : 1) << "\n";
-    o << "#define LDP " << pl.ldP << "\n#define NCOEF " << pl.ncoef << "\n#define NQI " << (pl.nqi ? pl.nqi : 1)
-      << "\n";
     // diagnostic phase stamps: s_memtime (slots 0-3) and s_memrealtime (6, 7)
     auto stamp = [&](int slot) {
         if (!pl.diag) return std::string();
@@ -120,10 +118,16 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                std::to_string(slot) + "] = " +
                (slot >= 6 ? "__builtin_amdgcn_s_memrealtime();\n" : "__builtin_amdgcn_s_memtime();\n");
     };
+    if (pl.fused)
+        o << "#define NJ " << pl.nj << "\n#define NVAR " << pl.nvar << "\n#define NITEMS " << pl.nitems
+          << "\n#define NCOEF " << pl.ncoef << "\n#define NQI " << (pl.nqi ? pl.nqi : 1) << "\n#define OFF_IT "
+          << pl.off_it << "\n#define OFF_QS " << pl.off_qs << "\n#define OFF_QI " << pl.off_qi << "\n#define OFF_ZS "
+          << pl.off_zs << "\n#define NSTG " << ((pl.ct_max / 2 + 255) / 256 > 0 ? (pl.ct_max / 2 + 255) / 256 : 1)
+          << "\n";
     o << "extern \"C\" __global__ __launch_bounds__(KBLOCK) void mdp_fwd_jit(\n"
-         "    const double *__restrict__ Pc, const u32 *__restrict__ qstart, const u32 *__restrict__ qitem,\n"
-         "    double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
-         "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps)\n{\n"
+         "    const double *__restrict__ Qrow, double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
+         "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps,\n"
+         "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax)\n{\n"
          "    __shared__ __attribute__((aligned(16))) double Ql[LDQ];\n"
       << stamp(6) << stamp(0) <<
          // XCD-aware order: the dispatcher deals blocks round-robin over the 8
@@ -147,25 +151,97 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        }\n"
              "    }\n";
     };
-    if (pl.qsum) {  // Q rows from k_qsum (the first pointer argument)
-        stage("Ql", "Pc + (size_t)ic * LDQ", "LDQ");
+    if (!pl.fused) {
+        stage("Ql", "Qrow + (size_t)ic * LDQ", "LDQ");  // this column's Q row (k_qrows)
         o << stamp(1);
     } else {
-        o << "    __shared__ __attribute__((aligned(16))) double Pl[LDP];\n"
-             "    __shared__ u32 Qs[NCOEF + 1];\n"
-             "    __shared__ u32 Qi[NQI];\n";
-        stage("Pl", "Pc + (size_t)ic * LDP", "LDP");
-        o << "    for (u32 i = threadIdx.x; i <= NCOEF; i += KBLOCK) Qs[i] = qstart[i];\n"
-             "    for (u32 i = threadIdx.x; i < NQI; i += KBLOCK) Qi[i] = qitem[i];\n"
+        // the k_qrows phases for this one c value (spom_engine.hip k_qrows):
+        // Z per hidden-state row, Pc per item, Q per entry -- all in LDS.
+        // The column tables (host-built, 1 KiB-padded: var-column S, items,
+        // CSR, then zs[k][row]) are copied to LDS by global_load_lds_dwordx4
+        // -- every wave-instruction 1 KiB, all in flight, one barrier.
+        o << "    extern __shared__ __attribute__((aligned(16))) double ct[];\n"
+             "    __shared__ double Zl[NJ];\n"
+             "    __shared__ double Pl[NITEMS];\n"
+             "    const double *Svl = ct;\n"
+             "    const uint2 *Itl = (const uint2 *)(ct + OFF_IT);\n"
+             "    const u32 *Qsl = (const u32 *)(ct + OFF_QS);\n"
+             "    const u32 *Qil = (const u32 *)(ct + OFF_QI);\n"
+             "    const double *zl = ct + OFF_ZS;\n"
+             "    const double c = cvals[ic];\n"
+          << (pl.glds ?
+             "    {\n"
+             "        typedef __attribute__((address_space(3))) void lds_void;\n"
+             "        const u32 w = threadIdx.x >> 6, l = threadIdx.x & 63;\n"
+             "        for (u32 i = w * 128; i < ct_len; i += KBLOCK * 2)\n"
+             "            __builtin_amdgcn_global_load_lds((const void *)(coltab + i + 2 * l), (lds_void *)(ct + i), 16, 0, 0);\n"
+             "    }\n" :
+             "    {\n"
+             "        const double2 *src = (const double2 *)coltab;\n"
+             "        double2 *dst = (double2 *)ct;\n"
+             "        const u32 n2 = ct_len / 2;\n"
+             "        double2 t[NSTG];\n"
+             "#pragma unroll\n"
+             "        for (int k = 0; k < NSTG; ++k) {\n"
+             "            const u32 i = threadIdx.x + k * KBLOCK;\n"
+             "            t[k] = src[i < n2 ? i : 0];\n"
+             "        }\n"
+             "#pragma unroll\n"
+             "        for (int k = 0; k < NSTG; ++k) {\n"
+             "            const u32 i = threadIdx.x + k * KBLOCK;\n"
+             "            if (i < n2) dst[i] = t[k];\n"
+             "        }\n"
+             "    }\n") <<
+             "    __syncthreads();\n"
+          << stamp(4) <<
+             "#pragma unroll\n"
+             "    for (int k = 0; k < (NJ + KBLOCK - 1) / KBLOCK; ++k) {\n"
+             "        const u32 r = threadIdx.x + k * KBLOCK;\n"
+             "        if (r < NJ) {\n"
+             "            double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
+             "            for (u32 kk = 0; kk < kmax; kk += 8) {\n"
+             "                double sk[8];\n"
+             "#pragma unroll\n"
+             "                for (int u = 0; u < 8; ++u) sk[u] = zl[(kk + u) * NJ + r];\n"
+             "                za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);\n"
+             "                zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);\n"
+             "                zc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);\n"
+             "                zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);\n"
+             "            }\n"
+             "            double z = (za * zb) * (zc * zd);\n"
+             "            if (kmax && !(fma(-c, zl[r], 1.0) > 0.0)) z = 0.0;\n"
+             "            Zl[r] = z;\n"
+             "        }\n"
+             "    }\n"
+             "    __syncthreads();\n"
+          << stamp(5) <<
+             "#pragma unroll\n"
+             "    for (int k = 0; k < (NITEMS + KBLOCK - 1) / KBLOCK; ++k) {\n"
+             "        const u32 it = threadIdx.x + k * KBLOCK;\n"
+             "        if (it < NITEMS) {\n"
+             "            const uint2 t = Itl[it];\n"
+             "            const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
+             "            double p = Zl[r];\n"
+             "#pragma unroll\n"
+             "            for (int b = 0; b < NVAR; ++b) {\n"
+             "                const u32 bit = NVAR - 1 - b;\n"
+             "                double pcv = c * Svl[r * NVAR + b];\n"
+             "                pcv = pcv > 1.0 ? 1.0 : pcv;\n"
+             "                const double f = ((B >> bit) & 1u) ? pcv : 1.0 - pcv;\n"
+             "                p *= ((j >> bit) & 1u) ? 1.0 : f;\n"
+             "            }\n"
+             "            Pl[it] = p;\n"
+             "        }\n"
+             "    }\n"
              "    __syncthreads();\n"
           << stamp(1) <<
-             // Q_ab[m] = sum over the pair's hidden states j (|j| = m,
-             // ascending) of Pc[j][b]: fixed order, deterministic
-             "    for (u32 q = threadIdx.x; q < LDQ; q += KBLOCK) {\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < (LDQ + KBLOCK - 1) / KBLOCK; ++k) {\n"
+             "        const u32 q = threadIdx.x + k * KBLOCK;\n"
              "        double a = 0.0;\n"
              "        if (q < NCOEF)\n"
-             "            for (u32 i = Qs[q], i1 = Qs[q + 1]; i < i1; ++i) a += Pl[Qi[i]];\n"
-             "        Ql[q] = a;\n"
+             "            for (u32 i = Qsl[q]; i < Qsl[q + 1]; ++i) a += Pl[Qil[i]];\n"
+             "        if (q < LDQ) Ql[q] = a;\n"
              "    }\n";
     }
     o <<
@@ -227,6 +303,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             last[pl.udesc[i]] = i;
         }
     }
+    // flops per point: weight table, transitions (below), prior sum
+    double flops = 2.0 * dmax + (double)nw + 2.0 * npmax;
     std::vector<uint32_t> slot_key(nslot, 0);
     std::vector<size_t> slot_next(nslot, SIZE_MAX);  // SIZE_MAX: free / dead
     // returns the expression for use u, emitting "pc[i][s] = P;" first when
@@ -238,6 +316,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                 slot_next[sl] = next_use[u];
                 return "pc[i][" + std::to_string(sl) + "]";
             }
+        flops += 2.0 * ((d >> 22) & 31u) + 1.0;  // nX FMAs + 1 MUL
         const std::string e = pexpr(d);
         if (nslot == 0 || next_use[u] == SIZE_MAX || next_use[u] - u > kHorizon) return "(" + e + ")";
         int best = 0;
@@ -256,6 +335,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             std::string pre;
             const std::string e = use_expr(u++, pre);
             o << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
+            flops += 1.0;
             fence();
             continue;
         }
@@ -266,6 +346,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                 const std::string e = use_expr(u++, pre);
                 o << "    for (int i = 0; i < EPL; ++i) { " << pre << "n[i][" << l << "] = fma(v[i][" << k << "], "
                   << e << ", " << (k ? "n[i][" + std::to_string(l) + "]" : std::string("0.0")) << "); }\n";
+                flops += k ? 2.0 : 1.0;
                 fence();
             }
         o << "    for (int i = 0; i < EPL; ++i) {\n";
@@ -284,6 +365,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
          "    }\n"
       << stamp(7) << "}\n";
+    pl.flops_pt = flops;
     o << "// EPL_CHOSEN " << EPL << "\n";
     return o.str();
 }

@@ -9,16 +9,22 @@
 struct MdpJitPlan {
     std::vector<uint32_t> np;     // possible states per year
     std::vector<uint32_t> udesc;  // per forward use: Q offset | nX << 22 | nA << 27
-    size_t ldQ = 0;               // Q block in LDS (doubles, even)
-    size_t ncoef = 0;             // Q entries assembled from the colonisation factors
-    size_t ldP = 0;               // per-c colonisation-factor row Pc[c][item] (doubles, even)
-    size_t nqi = 0;               // length of the Q-assembly item list (qitem)
+    size_t ldQ = 0;               // per-c Q row (doubles, even), staged in LDS
+    // fused variant: the kernel computes its column's Q itself (k_qrows'
+    // three phases for one c value) instead of reading Q rows
+    bool fused = false;
+    uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
+    // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
+    // items, qstart, qitem, then zs[kmax][nj]
+    uint32_t off_it = 0, off_qs = 0, off_qi = 0, off_zs = 0;
+    bool glds = false;  // stage the column tables with global_load_lds (else registers)
+    uint32_t ct_max = 0;  // largest column-table image (doubles), for the register staging
     int epl = 0;                  // grid points per lane (0: 2 unless the weight table is large)
     int window = 8;               // transitions per scheduling region
     bool diag = false;            // record s_memtime phase stamps (MDP_DIAG)
     bool xcd = true;              // XCD-aware block order
-    bool qsum = true;             // Q rows come from k_qsum (else assembled from Pc in LDS)
     int slots = 8;                // registers caching transitions that recur (0: none)
+    double flops_pt = 0;          // out: FP64 flops per grid point of the generated code
 };
 
 // HIP source of `mdp_fwd_jit` for this plan; sets plan.epl when it was 0.

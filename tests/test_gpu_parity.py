@@ -123,20 +123,22 @@ def test_q5_impossible_transition(tmp_path):
 # ---------------------------------------------------------------------------
 # fuzzing: random problems covering every forward-kernel variant
 # ---------------------------------------------------------------------------
-@pytest.fixture(params=["direct", "direct-qsum", "direct-inline-q", "generic"])
+@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic"])
 def engine_path(request, monkeypatch):
-    """Every engine path: the direct one (k_colonise + the hipRTC-specialised
-    forward kernel, the default; k_qsum assembles Q when a c column spans
-    several e blocks), the direct one with k_qsum forced (MDP_QSUM=1) or
-    disabled (MDP_QSUM=0), and the generic kernels (MDP_JIT=0)."""
-    monkeypatch.delenv("MDP_JIT", raising=False)
-    monkeypatch.delenv("MDP_QSUM", raising=False)
+    """Every engine path: the direct one (the hipRTC-specialised forward
+    kernel; on these small grids it computes its column's Q itself), the same
+    with Q rows from k_qrows (MDP_FUSED=0), the direct path with the
+    transition cache and XCD ordering off (MDP_JIT_SLOTS=0, MDP_JIT_XCD=0), and
+    the generic kernels (MDP_JIT=0)."""
+    for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED"):
+        monkeypatch.delenv(k, raising=False)
     if request.param == "generic":
         monkeypatch.setenv("MDP_JIT", "0")
-    elif request.param == "direct-inline-q":
-        monkeypatch.setenv("MDP_QSUM", "0")
-    elif request.param == "direct-qsum":
-        monkeypatch.setenv("MDP_QSUM", "1")
+    elif request.param == "direct-qrows":
+        monkeypatch.setenv("MDP_FUSED", "0")
+    elif request.param == "direct-plain":
+        monkeypatch.setenv("MDP_JIT_SLOTS", "0")
+        monkeypatch.setenv("MDP_JIT_XCD", "0")
     return request.param
 
 
@@ -234,8 +236,7 @@ def test_device_run_matches_host_path(golden):
         torch.cuda.synchronize()
         ms = eng.kernel_ms()
     assert np.array_equal(out[:, :96].cpu().numpy(), host)
-    assert set(ms) in ({"k_colonise", "k_qsum", "k_forward"}, {"k_colonise", "k_forward"},
-                       {"k_zpv", "k_coefs", "k_forward"})
+    assert set(ms) in ({"k_forward"}, {"k_qrows", "k_forward"}, {"k_zpv", "k_coefs", "k_forward"})
     assert all(v > 0 for v in ms.values())
 
 
@@ -248,12 +249,26 @@ def test_direct_and_generic_paths_agree(golden, monkeypatch, fname, s):
     with mdp.Engine(model) as eng:
         assert eng.info()["variant"] >= 10000  # the direct path is the default
         a = eng.loglik_grid(g, c)
-        assert set(eng.kernel_ms()) <= {"k_colonise", "k_qsum", "k_forward"}
+        assert set(eng.kernel_ms()) <= {"k_qrows", "k_forward"}
     monkeypatch.setenv("MDP_JIT", "0")
     with mdp.Engine(model) as eng:
         assert eng.info()["variant"] < 10000
         b = eng.loglik_grid(g, c)
     assert_loglik_close(a, b, atol=1e-11)
+
+
+@pytest.mark.parametrize("fname,s", [("config2_64x50.txt", 200), ("config3_256x200.txt", 64)])
+def test_fused_and_qrows_identical(golden, monkeypatch, fname, s):
+    """The fused forward kernel runs k_qrows' arithmetic for its column: the
+    two direct variants agree bit for bit."""
+    model = mdp.Model.load(golden / fname)
+    g, _ = mdp.grid(s)
+    out = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MDP_FUSED", mode)
+        with mdp.Engine(model) as eng:
+            out.append(eng.loglik_grid(g, g))
+    assert np.array_equal(out[0], out[1])
 
 
 def test_explicit_device_list(golden):
