@@ -1179,7 +1179,8 @@ int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 // dynamic LDS), Z, Pc and Q in LDS.
 size_t fused_lds(const mdp_engine *eng, size_t ct_len)
 {
-    return (ct_len + eng->nj + eng->nitems + eng->ldQ) * sizeof(double);
+    const size_t fc = (size_t)eng->jit_plan.fused_cols;
+    return (ct_len + fc * (eng->nj + eng->nitems + eng->ldQ)) * sizeof(double);
 }
 
 int upload_binomials()  // into the current device's constant bank
@@ -1377,11 +1378,12 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
                         (void *)&out,  (void *)&ld,     (void *)&one, (void *)&st, (void *)&cv,
                         (void *)&ctab, (void *)&ctl,    (void *)&kmax};
         const uint64_t gy = (d.ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
-        const uint64_t nb = gy * d.nc;
-        if (nb * kBlock > 0xffffffffull)
+        const uint32_t fc = d.fused ? (uint32_t)eng->jit_plan.fused_cols : 1u;
+        const uint64_t nb = d.fused ? (d.nc + fc - 1) / fc : gy * d.nc;
+        if (nb * kBlock * fc > 0xffffffffull)
             return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
         const uint32_t dyn = d.fused ? d.ct_len * (uint32_t)sizeof(double) : 0u;
-        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kBlock), 1, 1, kBlock, 1, 1, dyn, s, args,
+        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kBlock * fc), 1, 1, kBlock * fc, 1, 1, dyn, s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));
         return MDP_OK;
     }
@@ -1569,6 +1571,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             // compile the variant a small grid uses now (the other on demand)
             if (const char *fv = getenv("MDP_FUSED")) eng->fused_mode = atoi(fv) != 0;
             if (const char *gv = getenv("MDP_JIT_GLDS")) plan.glds = atoi(gv) != 0;
+            if (const char *cv = getenv("MDP_FUSED_COLS")) plan.fused_cols = std::max(1, std::min(4, atoi(cv)));
             plan.nj = eng->nj;
             plan.nvar = eng->nvar;
             plan.nitems = eng->nitems;

@@ -19,6 +19,7 @@
 #include <map>
 #include <mutex>
 #include <sstream>
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <sys/stat.h>
@@ -122,13 +123,15 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         o << "#define NJ " << pl.nj << "\n#define NVAR " << pl.nvar << "\n#define NITEMS " << pl.nitems
           << "\n#define NCOEF " << pl.ncoef << "\n#define NQI " << (pl.nqi ? pl.nqi : 1) << "\n#define OFF_IT "
           << pl.off_it << "\n#define OFF_QS " << pl.off_qs << "\n#define OFF_QI " << pl.off_qi << "\n#define OFF_ZS "
-          << pl.off_zs << "\n#define NSTG " << ((pl.ct_max / 2 + 255) / 256 > 0 ? (pl.ct_max / 2 + 255) / 256 : 1)
-          << "\n";
-    o << "extern \"C\" __global__ __launch_bounds__(KBLOCK) void mdp_fwd_jit(\n"
+          << pl.off_zs << "\n#define NSTG "
+          << std::max<uint32_t>(1u, (pl.ct_max / 2 + 256u * pl.fused_cols - 1) / (256u * pl.fused_cols)) << "\n";
+    const int FC = pl.fused ? (pl.fused_cols > 0 ? pl.fused_cols : 1) : 1;
+    o << "#define FC " << FC << "\n#define NT (KBLOCK * FC)\n";
+    o << "extern \"C\" __global__ __launch_bounds__(NT) void mdp_fwd_jit(\n"
          "    const double *__restrict__ Qrow, double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
          "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps,\n"
          "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax)\n{\n"
-         "    __shared__ __attribute__((aligned(16))) double Ql[LDQ];\n"
+         "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ];\n"
       << stamp(6) << stamp(0) <<
          // XCD-aware order: the dispatcher deals blocks round-robin over the 8
          // XCDs, so consecutive logical blocks (adjacent c columns of the
@@ -136,7 +139,11 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    const u32 nb = gridDim.x, full = nb & ~7u;\n"
       << (pl.xcd ? "    const u32 lb = blockIdx.x < full ? (blockIdx.x & 7u) * (full >> 3) + (blockIdx.x >> 3) : blockIdx.x;\n"
                  : "    const u32 lb = blockIdx.x + 0 * full;\n") <<
-         "    const u32 ic = lb % nc, by = lb / nc;\n";
+         // FC columns per workgroup (fused variant): KBLOCK threads each
+         "    const u32 half = threadIdx.x / KBLOCK, tid = threadIdx.x % KBLOCK;\n"
+         "    const u32 ic0 = FC == 1 ? lb % nc : lb * FC, by = FC == 1 ? lb / nc : 0u;\n"
+         "    const u32 ic = ic0 + half;\n"
+         "    const double *Qh = Ql + half * LDQ;\n";
     // stage n doubles from src (16-byte aligned, n even) into the LDS array dst
     auto stage = [&](const char *dst, const char *src, const char *n) {
         o << "    {\n"
@@ -161,19 +168,21 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         // CSR, then zs[k][row]) are copied to LDS by global_load_lds_dwordx4
         // -- every wave-instruction 1 KiB, all in flight, one barrier.
         o << "    extern __shared__ __attribute__((aligned(16))) double ct[];\n"
-             "    __shared__ double Zl[NJ];\n"
-             "    __shared__ double Pl[NITEMS];\n"
+             "    __shared__ double Zl[FC * NJ];\n"
+             "    __shared__ double Pl[FC * NITEMS];\n"
              "    const double *Svl = ct;\n"
              "    const uint2 *Itl = (const uint2 *)(ct + OFF_IT);\n"
              "    const u32 *Qsl = (const u32 *)(ct + OFF_QS);\n"
              "    const u32 *Qil = (const u32 *)(ct + OFF_QI);\n"
              "    const double *zl = ct + OFF_ZS;\n"
-             "    const double c = cvals[ic];\n"
+             "    double cc[FC];\n"
+             "#pragma unroll\n"
+             "    for (int f = 0; f < FC; ++f) cc[f] = ic0 + f < nc ? cvals[ic0 + f] : 0.0;\n"
           << (pl.glds ?
              "    {\n"
              "        typedef __attribute__((address_space(3))) void lds_void;\n"
              "        const u32 w = threadIdx.x >> 6, l = threadIdx.x & 63;\n"
-             "        for (u32 i = w * 128; i < ct_len; i += KBLOCK * 2)\n"
+             "        for (u32 i = w * 128; i < ct_len; i += NT * 2)\n"
              "            __builtin_amdgcn_global_load_lds((const void *)(coltab + i + 2 * l), (lds_void *)(ct + i), 16, 0, 0);\n"
              "    }\n" :
              "    {\n"
@@ -183,21 +192,23 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        double2 t[NSTG];\n"
              "#pragma unroll\n"
              "        for (int k = 0; k < NSTG; ++k) {\n"
-             "            const u32 i = threadIdx.x + k * KBLOCK;\n"
+             "            const u32 i = threadIdx.x + k * NT;\n"
              "            t[k] = src[i < n2 ? i : 0];\n"
              "        }\n"
              "#pragma unroll\n"
              "        for (int k = 0; k < NSTG; ++k) {\n"
-             "            const u32 i = threadIdx.x + k * KBLOCK;\n"
+             "            const u32 i = threadIdx.x + k * NT;\n"
              "            if (i < n2) dst[i] = t[k];\n"
              "        }\n"
              "    }\n") <<
              "    __syncthreads();\n"
           << stamp(4) <<
              "#pragma unroll\n"
-             "    for (int k = 0; k < (NJ + KBLOCK - 1) / KBLOCK; ++k) {\n"
-             "        const u32 r = threadIdx.x + k * KBLOCK;\n"
-             "        if (r < NJ) {\n"
+             "    for (int k = 0; k < (FC * NJ + NT - 1) / NT; ++k) {\n"
+             "        const u32 w = threadIdx.x + k * NT;\n"
+             "        if (w < FC * NJ) {\n"
+             "            const u32 col = w % FC, r = w / FC;\n"
+             "            const double c = cc[col];\n"
              "            double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
              "            for (u32 kk = 0; kk < kmax; kk += 8) {\n"
              "                double sk[8];\n"
@@ -210,18 +221,20 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "            }\n"
              "            double z = (za * zb) * (zc * zd);\n"
              "            if (kmax && !(fma(-c, zl[r], 1.0) > 0.0)) z = 0.0;\n"
-             "            Zl[r] = z;\n"
+             "            Zl[col * NJ + r] = z;\n"
              "        }\n"
              "    }\n"
              "    __syncthreads();\n"
           << stamp(5) <<
              "#pragma unroll\n"
-             "    for (int k = 0; k < (NITEMS + KBLOCK - 1) / KBLOCK; ++k) {\n"
-             "        const u32 it = threadIdx.x + k * KBLOCK;\n"
-             "        if (it < NITEMS) {\n"
+             "    for (int k = 0; k < (FC * NITEMS + NT - 1) / NT; ++k) {\n"
+             "        const u32 w = threadIdx.x + k * NT;\n"
+             "        if (w < FC * NITEMS) {\n"
+             "            const u32 col = w % FC, it = w / FC;\n"
+             "            const double c = cc[col];\n"
              "            const uint2 t = Itl[it];\n"
              "            const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
-             "            double p = Zl[r];\n"
+             "            double p = Zl[col * NJ + r];\n"
              "#pragma unroll\n"
              "            for (int b = 0; b < NVAR; ++b) {\n"
              "                const u32 bit = NVAR - 1 - b;\n"
@@ -230,25 +243,28 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "                const double f = ((B >> bit) & 1u) ? pcv : 1.0 - pcv;\n"
              "                p *= ((j >> bit) & 1u) ? 1.0 : f;\n"
              "            }\n"
-             "            Pl[it] = p;\n"
+             "            Pl[col * NITEMS + it] = p;\n"
              "        }\n"
              "    }\n"
              "    __syncthreads();\n"
           << stamp(1) <<
              "#pragma unroll\n"
-             "    for (int k = 0; k < (LDQ + KBLOCK - 1) / KBLOCK; ++k) {\n"
-             "        const u32 q = threadIdx.x + k * KBLOCK;\n"
-             "        double a = 0.0;\n"
-             "        if (q < NCOEF)\n"
-             "            for (u32 i = Qsl[q]; i < Qsl[q + 1]; ++i) a += Pl[Qil[i]];\n"
-             "        if (q < LDQ) Ql[q] = a;\n"
+             "    for (int k = 0; k < (FC * LDQ + NT - 1) / NT; ++k) {\n"
+             "        const u32 w = threadIdx.x + k * NT;\n"
+             "        if (w < FC * LDQ) {\n"
+             "            const u32 col = w / LDQ, q = w - col * LDQ;\n"
+             "            double a = 0.0;\n"
+             "            if (q < NCOEF)\n"
+             "                for (u32 i = Qsl[q]; i < Qsl[q + 1]; ++i) a += Pl[col * NITEMS + Qil[i]];\n"
+             "            Ql[w] = a;\n"
+             "        }\n"
              "    }\n";
     }
     o <<
          "    u32 ie[EPL];\n    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n"
          "#pragma unroll\n"
          "    for (int i = 0; i < EPL; ++i) {\n"
-         "        ie[i] = by * (KBLOCK * EPL) + i * KBLOCK + threadIdx.x;\n"
+         "        ie[i] = by * (KBLOCK * EPL) + i * KBLOCK + tid;\n"
          "        const double e = ie[i] < ne ? evals[ie[i]] : 0.0;\n"
          "        const double x = e > 1.0 ? 1.0 : e;\n"
          "        const double y = 1.0 - x;\n"
@@ -265,10 +281,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     // P = sum_m Q[off+m] W[|A|][m] as an expression for point i
     auto pexpr = [&](uint32_t d) {
         const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u, nA = d >> 27;
-        std::string e = "Ql[" + std::to_string(off) + "] * W[i][" +
+        std::string e = "Qh[" + std::to_string(off) + "] * W[i][" +
                         std::to_string(widx[std::make_pair(nA, 0u)]) + "]";
         for (uint32_t m = 1; m <= nX; ++m)
-            e = "fma(Ql[" + std::to_string(off + m) + "], W[i][" +
+            e = "fma(Qh[" + std::to_string(off + m) + "], W[i][" +
                 std::to_string(widx[std::make_pair(nA, m)]) + "], " + e + ")";
         return e;
     };
@@ -362,7 +378,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "        double L = 0.0;\n"
          "#pragma unroll\n"
          "        for (int l = 0; l < NPMAX; ++l) L += v[i][l] * prior0;\n"
-         "        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
+         "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
          "    }\n"
       << stamp(7) << "}\n";
     pl.flops_pt = flops;

@@ -13,6 +13,7 @@ struct MdpJitPlan {
     // fused variant: the kernel computes its column's Q itself (k_qrows'
     // three phases for one c value) instead of reading Q rows
     bool fused = false;
+    int fused_cols = 2;  // c columns per fused workgroup (KBLOCK threads each)
     uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
     // items, qstart, qitem, then zs[kmax][nj]
