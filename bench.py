@@ -144,22 +144,26 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    # Kernel durations: the same K steps again, every kernel launched with its
-    # own start/stop HIP events (hipExtLaunchKernel).  Kept out of the timed
-    # region above because the event completion signals cost the stream
-    # several microseconds between kernels; the per-kernel durations agree
-    # with rocprofv3 --kernel-trace (profiles/).
-    eng.set_profiling(True)
-    for _ in range(args.steps):
-        step()
+    # Kernel durations, measured live with HIP events on the engine's stream:
+    # each kernel of the path launched K times back to back between two
+    # events (mdp_engine_time_kernels; no per-launch events, whose completion
+    # signals would add microseconds to every launch).  They agree with
+    # rocprofv3 --kernel-trace --stats of the same command (profiles/).
+    kms = eng.time_kernels(out.data_ptr(), s, stream, reps=args.steps)
     torch.cuda.synchronize(dev)
-    kms = eng.kernel_ms()
-    eng.set_profiling(False)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    # HBM traffic of the forward kernel per launch, from the committed
+    # rocprofv3 PMC passes of this workload (scripts/gpu_pmc.sh,
+    # scripts/pmc_traffic.py); null when no profile of this config exists
+    traffic, traffic_src = None, None
+    tf = ROOT / "profiles" / f"pmc_traffic_cfg{args.config}.json"
+    if tf.exists():
+        traffic = json.loads(tf.read_text())["hbm_bytes_per_launch"]
+        traffic_src = str(tf.relative_to(ROOT))
     units = world * s * s * (tmax - 1) * args.steps
     work = eng.work(s, s)
     info = eng.info()
@@ -190,7 +194,9 @@ def main():
             "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved_tf / FP64_PEAK_TFLOPS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
             "flop_per_launch": work["flop_impl"],
             "flop_per_launch_survey_dense": work["flop_survey"],
             # SURVEY §8(d) F_alg over the whole step: exceeds the FP64 peak

@@ -134,6 +134,14 @@ int mdp_engine_set_profiling(mdp_engine *engine, int enable);
 int mdp_engine_kernel_ms(mdp_engine *engine, double *ms, int max_k);
 const char *mdp_engine_kernel_name(const mdp_engine *engine, int k);
 
+/* Per-kernel durations without per-launch events: one full run into d_out,
+ * then each kernel of the path launched `reps` times back to back between two
+ * events on `stream`; ms[k] = mean duration of slot k (0 where the path has no
+ * such kernel; names via mdp_engine_kernel_name), and a final full run leaves
+ * d_out as mdp_engine_run computes it.  Returns the number of slots filled. */
+int mdp_engine_time_kernels(mdp_engine *engine, double *d_out, uint32_t ld_out, void *stream, int reps,
+                            double *ms, int max_k);
+
 /* Diagnostics (MDP_DIAG=1 in the environment at engine creation): text
  * report of per-workgroup s_memtime phase durations (shader cycles) of the
  * last run's kernels; returns the report length (0 when disabled). */

@@ -185,6 +185,15 @@ class Engine:
         names = [lib().mdp_engine_kernel_name(self._h, i).decode() for i in range(k)]
         return {nm: buf[i] for i, nm in enumerate(names) if nm}
 
+    def time_kernels(self, d_out: int, ld_out: int, stream: int = 0, reps: int = 50) -> dict:
+        """Mean duration (ms) of each kernel of the path, each launched `reps`
+        times back to back (no per-launch events); d_out ends as run() leaves it."""
+        buf = (ctypes.c_double * 3)()
+        k = check(lib().mdp_engine_time_kernels(self._h, ctypes.c_void_p(d_out), ld_out,
+                                                ctypes.c_void_p(stream), reps, buf, 3))
+        names = [lib().mdp_engine_kernel_name(self._h, i).decode() for i in range(k)]
+        return {nm: buf[i] for i, nm in enumerate(names) if nm}
+
     def diag_report(self) -> str:
         """Phase-stamp report of the last run (engine created with MDP_DIAG=1)."""
         buf = ctypes.create_string_buffer(8192)

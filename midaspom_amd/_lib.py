@@ -90,6 +90,8 @@ SIGNATURES = [
     ("mdp_engine_run", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u32, ctypes.c_void_p]),
     ("mdp_engine_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("mdp_engine_kernel_ms", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, ctypes.c_int]),
+    ("mdp_engine_time_kernels", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, c_dbl_p, ctypes.c_int]),
     ("mdp_engine_kernel_name", ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_int]),
     ("mdp_engine_work", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_dbl_p, c_dbl_p, c_dbl_p]),

@@ -792,6 +792,7 @@ struct DevCtx {
     hipFunction_t jit_fn[2] = {nullptr, nullptr};
     bool fused = false;  // this grid runs the fused forward kernel (no k_qrows)
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
+    std::vector<uint8_t> ev_mask;  // per profiled run: slots whose kernel was launched
     size_t ev_used = 0;          // event sets recorded since the last collect
 };
 
@@ -1427,6 +1428,42 @@ int launch_coefs(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
     return MDP_OK;
 }
 
+// Does kernel slot k (0: Q rows / k_zpv, 1: k_coefs, 2: forward) run on this path?
+bool slot_active(const mdp_engine *eng, const DevCtx &d, int k)
+{
+    if (eng->jit) return k == 2 || (k == 0 && eng->nitems && !d.fused);
+    return k != 1 || eng->nuses;
+}
+
+int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hipStream_t s)
+{
+    if (!slot_active(eng, d, k)) return MDP_OK;
+    if (k == 2) return launch_forward(eng, d, out, ld, s);
+    if (eng->jit) {  // k == 0: Q rows
+        const uint32_t cb = d.qrows_cb;
+        const dim3 grid((d.nc + cb - 1) / cb);
+        const size_t lds = qrows_lds(eng, cb);
+#define MDP_QROWS(NV)                                                                                  \
+    MDP_LAUNCH(k_qrows<NV>, grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj, d.zs_kmax, \
+               d.zs, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                               \
+               (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[0])
+        if (eng->nvar <= 8) MDP_QROWS(8);
+        else if (eng->nvar <= 16) MDP_QROWS(16);
+        else MDP_QROWS(24);
+#undef MDP_QROWS
+        HIP_TRY(hipGetLastError());
+        return MDP_OK;
+    }
+    if (k == 0) {
+        dim3 grid((eng->nstates + kZpvJ - 1) / kZpvJ, (d.nc + kZpvCT - 1) / kZpvCT);
+        MDP_LAUNCH(k_zpv, grid, dim3(kBlock), 0, s, d.S, eng->nstates, eng->n - eng->nvar, eng->nvar, d.c,
+                   d.nc, d.ZPV, d.stamps[0]);
+        HIP_TRY(hipGetLastError());
+        return MDP_OK;
+    }
+    return launch_coefs(eng, d, s);
+}
+
 int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
 {
     HIP_TRY(hipSetDevice(d.device));
@@ -1445,56 +1482,51 @@ int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
         }
         ev = &d.ev[d.ev_used * kNumEv];
         ++d.ev_used;
+        d.ev_mask.resize(d.ev_used);
+        d.ev_mask.back() = 0;
     }
-    auto timed = [&](int k) { t_kev = prof ? KernelEvents{ev[2 * k], ev[2 * k + 1]} : KernelEvents{}; };
     struct Reset {
         ~Reset() { t_kev = KernelEvents{}; }
     } reset;
-    if (eng->jit) {  // direct path: colonisation factors, then the specialised forward kernel
-        timed(0);
-        if (eng->nitems && !d.fused) {
-            const uint32_t cb = d.qrows_cb;
-            const dim3 grid((d.nc + cb - 1) / cb);
-            const size_t lds = qrows_lds(eng, cb);
-#define MDP_QROWS(NV)                                                                                  \
-    MDP_LAUNCH(k_qrows<NV>, grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj, d.zs_kmax, \
-               d.zs, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                               \
-               (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[0])
-            if (eng->nvar <= 8) MDP_QROWS(8);
-            else if (eng->nvar <= 16) MDP_QROWS(16);
-            else MDP_QROWS(24);
-#undef MDP_QROWS
-            HIP_TRY(hipGetLastError());
-        } else if (prof) {
-            HIP_TRY(hipEventRecord(ev[0], s));
-            HIP_TRY(hipEventRecord(ev[1], s));
-        }
-        if (prof) {  // no second kernel on this path
-            HIP_TRY(hipEventRecord(ev[2], s));
-            HIP_TRY(hipEventRecord(ev[3], s));
-        }
-        timed(2);
-        return launch_forward(eng, d, out, ld, s);
-    }
-    {
-        timed(0);
-        dim3 grid((eng->nstates + kZpvJ - 1) / kZpvJ, (d.nc + kZpvCT - 1) / kZpvCT);
-        MDP_LAUNCH(k_zpv, grid, dim3(kBlock), 0, s, d.S, eng->nstates, eng->n - eng->nvar,
-                   eng->nvar, d.c, d.nc, d.ZPV, d.stamps[0]);
-        HIP_TRY(hipGetLastError());
-    }
-    if (eng->nuses) {
-        timed(1);
-        int rc = launch_coefs(eng, d, s);
+    for (int k = 0; k < 3; ++k) {
+        if (!slot_active(eng, d, k)) continue;
+        // only launched kernels carry events (no marker packets between kernels)
+        t_kev = prof ? KernelEvents{ev[2 * k], ev[2 * k + 1]} : KernelEvents{};
+        if (prof) d.ev_mask.back() |= (uint8_t)(1u << k);
+        int rc = launch_slot(eng, d, k, out, ld, s);
         if (rc) return rc;
-    } else if (prof) {  // no coefficient kernel: zero-length interval
-        HIP_TRY(hipEventRecord(ev[2], s));
-        HIP_TRY(hipEventRecord(ev[3], s));
     }
-    timed(2);
-    int rc = launch_forward(eng, d, out, ld, s);
-    if (rc) return rc;
     return MDP_OK;
+}
+
+// Mean duration of each kernel of the run: one full run, then every kernel
+// launched `reps` times back to back between two events on the stream (no
+// per-launch events, so the figure is the kernel's own, as rocprofv3 sees it).
+int time_kernels(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s, int reps, double *ms)
+{
+    int rc = run_dev(eng, d, out, ld, s);
+    if (rc) return rc;
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreate(&a));
+    HIP_TRY(hipEventCreate(&b));
+    for (int k = 0; k < 3; ++k) {
+        ms[k] = 0.0;
+        if (!slot_active(eng, d, k)) continue;
+        if ((rc = launch_slot(eng, d, k, out, ld, s))) break;  // warm
+        (void)hipEventRecord(a, s);
+        for (int r = 0; r < reps && !rc; ++r) rc = launch_slot(eng, d, k, out, ld, s);
+        (void)hipEventRecord(b, s);
+        if (rc) break;
+        float t = 0;
+        (void)hipEventSynchronize(b);
+        (void)hipEventElapsedTime(&t, a, b);
+        ms[k] = t / reps;
+    }
+    // leave the output as a full run computes it
+    if (!rc) rc = run_dev(eng, d, out, ld, s);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return rc;
 }
 
 // Mean kernel durations over every profiled run since the last collect.
@@ -1504,13 +1536,16 @@ int collect_times(mdp_engine *eng, DevCtx &d)
     HIP_TRY(hipSetDevice(d.device));
     HIP_TRY(hipEventSynchronize(d.ev[(d.ev_used - 1) * kNumEv + kNumEv - 1]));
     double sum[3] = {0, 0, 0};
+    size_t cnt[3] = {0, 0, 0};
     for (size_t r = 0; r < d.ev_used; ++r)
         for (int k = 0; k < 3; ++k) {
+            if (!((d.ev_mask[r] >> k) & 1u)) continue;
             float ms = 0;
             HIP_TRY(hipEventElapsedTime(&ms, d.ev[r * kNumEv + 2 * k], d.ev[r * kNumEv + 2 * k + 1]));
             sum[k] += ms;
+            ++cnt[k];
         }
-    for (int k = 0; k < 3; ++k) eng->last_ms[k] = sum[k] / (double)d.ev_used;
+    for (int k = 0; k < 3; ++k) eng->last_ms[k] = cnt[k] ? sum[k] / (double)cnt[k] : 0.0;
     eng->nlast = 3;
     eng->runs_collected = d.ev_used;
     d.ev_used = 0;
@@ -1752,6 +1787,25 @@ int mdp_engine_set_profiling(mdp_engine *eng, int enable)
     if (!eng) return mdp_set_error(MDP_EINVAL, "null engine");
     eng->profiling = enable;
     return MDP_OK;
+}
+
+int mdp_engine_time_kernels(mdp_engine *eng, double *d_out, uint32_t ld_out, void *stream, int reps,
+                            double *ms, int max_k)
+{
+    if (!eng || !d_out || !ms || reps < 1) return mdp_set_error(MDP_EINVAL, "bad argument");
+    if (eng->devs.size() != 1)
+        return mdp_set_error(MDP_EINVAL, "mdp_engine_time_kernels needs a single-device engine");
+    DevCtx &d = eng->devs[0];
+    if (ld_out < d.nc) return mdp_set_error(MDP_EINVAL, "ld_out %u < nc %u", ld_out, d.nc);
+    double t[3];
+    const int saved = eng->profiling;
+    eng->profiling = 0;
+    int rc = time_kernels(eng, d, d_out, ld_out, stream ? (hipStream_t)stream : d.stream, reps, t);
+    eng->profiling = saved;
+    if (rc) return rc;
+    const int k = std::min(max_k, 3);
+    for (int i = 0; i < k; ++i) ms[i] = t[i];
+    return k;
 }
 
 int mdp_engine_kernel_ms(mdp_engine *eng, double *ms, int max_k)

@@ -240,6 +240,22 @@ def test_device_run_matches_host_path(golden):
     assert all(v > 0 for v in ms.values())
 
 
+def test_time_kernels_leaves_run_output(golden):
+    import torch
+    model = mdp.Model.load(golden / "config3_256x200.txt")
+    g, _ = mdp.grid(600)
+    with mdp.Engine(model) as eng:
+        eng.set_grid(g, g)
+        st = torch.cuda.current_stream().cuda_stream
+        a = torch.empty((600, 600), dtype=torch.float64, device="cuda")
+        b = torch.empty_like(a)
+        eng.run(a.data_ptr(), 600, st)
+        ms = eng.time_kernels(b.data_ptr(), 600, st, reps=3)
+        torch.cuda.synchronize()
+    assert "k_forward" in ms and all(v > 0 for v in ms.values())
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("fname,s", [("config2_64x50.txt", 256), ("config3_256x200.txt", 128)])
 def test_direct_and_generic_paths_agree(golden, monkeypatch, fname, s):
     model = mdp.Model.load(golden / fname)
