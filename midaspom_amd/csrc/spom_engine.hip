@@ -208,6 +208,44 @@ __global__ __launch_bounds__(kBlock) void k_zpv(
     MDP_RSTAMP(stamps, 7);
 }
 
+// Z rows of the direct path: Zg[row][c] = prod over the always-zero columns k
+// of 1 - min(1, c S[j][k]) for every needed hidden state j ("row").  Lanes run
+// over 64 c values and each wave over one row, so the S values are LDS
+// broadcasts (the workgroup's rows staged once from zs[k][row]); the product
+// is FP64-VALU bound.  Same multiplication order as the fused forward kernel
+// (four chains over k mod 8), so both variants give identical bits.
+constexpr uint32_t kZRows = kBlock / 64;  // rows per workgroup
+__global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cvals, uint32_t nc,
+                                                  uint32_t nrows, uint32_t kmax,
+                                                  const double *__restrict__ zs, double *__restrict__ Zg)
+{
+    extern __shared__ __attribute__((aligned(16))) double zl[];  // [kZRows][kmax]
+    const uint32_t r0 = blockIdx.y * kZRows, nr = min(kZRows, nrows - r0);
+    for (uint32_t i = threadIdx.x; i < kZRows * kmax; i += kBlock) {
+        const uint32_t w = i % kZRows, k = i / kZRows;
+        zl[w * kmax + k] = w < nr ? zs[(size_t)k * nrows + r0 + w] : 0.0;
+    }
+    __syncthreads();
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    if (w >= nr) return;
+    const uint32_t ic = blockIdx.x * 64 + (threadIdx.x & 63);
+    const double c = ic < nc ? cvals[ic] : 0.0;
+    const double *z = zl + w * kmax;
+    double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;
+    for (uint32_t k = 0; k < kmax; k += 8) {
+        double sk[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sk[u] = z[k + u];
+        za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
+        zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);
+        zc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);
+        zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
+    }
+    double zz = (za * zb) * (zc * zd);
+    if (kmax && !(fma(-c, z[0], 1.0) > 0.0)) zz = 0.0;
+    if (ic < nc) Zg[(size_t)(r0 + w) * nc + ic] = zz;
+}
+
 // Transition coefficients of the direct path, one workgroup per kQrowsMaxC
 // (or fewer) consecutive c values, every hidden state j some transition needs
 // ("rows", r) and every (j, b) item:
@@ -228,7 +266,7 @@ constexpr uint32_t kQrowsMaxC = 4;
 template <int NV>
 __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     const double *__restrict__ cvals, uint32_t nc, uint32_t cb, uint32_t nvar, uint32_t nrows,
-    uint32_t kmax, const double *__restrict__ zs, const double *__restrict__ sv,
+    const double *__restrict__ Zg, const double *__restrict__ sv,
     uint32_t nitems, const uint2 *__restrict__ items, uint32_t ncoef, const uint32_t *__restrict__ qstart,
     uint32_t nqi, const uint32_t *__restrict__ qitem, double *__restrict__ Q, uint32_t ldQ,
     unsigned long long *__restrict__ stamps)
@@ -243,37 +281,29 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     uint2 *It = (uint2 *)(Pl + (size_t)cb * nitems);   // [nitems] {B, j}, row in the top bytes
     uint32_t *Qs = (uint32_t *)(It + nitems);          // [ncoef + 1]
     uint32_t *Qi = Qs + ncoef + 1;                     // [nqi]
-    for (uint32_t i = threadIdx.x; i < nrows * nvar; i += kQrowsBlock) Sv[i] = sv[i];
+    // var-column S transposed to [b][row]: lanes holding items of different
+    // rows read different banks
+    for (uint32_t i = threadIdx.x; i < nrows * nvar; i += kQrowsBlock) Sv[(i % nvar) * nrows + i / nvar] = sv[i];
     for (uint32_t i = threadIdx.x; i < nitems; i += kQrowsBlock) It[i] = items[i];
     for (uint32_t i = threadIdx.x; i <= ncoef; i += kQrowsBlock) Qs[i] = qstart[i];
     for (uint32_t i = threadIdx.x; i < nqi; i += kQrowsBlock) Qi[i] = qitem[i];
-    // 1. Z per (c, row)
-    for (uint32_t w = threadIdx.x; w < ncb * nrows; w += kQrowsBlock) {
-        const uint32_t cl = w % ncb, r = w / ncb;
-        const double c = cvals[c0 + cl];
-        // zs[k][row]: lanes over rows read consecutive addresses; eight
-        // loads in flight per step, four product chains
-        const double *zc0 = zs + r;
-        double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;
-        for (uint32_t k = 0; k < kmax; k += 8) {
-            double sk[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) sk[u] = zc0[(size_t)(k + u) * nrows];
-            za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
-            zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);
-            zc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);
-            zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
-        }
-        double z = (za * zb) * (zc * zd);
-        if (kmax && !(fma(-c, zc0[0], 1.0) > 0.0)) z = 0.0;
-        Zl[cl * nrows + r] = z;
+    // 1. Z per (c, row), computed by k_zrows
+    const uint32_t lcb = cb == 4 ? 2u : cb == 2 ? 1u : 0u;  // cb is 1, 2 or 4
+    for (uint32_t w = threadIdx.x; w < (nrows << lcb); w += kQrowsBlock) {
+        const uint32_t cl = w & (cb - 1), r = w >> lcb;
+        if (cl < ncb) Zl[cl * nrows + r] = Zg[(size_t)r * nc + c0 + cl];
     }
     __syncthreads();
     MDP_STAMP(stamps, 1);
     // 2. Pc per (c, item)
-    for (uint32_t w = threadIdx.x; w < ncb * nitems; w += kQrowsBlock) {
-        const uint32_t cl = w % ncb, it = w / ncb;
-        const double c = cvals[c0 + cl];
+    double cv[kQrowsMaxC];  // this workgroup's c values, loaded once
+#pragma unroll
+    for (uint32_t i = 0; i < kQrowsMaxC; ++i) cv[i] = i < ncb ? cvals[c0 + i] : 0.0;
+    for (uint32_t w = threadIdx.x; w < (nitems << lcb); w += kQrowsBlock) {
+        const uint32_t cl = w & (cb - 1), it = w >> lcb;
+        double c = cv[0];
+#pragma unroll
+        for (uint32_t i = 1; i < kQrowsMaxC; ++i) c = cl == i ? cv[i] : c;
         const uint2 t = It[it];
         const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;
         double p = Zl[cl * nrows + r];
@@ -283,7 +313,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         for (int b = 0; b < NV; ++b) {
             const bool live = (uint32_t)b < nvar;
             const uint32_t bit = live ? nvar - 1 - (uint32_t)b : 0u;
-            double pc = c * Sv[r * nvar + (live ? (uint32_t)b : 0u)];
+            double pc = c * Sv[(live ? (uint32_t)b : 0u) * nrows + r];
             pc = pc > 1.0 ? 1.0 : pc;
             const double f = ((B >> bit) & 1u) ? pc : 1.0 - pc;
             p *= (!live || ((j >> bit) & 1u)) ? 1.0 : f;
@@ -759,7 +789,7 @@ int dev_reserve(T **p, size_t *cap, size_t count)
 
 constexpr int kNumEv = 6;  // start/stop per kernel: k_zpv, k_coefs, k_forward
 const char *const kKernelNames[2][3] = {{"k_zpv", "k_coefs", "k_forward"},
-                                        {"k_qrows", "", "k_forward"}};
+                                        {"k_zrows", "k_qrows", "k_forward"}};
 
 struct DevCtx {
     int device = 0;
@@ -777,10 +807,10 @@ struct DevCtx {
     size_t cap_st[3] = {0, 0, 0};
     size_t nst[3] = {0, 0, 0};
     // direct path: k_qrows tables (zs depends on the grid's c range)
-    double *zs = nullptr, *sv = nullptr, *Qrow = nullptr;
+    double *zs = nullptr, *sv = nullptr, *Qrow = nullptr, *Zg = nullptr;
     uint2 *items = nullptr;  // per item {B | row << 24, j | (row >> 8) << 24}
     uint32_t *itemB = nullptr, *qstart = nullptr, *qitem = nullptr;
-    size_t cap_zs = 0, cap_qrow = 0;
+    size_t cap_zs = 0, cap_qrow = 0, cap_zg = 0;
     uint32_t zs_len = 0;    // doubles in zs = zs_kmax * nj
     double *coltab = nullptr;  // fused kernel's column tables (plan offsets, zs last), 1 KiB padded
     size_t cap_coltab = 0;
@@ -1267,7 +1297,7 @@ void free_device(DevCtx &d)
     (void)hipSetDevice(d.device);
     void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog,
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
-                    d.zs, d.sv, d.Qrow, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
+                    d.zs, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -1291,7 +1321,9 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     if (eng->jit) {
         double cmax = 0.0;
         for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
-        if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ))) return rc;
+        if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ)) ||
+            (rc = dev_reserve(&d.Zg, &d.cap_zg, (size_t)nc * eng->nj + 1)))
+            return rc;
         if (!(d.zs_cmax == cmax) && (rc = upload_qrows_tables(eng, d, cmax))) return rc;
         // one e block per c column and a small per-c problem: the forward
         // kernel computes its column's Q itself (one launch)
@@ -1300,8 +1332,8 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
                   (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
         if ((rc = jit_load(eng, d, d.fused))) return rc;
         // c values per k_qrows workgroup: enough workgroups for every CU, within the LDS
-        uint32_t cb = std::max(1u, std::min(kQrowsMaxC, nc / 256u));
-        while (cb > 1 && qrows_lds(eng, cb) > kQrowsLdsMax) --cb;
+        uint32_t cb = nc >= 1024 ? 4u : nc >= 512 ? 2u : 1u;  // power of two
+        while (cb > 1 && qrows_lds(eng, cb) > kQrowsLdsMax) cb >>= 1;
         d.qrows_cb = cb;
     } else if ((rc = dev_reserve(&d.ZPV, &d.cap_zpv, (size_t)nc * (eng->nvar + 1) * eng->nstates)) ||
                (rc = dev_reserve(&d.R, &d.cap_r, (size_t)nc * ldR_of(eng)))) {
@@ -1431,7 +1463,7 @@ int launch_coefs(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
 // Does kernel slot k (0: Q rows / k_zpv, 1: k_coefs, 2: forward) run on this path?
 bool slot_active(const mdp_engine *eng, const DevCtx &d, int k)
 {
-    if (eng->jit) return k == 2 || (k == 0 && eng->nitems && !d.fused);
+    if (eng->jit) return k == 2 || (k < 2 && eng->nitems && !d.fused);
     return k != 1 || eng->nuses;
 }
 
@@ -1439,14 +1471,22 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
 {
     if (!slot_active(eng, d, k)) return MDP_OK;
     if (k == 2) return launch_forward(eng, d, out, ld, s);
-    if (eng->jit) {  // k == 0: Q rows
+    if (eng->jit && k == 0) {  // Z rows
+        const uint32_t kmax = d.zs_kmax;
+        const dim3 grid((d.nc + 63) / 64, (eng->nj + kZRows - 1) / kZRows);
+        MDP_LAUNCH(k_zrows, grid, dim3(kBlock), (size_t)kZRows * kmax * sizeof(double), s, d.c, d.nc, eng->nj,
+                   kmax, d.zs, d.Zg);
+        HIP_TRY(hipGetLastError());
+        return MDP_OK;
+    }
+    if (eng->jit) {  // k == 1: Q rows
         const uint32_t cb = d.qrows_cb;
         const dim3 grid((d.nc + cb - 1) / cb);
         const size_t lds = qrows_lds(eng, cb);
 #define MDP_QROWS(NV)                                                                                  \
-    MDP_LAUNCH(k_qrows<NV>, grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj, d.zs_kmax, \
-               d.zs, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                               \
-               (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[0])
+    MDP_LAUNCH(k_qrows<NV>, grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj, d.Zg,    \
+               d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart, (uint32_t)eng->qitem.size(),        \
+               d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1])
         if (eng->nvar <= 8) MDP_QROWS(8);
         else if (eng->nvar <= 16) MDP_QROWS(16);
         else MDP_QROWS(24);
@@ -1722,11 +1762,11 @@ int mdp_engine_diag_report(mdp_engine *eng, char *buf, size_t len)
     const char *names[3] = {"k_zpv", "k_coefs", "k_forward_lds"};
     int slots[3] = {3, 5, 3};
     if (eng->jit) {  // direct path: k_qrows and the hipRTC forward kernel
-        names[0] = "k_qrows";
+        names[1] = "k_qrows";
         names[2] = "k_forward(jit)";
-        slots[0] = 4;
+        slots[0] = 0;
+        slots[1] = 4;
         slots[2] = d.fused ? 6 : 4;
-        slots[1] = 0;
     }
     size_t used = 0;
     for (int k = 0; k < 3; ++k) {
@@ -1823,7 +1863,7 @@ int mdp_engine_kernel_ms(mdp_engine *eng, double *ms, int max_k)
 const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
     if (!eng || k < 0 || k >= 3) return "";
-    if (eng->jit && k == 0 && (eng->devs.empty() || eng->devs[0].fused)) return "";  // fused: one kernel
+    if (eng->jit && k < 2 && (eng->devs.empty() || eng->devs[0].fused)) return "";  // fused: one kernel
     return kKernelNames[eng->jit ? 1 : 0][k];
 }
 
