@@ -166,6 +166,37 @@ typedef struct mdp_engine_info {
 } mdp_engine_info;
 int mdp_engine_get_info(const mdp_engine *engine, mdp_engine_info *info);
 
+/* ------------------------------------------------------------------ */
+/* Scenario likelihoods: in-situ die-off and habitat loss              */
+/* (main_MIDASPOM_dieoff.c / main_MIDASPOM_loss.c)     */
+/* ------------------------------------------------------------------ */
+
+/* K grid, log10-spaced on [lo, hi] (dieoff.c:284-286, loss.c:315-317);
+ * source-distance grid, linear on [lo, hi] (loss.c:319-322).  Return g[0]. */
+double mdp_kgrid(uint32_t s, double lo, double hi, double *K);
+double mdp_dgrid(uint32_t s, double lo, double hi, double *d);
+
+typedef struct mdp_scenario mdp_scenario;
+
+/* Engine for the likelihood of the FIRST survey row `row` (n patches, values
+ * -1/0/1; dieoff.c:185-232) under the die-off (kind 0) or habitat-loss
+ * (kind 1) scenario, on HIP device `device`.  m, p, d as for mdp_model_load
+ * (-m, -p, -d).  n <= 8 (the Pc table of 3^n entries lives in LDS). */
+int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, double d, int kind, int device,
+                        mdp_scenario **out);
+void mdp_scenario_destroy(mdp_scenario *scenario);
+
+/* out[((ie*nc + ic)*nK + iK)*nd + id] = L(e, c, K[, dsrc]) =
+ * sum_i sum_s [PK^ts P^tdis]_{i,s} prior_s  (not normalised, not log), with
+ * ts years before the event (-b) and tdis after (-a).  Die-off
+ * (dieoff.c:304-351): PK = Pe(e/K) Pc(c K); dsrc ignored (nd = 1).  Loss
+ * (loss.c:341-386): PK = Pe(e) Pc(c, source K at distance dsrc).  The
+ * reference programs are the cases ne = nc = 1 (K column, or K x d table);
+ * the engine evaluates any (e, c, K[, d]) product grid.  Host memory. */
+int mdp_scenario_lik(mdp_scenario *scenario, int ts, int tdis, const double *e, uint32_t ne,
+                     const double *c, uint32_t nc, const double *K, uint32_t nK, const double *dsrc,
+                     uint32_t nd, double *out);
+
 /* Thread-local description of the last error. */
 const char *mdp_last_error(void);
 

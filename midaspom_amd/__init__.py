@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+from pathlib import Path
 
 import numpy as np
 
@@ -25,7 +26,7 @@ from ._lib import MidaspomError, check, lib
 
 __all__ = [
     "Model", "Engine", "grid", "log_total", "write_posterior", "posterior",
-    "run_file", "MidaspomError",
+    "run_file", "MidaspomError", "Scenario", "kgrid", "dgrid", "first_row",
 ]
 
 
@@ -248,3 +249,80 @@ def run_file(input_path, output_path=None, m=400.0, p=0.5, d=100.0, s=101, lo=0.
     if output_path is not None:
         write_posterior(output_path, lik, ltot)
     return lik, ltot
+
+
+# ---------------------------------------------------------------------------
+# scenario likelihoods: in-situ die-off and habitat loss
+# ---------------------------------------------------------------------------
+def kgrid(s: int, lo: float = 0.1, hi: float = 100.0) -> np.ndarray:
+    """log10-spaced K grid of main_MIDASPOM_dieoff.c:284-286."""
+    K = np.empty(s)
+    lib().mdp_kgrid(s, lo, hi, _dptr(K))
+    return K
+
+
+def dgrid(s: int, lo: float = 200.0, hi: float = 4000.0) -> np.ndarray:
+    """Linear source-distance grid of main_MIDASPOM_loss.c:319-322."""
+    d = np.empty(s)
+    lib().mdp_dgrid(s, lo, hi, _dptr(d))
+    return d
+
+
+def first_row(path) -> np.ndarray:
+    """The first survey row as the scenario programs read it
+    (main_MIDASPOM_dieoff.c:185-201: n from line 1, then n integers)."""
+    data = Path(path).read_bytes()
+    n = 1 + sum(1 for ch in data.split(b"\n", 1)[0] if ch in (32, 9))
+    return np.array([int(t) for t in data.split()[:n]], dtype=np.int32)
+
+
+class Scenario:
+    """GPU likelihood of the first survey row under the die-off (kind
+    'dieoff', main_MIDASPOM_dieoff.c) or habitat-loss (kind 'loss',
+    main_MIDASPOM_loss.c) scenario."""
+
+    def __init__(self, row, kind: str = "dieoff", m: float = 400.0, p: float = 0.5, d: float = 200.0,
+                 device: int = 0):
+        if kind not in ("dieoff", "loss"):
+            raise ValueError("kind must be 'dieoff' or 'loss'")
+        self.kind = kind
+        row = np.ascontiguousarray(row, dtype=np.int32)
+        h = ctypes.c_void_p()
+        check(lib().mdp_scenario_create(row.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row.size, m, p, d,
+                                        1 if kind == "loss" else 0, device, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib().mdp_scenario_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def lik(self, e, c, K, dsrc=None, ts: int = 20, tdis: int = 10) -> np.ndarray:
+        """L[ie][ic][iK] (die-off) or L[ie][ic][iK][id] (loss), raw likelihoods."""
+        e = np.ascontiguousarray(np.atleast_1d(e), dtype=np.float64)
+        c = np.ascontiguousarray(np.atleast_1d(c), dtype=np.float64)
+        K = np.ascontiguousarray(np.atleast_1d(K), dtype=np.float64)
+        if self.kind == "loss":
+            dsrc = np.ascontiguousarray(np.atleast_1d(dsrc), dtype=np.float64)
+            nd = dsrc.size
+            shape = (e.size, c.size, K.size, nd)
+        else:
+            dsrc = np.zeros(1)
+            nd = 1
+            shape = (e.size, c.size, K.size)
+        out = np.empty(int(np.prod(shape)))
+        check(lib().mdp_scenario_lik(self._h, ts, tdis, _dptr(e), e.size, _dptr(c), c.size, _dptr(K), K.size, _dptr(dsrc),
+                                     nd, _dptr(out)))
+        return out.reshape(shape)

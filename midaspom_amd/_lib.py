@@ -14,6 +14,8 @@ PKG_DIR = Path(__file__).resolve().parent
 BUILD_DIR = PKG_DIR / "_build"
 LIB_PATH = BUILD_DIR / "libmidaspom.so"
 CLI_PATH = BUILD_DIR / "midaspom"
+DIEOFF_CLI_PATH = BUILD_DIR / "midaspom_dieoff"
+LOSS_CLI_PATH = BUILD_DIR / "midaspom_loss"
 
 MDP_OK = 0
 ERRORS = {
@@ -99,6 +101,15 @@ SIGNATURES = [
     ("mdp_engine_diag_report", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
     ("mdp_last_error", ctypes.c_char_p, []),
     ("mdp_abi_version", ctypes.c_int, []),
+    ("mdp_kgrid", ctypes.c_double, [ctypes.c_uint32, ctypes.c_double, ctypes.c_double, c_dbl_p]),
+    ("mdp_dgrid", ctypes.c_double, [ctypes.c_uint32, ctypes.c_double, ctypes.c_double, c_dbl_p]),
+    ("mdp_scenario_create", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32, ctypes.c_double, ctypes.c_float, ctypes.c_double,
+      ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("mdp_scenario_destroy", None, [ctypes.c_void_p]),
+    ("mdp_scenario_lik", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_dbl_p, ctypes.c_uint32, c_dbl_p, ctypes.c_uint32, c_dbl_p,
+      ctypes.c_uint32, c_dbl_p, ctypes.c_uint32, c_dbl_p]),
 ]
 
 _lib = None

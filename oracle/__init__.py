@@ -62,6 +62,12 @@ def lib():
         h.orc_ltot.argtypes = [_dp, ctypes.c_uint, ctypes.c_double]
         h.orc_ltot.restype = ctypes.c_double
         h.orc_write_posterior.argtypes = [ctypes.c_char_p, _dp, ctypes.c_uint, ctypes.c_double]
+        ip = ctypes.POINTER(ctypes.c_int32)
+        common = [ip, ctypes.c_uint32, ctypes.c_double, ctypes.c_float, ctypes.c_double, ctypes.c_int,
+                  ctypes.c_int, ctypes.c_double, ctypes.c_double, _dp, ctypes.c_uint32]
+        h.orc_dieoff_lik.argtypes = common + [_dp]
+        h.orc_loss_lik.argtypes = common + [_dp, ctypes.c_uint32, _dp]
+        h.orc_kgrid.argtypes = [ctypes.c_uint32, ctypes.c_double, ctypes.c_double, _dp]
         _lib = h
     return _lib
 
@@ -186,3 +192,43 @@ def run(path, out=None, m=400.0, p=0.5, d=100.0, s=101, lo=0.0, hi=1.0, threads=
     if out is not None:
         write_posterior(out, lik, lt)
     return lik, lt
+
+
+# ---------------------------------------------------------------------------
+# scenario likelihoods (oracle/spom_dieoff_oracle.c): dieoff.c / loss.c
+# ---------------------------------------------------------------------------
+def first_row(path):
+    """The first survey row as the reference reads it (dieoff.c:185-201)."""
+    data = Path(path).read_bytes()
+    n = 1 + sum(1 for ch in data.split(b"\n", 1)[0] if ch in (32, 9))
+    toks = data.split()
+    return np.array([int(t) for t in toks[:n]], dtype=np.int32)
+
+
+def kgrid(s, lo=0.1, hi=100.0):
+    K = np.empty(s)
+    lib().orc_kgrid(s, lo, hi, _p(K))
+    return K
+
+
+def dieoff_lik(row, K, e, c, ts=20, tdis=10, m=400.0, p=0.5, d=200.0):
+    row = np.ascontiguousarray(row, dtype=np.int32)
+    K = np.ascontiguousarray(K, dtype=np.float64)
+    out = np.empty(K.size)
+    rc = lib().orc_dieoff_lik(row.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row.size, m, p, d, ts, tdis,
+                              e, c, _p(K), K.size, _p(out))
+    if rc:
+        raise RuntimeError("orc_dieoff_lik failed")
+    return out
+
+
+def loss_lik(row, K, dsrc, e, c, ts=20, tdis=10, m=400.0, p=0.5, d=200.0):
+    row = np.ascontiguousarray(row, dtype=np.int32)
+    K = np.ascontiguousarray(K, dtype=np.float64)
+    dsrc = np.ascontiguousarray(dsrc, dtype=np.float64)
+    out = np.empty((K.size, dsrc.size))
+    rc = lib().orc_loss_lik(row.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row.size, m, p, d, ts, tdis,
+                            e, c, _p(K), K.size, _p(dsrc), dsrc.size, _p(out))
+    if rc:
+        raise RuntimeError("orc_loss_lik failed")
+    return out

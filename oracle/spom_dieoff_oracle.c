@@ -1,0 +1,205 @@
+/*
+ * oracle/spom_dieoff_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's two scenario likelihoods, in the
+ * reference's dense operation order (full 2^n state space, naive row-major
+ * dgemm, the same binary matrix power):
+ *   in-situ die-off   /root/reference/sources/main_MIDASPOM_dieoff.c
+ *   habitat loss      /root/reference/sources/main_MIDASPOM_loss.c
+ * Callers allowed: tests/ (checker), never the product.
+ *
+ * Pinned by the manual's worked examples (Manual_linux.pdf p.4 dieoff and
+ * p.5 loss tables, tests/golden/anchors.json) in tests/test_oracle_golden.py.
+ *
+ * Anchors (dieoff.c unless noted):
+ *   matpow                    :17-49   (orc_matpow)
+ *   pije  (E = min(1, e/K))   :51-64   (loss.c:52-65: E = min(1, e))
+ *   pijc  (pC = c*s1*K)       :66-83
+ *   pijcsource (loss)         loss.c:86-105  (s1 += M[n][k]*Ksource, pC = c*s1)
+ *   first survey row, states  :185-232
+ *   dispersal M               :238-248 (loss.c:269-279 + source row :365)
+ *   K grid (log10)            :284-286;  d grid (loss)  loss.c:319-322
+ *   P = Pe*Pc, P^tdis         :307-316
+ *   per K: PK, PK^ts, PK^ts*P^tdis, sum over columns of observed states
+ *                             :322-351  (loss.c:360-386)
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* c = a*b, row-major n x n, the reference's cblas_dgemm(RowMajor,NoTrans,NoTrans) */
+static void dgemm(const double *a, const double *b, double *c, int n)
+{
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < n; ++k) s += a[i * n + k] * b[k * n + j];
+            c[i * n + j] = s;
+        }
+}
+
+/* z = x^k, dieoff.c:17-49 (x is overwritten, as in the reference) */
+static void orc_matpow(double *x, int n, int k, double *z)
+{
+    if (k == 0) {
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) z[i * n + j] = i == j ? 1.0 : 0.0;
+        return;
+    }
+    double *tmp = malloc(sizeof(double) * n * n);
+    memcpy(z, x, sizeof(double) * n * n);
+    k--;
+    while (k > 0) {
+        if (k & 1) {
+            dgemm(x, z, tmp, n);
+            memcpy(z, tmp, sizeof(double) * n * n);
+        }
+        if (k == 1) break;
+        k >>= 1;
+        dgemm(x, x, tmp, n);
+        memcpy(x, tmp, sizeof(double) * n * n);
+    }
+    free(tmp);
+}
+
+static int bit(int s, int j, int n) { return (s >> (n - 1 - j)) & 1; }
+
+/* extinction phase, dieoff.c:51-64 (K = 1 gives loss.c's pije) */
+static double pije(int from, int to, double e, double K, int n)
+{
+    int s1 = 0, s2 = 0;
+    double E = e / K;
+    if (E > 1) E = 1;
+    for (int k = 0; k < n; ++k) {
+        const int po = bit(from, k, n), pt = bit(to, k, n);
+        if (pt * (1 - po) > 0) return 0;
+        s1 += (1 - pt) * po;
+        s2 += pt * po;
+    }
+    return pow(E, s1) * pow(1 - E, s2);
+}
+
+/* colonisation phase: dieoff.c:66-83 (src == NULL) or loss.c:86-105 */
+static double pijc(int tmp, int nw, double c, double K, const double *M, const double *src, double Ks, int n)
+{
+    double res = 1;
+    for (int k = 0; k < n; ++k) {
+        const int pt = bit(tmp, k, n), pn = bit(nw, k, n);
+        if (pt * (1 - pn) > 0) return 0;
+        double s1 = 0;
+        for (int l = 0; l < n; ++l)
+            if (l != k) s1 += M[l * n + k] * bit(tmp, l, n);
+        double pC;
+        if (src) {
+            s1 += src[k] * Ks;
+            pC = c * s1;
+        } else {
+            pC = c * s1 * K;
+        }
+        if (pC > 1) pC = 1;
+        res *= pt + (1 - pt) * (1 - pn) * (1 - pC) + (1 - pt) * pn * pC;
+    }
+    return res;
+}
+
+/* first-survey states and float priors, dieoff.c:198-232 */
+static int states_of(const int32_t *row, int n, float p, int **ps, float **pr)
+{
+    int s1 = 0;
+    for (int j = 0; j < n; ++j) s1 += row[j] == -1;
+    const int np = 1 << s1;
+    *ps = calloc(np, sizeof(int));
+    *pr = malloc(np * sizeof(float));
+    for (int k = 0; k < np; ++k) (*pr)[k] = 1;
+    s1 = 0;
+    for (int j = 0; j < n; ++j) {
+        if (row[j] == -1) s1++;
+        for (int k = 0; k < np; ++k) {
+            if (row[j] > -1) {
+                (*ps)[k] += row[j] * (1 << (n - j - 1));
+            } else {
+                const int st1 = np >> s1;
+                (*ps)[k] += (k / st1 % 2) * (1 << (n - j - 1));
+                (*pr)[k] *= (k / st1 % 2) * p + (1 - k / st1 % 2) * (1 - p);
+            }
+        }
+    }
+    return np;
+}
+
+static void dispersal(int n, double m, double d, double *M)
+{
+    const double a = 1.0 / m;
+    for (int i = 0; i < n; ++i)
+        for (int j = i; j < n; ++j) {
+            if (i == j) M[i * n + j] = 0.0;
+            else M[i * n + j] = M[j * n + i] = exp(-a * (j - i) * d);
+        }
+}
+
+/* log10 K grid, dieoff.c:284-286 */
+void orc_kgrid(uint32_t s, double lo, double hi, double *K)
+{
+    for (uint32_t i = 0; i < s; ++i)
+        K[i] = pow(10.0, ((double)i) / (s - 1) * (log10(hi) - log10(lo)) + log10(lo));
+}
+
+/* L = sum_i sum_j [PK^ts P^tdis]_{i, ps_j} pr_j for each K (and source
+ * distance), i.e. dieoff.c:304-351 / loss.c:341-386.  out[iK * nd + id]. */
+static int scenario(const int32_t *row, uint32_t n, double m, float p, double d, int ts, int tdis, double e,
+                    double c, const double *K, uint32_t nK, const double *dsrc, uint32_t nd, int loss,
+                    double *out)
+{
+    if (n == 0 || n > 12) return -1;
+    const int ns = 1 << n;
+    int *ps;
+    float *pr;
+    const int np = states_of(row, (int)n, p, &ps, &pr);
+    double *M = malloc(sizeof(double) * n * n), *src = malloc(sizeof(double) * n);
+    dispersal((int)n, m, d, M);
+    const size_t sz = (size_t)ns * ns * sizeof(double);
+    double *Pe = malloc(sz), *Pc = malloc(sz), *P = malloc(sz), *Ppow = malloc(sz), *PK = malloc(sz),
+           *PKpow = malloc(sz), *Ptot = malloc(sz);
+    for (int i = 0; i < ns; ++i)
+        for (int j = 0; j < ns; ++j) {
+            Pe[i * ns + j] = pije(i, j, e, 1.0, (int)n);
+            Pc[i * ns + j] = pijc(i, j, c, 1.0, M, NULL, 0.0, (int)n);
+        }
+    dgemm(Pe, Pc, P, ns);
+    orc_matpow(P, ns, tdis, Ppow);
+    const double a = 1.0 / m;
+    for (uint32_t iK = 0; iK < nK; ++iK)
+        for (uint32_t id = 0; id < (loss ? nd : 1u); ++id) {
+            if (loss)
+                for (uint32_t j = 0; j < n; ++j) src[j] = exp(-a * (j + 1) * dsrc[id]);
+            for (int i = 0; i < ns; ++i)
+                for (int j = 0; j < ns; ++j) {
+                    Pe[i * ns + j] = pije(i, j, e, loss ? 1.0 : K[iK], (int)n);
+                    Pc[i * ns + j] = loss ? pijc(i, j, c, 1.0, M, src, K[iK], (int)n)
+                                          : pijc(i, j, c, K[iK], M, NULL, 0.0, (int)n);
+                }
+            dgemm(Pe, Pc, PK, ns);
+            orc_matpow(PK, ns, ts, PKpow);
+            dgemm(PKpow, Ppow, Ptot, ns);
+            double L = 0;
+            for (int i = 0; i < ns; ++i)
+                for (int j = 0; j < np; ++j) L += Ptot[i * ns + ps[j]] * pr[j];
+            out[(size_t)iK * (loss ? nd : 1u) + id] = L;
+        }
+    free(Pe), free(Pc), free(P), free(Ppow), free(PK), free(PKpow), free(Ptot);
+    free(M), free(src), free(ps), free(pr);
+    return 0;
+}
+
+int orc_dieoff_lik(const int32_t *row, uint32_t n, double m, float p, double d, int ts, int tdis, double e,
+                   double c, const double *K, uint32_t nK, double *out)
+{
+    return scenario(row, n, m, p, d, ts, tdis, e, c, K, nK, NULL, 0, 0, out);
+}
+
+int orc_loss_lik(const int32_t *row, uint32_t n, double m, float p, double d, int ts, int tdis, double e,
+                 double c, const double *K, uint32_t nK, const double *dsrc, uint32_t nd, double *out)
+{
+    return scenario(row, n, m, p, d, ts, tdis, e, c, K, nK, dsrc, nd, 1, out);
+}
