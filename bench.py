@@ -86,12 +86,99 @@ def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, budget_s=12.0):
         "points_checked": int(ee.size), "neginf_positions_match": same_inf}
 
 
+def bench_future(args, world, rank, dev):
+    """Config 5: MIDASPOM_future on examples/input with the
+    config-1 posterior (s = 101, computed by the GPU engine before timing),
+    `-a 50 -m 400 -d 100`, 10^6 replicates split over the ranks (strong
+    scaling) + one sum-reduce of the per-year counts over RCCL.  A step = the
+    whole ensemble; units = replicate-years."""
+    inp = ROOT / "tests" / "golden" / "occupancies.txt"
+    tfut, nsim, seed = 50, args.replicates, 20161014
+    post_lik, ltot = mdp.run_file(inp, None, m=400.0, d=100.0, s=101, devices=[dev.index])
+    post = mdp.posterior(post_lik, ltot)
+    _, _, row = mdp.read_survey(inp)
+    fut = mdp.Future(row, post, m=400.0, d=100.0, device=dev.index)
+    from midaspom_amd import dist as mdist
+    r0, r1 = mdist.replicate_range(rank, world, nsim)
+    counts = torch.zeros(tfut, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        fut.simulate_device(counts.data_ptr(), r1 - r0, tfut, seed=seed, rep0=r0, stream=stream)
+        if world > 1:
+            dist.reduce(counts, dst=0, op=dist.ReduceOp.SUM)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    kms = fut.time_kernel(r1 - r0, tfut, seed=seed, reps=args.steps)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    # FP64 work the model needs per replicate-year (simpij, future.c:64-110):
+    # n^2 colonisation-sum adds + n source adds + n products c*s1, and one
+    # division per draw (n draws at least: every patch draws once).  The
+    # Philox integer work is not counted.
+    n = row.size
+    flop_per_ry = n * n + 2 * n + n
+    achieved = flop_per_ry * (r1 - r0) * tfut / (kms * 1e-3) / 1e12
+    result = {
+        "metric": "replicate-year simulations/sec (MIDASPOM_future ensemble)",
+        "value": nsim * tfut * args.steps / dt,
+        "unit": "replicate-years/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "examples/input (shipped), posterior from the GPU engine at s=101",
+        "config": {"workload": "config5: MIDASPOM_future, 10^6 replicates x 50 years, examples/input",
+                   "patches": int(n), "replicates": nsim, "years": tfut,
+                   "parallelism": f"replicate ranges x{world}" + (", RCCL reduce" if world > 1 else "")},
+        "kernel_ms": {"k_future": kms},
+        "roofline": {"kernel": "k_future", "bound": "mfma", "compute_unit": "FP64 VALU",
+                     "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "flop_per_replicate_year": flop_per_ry},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
+        t0 = time.perf_counter()
+        oracle.future_counts(row, post, tfut=tfut, nrep=2000, m=400.0, d=100.0, seed=seed, threads=1)
+        per = (time.perf_counter() - t0) / 2000
+        nref = int(min(nsim, max(threads * 100, 12.0 * threads / per)))
+        t0 = time.perf_counter()
+        ref = oracle.future_counts(row, post, tfut=tfut, nrep=nref, m=400.0, d=100.0, seed=seed, threads=threads)
+        wall = time.perf_counter() - t0
+        got = fut.simulate(nref, tfut, seed=seed)
+        result["cpu_baseline"] = {
+            "value": nref * tfut / wall, "unit": "replicate-years/s", "cores": threads, "kind": "port",
+            "sample": f"replicates [0, {nref}) of the same stream, oracle/spom_future_oracle.c, {threads} threads, "
+                      f"{wall:.1f} s"}
+        result["parity"] = {"replicates_checked": nref, "counts_identical": bool(np.array_equal(got, ref))}
+    fut.close()
+    return result
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [5])
+    ap.add_argument("--replicates", type=int, default=1_000_000, help="config 5 ensemble size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -105,6 +192,13 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.config == 5:
+        result = bench_future(args, world, rank, dev)
+        if rank == 0:
+            print(json.dumps(result))
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     cfg = CONFIGS[args.config]
     s = cfg["s"]

@@ -13,7 +13,8 @@
  *    code; the reason is in mdp_last_error() (thread-local).  Nothing aborts
  *    or exits across the ABI;
  *  - an engine is not re-entrant; one host thread drives all its devices;
- *  - results are deterministic (no atomics in any reduction).
+ *  - results are deterministic (no floating-point atomics in any reduction;
+ *    the future engine's integer counts use LDS atomics, exact in any order).
  */
 #ifndef MIDASPOM_H
 #define MIDASPOM_H
@@ -33,7 +34,7 @@ extern "C" {
 #define MDP_ENODEV (-5)       /* no usable GPU                             */
 #define MDP_EUNSUPPORTED (-6) /* problem outside the engine's limits       */
 
-#define MDP_ABI_VERSION 2
+#define MDP_ABI_VERSION 3
 
 /* ------------------------------------------------------------------ */
 /* Host model: parse + state enumeration (the reference's L2 layer)    */
@@ -196,6 +197,48 @@ void mdp_scenario_destroy(mdp_scenario *scenario);
 int mdp_scenario_lik(mdp_scenario *scenario, int ts, int tdis, const double *e, uint32_t ne,
                      const double *c, uint32_t nc, const double *K, uint32_t nK, const double *dsrc,
                      uint32_t nd, double *out);
+
+/* ------------------------------------------------------------------ */
+/* Forward simulation of extinction under management scenarios         */
+/* (main_MIDASPOM_future.c)                      */
+/* ------------------------------------------------------------------ */
+
+/* Input readers of the future program.  *row = the LAST survey row of an
+ * occupancy file (n from line 1, tokens streamed across lines;
+ * future.c:193-225); *post = the necstep x necstep posterior matrix, necstep
+ * = separators on its first line (future.c:237-262).  Free with mdp_free. */
+int mdp_future_read_survey(const char *path, uint32_t *n, uint32_t *tmax, int32_t **row);
+int mdp_future_read_posterior(const char *path, uint32_t *necstep, double **post);
+void mdp_free(void *p);
+
+typedef struct mdp_future mdp_future;
+
+/* Engine for the replicate loop of future.c:343-386 on HIP device `device`:
+ * last survey row (n <= 64 patches, values -1/0/1, <= 30 missing), the
+ * posterior it samples (e, c) from (row-major necstep^2; e = ie*0.01 and
+ * c = ic*0.01 as hard-coded at :370-371), m = mean dispersal (-m), d =
+ * segment length (-d), KD = relative population size (-D), KS = source
+ * size (-S), dS = source distance (-s). */
+int mdp_future_create(const int32_t *last_row, uint32_t n, const double *post, uint32_t necstep, double m,
+                      double d, double KD, double KS, double dS, int device, mdp_future **out);
+void mdp_future_destroy(mdp_future *future);
+
+/* counts[t] += number of replicates r in [rep0, rep0 + nrep) with every patch
+ * empty after year t+1, t < tfut (future.c:381-385; Lik[] there).  Draws are
+ * Philox4x32-10 keyed by `seed` and addressed by (replicate, year, patch):
+ * results do not depend on how replicates are split (over GPUs, ranks or
+ * calls).  Host memory. */
+int mdp_future_simulate(mdp_future *future, uint64_t seed, uint64_t rep0, uint64_t nrep, uint32_t tfut,
+                        uint64_t *counts);
+/* Same into caller-owned device memory d_counts[tfut] (overwritten, not
+ * accumulated) on `stream` (NULL = engine stream); asynchronous. */
+int mdp_future_simulate_device(mdp_future *future, uint64_t seed, uint64_t rep0, uint64_t nrep, uint32_t tfut,
+                               uint64_t *d_counts, void *stream);
+/* Mean duration (ms) of the simulation kernel over `reps` back-to-back
+ * launches of replicates [0, nrep) between two events. */
+int mdp_future_time_kernel(mdp_future *future, uint64_t seed, uint64_t nrep, uint32_t tfut, int reps, double *ms);
+/* The generator itself: out[4] = Philox4x32-10(key, ctr[4]) (host). */
+int mdp_future_philox(uint64_t key, const uint32_t *ctr, uint32_t *out);
 
 /* Thread-local description of the last error. */
 const char *mdp_last_error(void);

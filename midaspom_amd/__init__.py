@@ -27,6 +27,7 @@ from ._lib import MidaspomError, check, lib
 __all__ = [
     "Model", "Engine", "grid", "log_total", "write_posterior", "posterior",
     "run_file", "MidaspomError", "Scenario", "kgrid", "dgrid", "first_row",
+    "Future", "read_survey", "read_posterior",
 ]
 
 
@@ -326,3 +327,89 @@ class Scenario:
         check(lib().mdp_scenario_lik(self._h, ts, tdis, _dptr(e), e.size, _dptr(c), c.size, _dptr(K), K.size, _dptr(dsrc),
                                      nd, _dptr(out)))
         return out.reshape(shape)
+
+
+# ---------------------------------------------------------------------------
+# forward simulation of extinction (main_MIDASPOM_future.c)
+# ---------------------------------------------------------------------------
+def read_survey(path):
+    """(n, tmax, last survey row) as future.c:193-225 reads them."""
+    n, t = ctypes.c_uint32(), ctypes.c_uint32()
+    p = ctypes.POINTER(ctypes.c_int32)()
+    check(lib().mdp_future_read_survey(os.fsencode(str(path)), ctypes.byref(n), ctypes.byref(t), ctypes.byref(p)))
+    try:
+        row = np.ctypeslib.as_array(p, shape=(n.value,)).copy()
+    finally:
+        lib().mdp_free(p)
+    return n.value, t.value, row
+
+
+def read_posterior(path) -> np.ndarray:
+    """necstep x necstep posterior as future.c:237-262 reads it."""
+    s = ctypes.c_uint32()
+    p = ctypes.POINTER(ctypes.c_double)()
+    check(lib().mdp_future_read_posterior(os.fsencode(str(path)), ctypes.byref(s), ctypes.byref(p)))
+    try:
+        post = np.ctypeslib.as_array(p, shape=(s.value * s.value,)).copy() if s.value else np.zeros(0)
+    finally:
+        lib().mdp_free(p)
+    return post.reshape(s.value, s.value)
+
+
+class Future:
+    """GPU replicate loop of MIDASPOM_future (``mdp_future``): per-year counts
+    of replicates with every patch extinct."""
+
+    def __init__(self, row, post, m: float = 400.0, d: float = 200.0, KD: float = 1.0, KS: float = 0.0,
+                 dS: float = 200.0, device: int = 0):
+        row = np.ascontiguousarray(row, dtype=np.int32)
+        post = np.ascontiguousarray(post, dtype=np.float64)
+        self._post = post
+        h = ctypes.c_void_p()
+        check(lib().mdp_future_create(row.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row.size, _dptr(post),
+                                      post.shape[0] if post.size else 0, m, d, KD, KS, dS, device,
+                                      ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mdp_future_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def simulate(self, nrep: int, tfut: int = 50, seed: int = 0, rep0: int = 0) -> np.ndarray:
+        """counts[t] over replicates [rep0, rep0 + nrep) (host uint64 array)."""
+        counts = np.zeros(tfut, dtype=np.uint64)
+        check(lib().mdp_future_simulate(self._h, seed, rep0, nrep, tfut,
+                                        counts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+        return counts
+
+    def simulate_device(self, d_counts: int, nrep: int, tfut: int, seed: int = 0, rep0: int = 0,
+                        stream: int | None = None) -> None:
+        """Into device memory at ``d_counts`` (uint64[tfut]), asynchronously."""
+        check(lib().mdp_future_simulate_device(self._h, seed, rep0, nrep, tfut, ctypes.c_void_p(d_counts),
+                                               ctypes.c_void_p(stream) if stream else None))
+
+    def time_kernel(self, nrep: int, tfut: int, seed: int = 0, reps: int = 10) -> float:
+        ms = ctypes.c_double()
+        check(lib().mdp_future_time_kernel(self._h, seed, nrep, tfut, reps, ctypes.byref(ms)))
+        return ms.value
+
+
+def philox(key: int, ctr) -> list:
+    """The engine's generator, Philox4x32-10(key, ctr[4]) (host restatement)."""
+    c = (ctypes.c_uint32 * 4)(*[int(x) & 0xffffffff for x in ctr])
+    o = (ctypes.c_uint32 * 4)()
+    check(lib().mdp_future_philox(key & 0xffffffffffffffff, c, o))
+    return list(o)

@@ -16,6 +16,7 @@ LIB_PATH = BUILD_DIR / "libmidaspom.so"
 CLI_PATH = BUILD_DIR / "midaspom"
 DIEOFF_CLI_PATH = BUILD_DIR / "midaspom_dieoff"
 LOSS_CLI_PATH = BUILD_DIR / "midaspom_loss"
+FUTURE_CLI_PATH = BUILD_DIR / "midaspom_future"
 
 MDP_OK = 0
 ERRORS = {
@@ -110,6 +111,26 @@ SIGNATURES = [
     ("mdp_scenario_lik", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_dbl_p, ctypes.c_uint32, c_dbl_p, ctypes.c_uint32, c_dbl_p,
       ctypes.c_uint32, c_dbl_p, ctypes.c_uint32, c_dbl_p]),
+    ("mdp_future_read_survey", ctypes.c_int,
+     [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+      ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))]),
+    ("mdp_future_read_posterior", ctypes.c_int,
+     [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(c_dbl_p)]),
+    ("mdp_free", None, [ctypes.c_void_p]),
+    ("mdp_future_create", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32, c_dbl_p, ctypes.c_uint32, ctypes.c_double, ctypes.c_double,
+      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("mdp_future_destroy", None, [ctypes.c_void_p]),
+    ("mdp_future_simulate", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+      ctypes.POINTER(ctypes.c_uint64)]),
+    ("mdp_future_simulate_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+      ctypes.c_void_p]),
+    ("mdp_future_time_kernel", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, c_dbl_p]),
+    ("mdp_future_philox", ctypes.c_int,
+     [ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
 ]
 
 _lib = None

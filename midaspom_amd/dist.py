@@ -84,3 +84,54 @@ def gpu_slab_compute(model, device_index: int):
 
     compute.engine = eng
     return compute
+
+
+# ---------------------------------------------------------------------------
+# forward simulation: replicate ranges + one sum-reduce (future_MPI.c)
+# ---------------------------------------------------------------------------
+def replicate_range(rank: int, world: int, nsimul: int):
+    """[r0, r1) replicates of rank `rank`: floor(nsimul/N) each, the
+    remainder on rank 0 (main_MIDASPOM_future_MPI.c:376-383)."""
+    return row_slab(rank, world, nsimul)
+
+
+def reduce_counts(local, rank: int, world: int):
+    """Sum every rank's per-year counts (torch int64 tensor [tfut]) onto rank
+    0 in ONE collective (the root's MPI_Recv accumulate,
+    future_MPI.c:432-444); returns the numpy totals on rank 0, None elsewhere."""
+    import torch.distributed as dist
+
+    dist.reduce(local, dst=0, op=dist.ReduceOp.SUM)
+    return local.cpu().numpy().astype(np.uint64) if rank == 0 else None
+
+
+def distributed_future_counts(nsimul: int, rank: int, world: int,
+                              compute: Callable[[int, int], object], device=None):
+    """Each rank simulates its replicate range with `compute(rep0, nrep)` (a
+    torch int64 tensor or numpy array [tfut]) and the counts are summed on
+    rank 0.  Replicate r draws from the same addressed stream wherever it runs,
+    so the totals do not depend on the world size."""
+    import torch
+
+    r0, r1 = replicate_range(rank, world, nsimul)
+    local = compute(r0, r1 - r0)
+    if not torch.is_tensor(local):
+        local = torch.from_numpy(np.asarray(local).astype(np.int64))
+    if device is not None:
+        local = local.to(device)
+    return reduce_counts(local, rank, world)
+
+
+def gpu_future_compute(fut, tfut: int, seed: int, device_index: int):
+    """compute(rep0, nrep) on this rank's GPU through the C ABI; the counts
+    stay in HBM (a torch int64 tensor) until the reduce."""
+    import torch
+
+    def compute(rep0, nrep):
+        out = torch.zeros(tfut, dtype=torch.int64, device=f"cuda:{device_index}")
+        if nrep:
+            fut.simulate_device(out.data_ptr(), nrep, tfut, seed=seed, rep0=rep0,
+                                stream=torch.cuda.current_stream(device_index).cuda_stream)
+        return out
+
+    return compute

@@ -68,6 +68,12 @@ def lib():
         h.orc_dieoff_lik.argtypes = common + [_dp]
         h.orc_loss_lik.argtypes = common + [_dp, ctypes.c_uint32, _dp]
         h.orc_kgrid.argtypes = [ctypes.c_uint32, ctypes.c_double, ctypes.c_double, _dp]
+        h.orc_philox.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                 ctypes.POINTER(ctypes.c_uint32)]
+        h.orc_future_sim.argtypes = [ip, ctypes.c_uint, _dp, ctypes.c_uint, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint,
+                                     ctypes.c_uint, ctypes.POINTER(ctypes.c_uint64)]
         _lib = h
     return _lib
 
@@ -232,3 +238,54 @@ def loss_lik(row, K, dsrc, e, c, ts=20, tdis=10, m=400.0, p=0.5, d=200.0):
     if rc:
         raise RuntimeError("orc_loss_lik failed")
     return out
+
+
+# ---------------------------------------------------------------------------
+# forward simulation (oracle/spom_future_oracle.c): future.c
+# ---------------------------------------------------------------------------
+RNG_PHILOX, RNG_GLIBC = 0, 1
+
+
+def philox(key: int, ctr):
+    """Philox4x32-10(key, ctr[4]) -> 4 uint32 words."""
+    h = lib()
+    c = (ctypes.c_uint32 * 4)(*[int(x) & 0xffffffff for x in ctr])
+    o = (ctypes.c_uint32 * 4)()
+    h.orc_philox(ctypes.c_uint32(key & 0xffffffff), ctypes.c_uint32((key >> 32) & 0xffffffff), c, o)
+    return list(o)
+
+
+def last_row(path):
+    """(n, tmax, last survey row) as future.c:193-225 reads them."""
+    data = Path(path).read_bytes()
+    n = 1 + sum(1 for ch in data.split(b"\n", 1)[0] if ch in (32, 9))
+    tmax = data.count(b"\n")
+    row = [0] * n
+    for q, tok in enumerate(data.split()[: tmax * n]):
+        row[q % n] = int(tok)
+    return n, tmax, np.array(row, dtype=np.int32)
+
+
+def read_posterior(path):
+    """necstep x necstep posterior as future.c:237-262 reads it."""
+    data = Path(path).read_bytes()
+    s = sum(1 for ch in data.split(b"\n", 1)[0] if ch in (32, 9))
+    vals = np.array([float(t) for t in data.split()[: s * s]], dtype=np.float64)
+    return vals.reshape(s, s)
+
+
+def future_counts(row, post, tfut=50, nrep=10000, m=400.0, d=200.0, KD=1.0, KS=0.0, dS=200.0,
+                  mode=RNG_PHILOX, seed=0, rep0=0, threads=None):
+    """Per-year all-extinct counts over replicates [rep0, rep0 + nrep)."""
+    h = lib()
+    row = np.ascontiguousarray(row, dtype=np.int32)
+    post = np.ascontiguousarray(post, dtype=np.float64)
+    counts = np.zeros(tfut, dtype=np.uint64)
+    threads = threads or min(16, os.cpu_count() or 1)
+    rc = h.orc_future_sim(row.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row.size, _p(post),
+                          post.shape[0] if post.size else 0, m, d, KD, KS, dS, mode,
+                          ctypes.c_uint64(seed), ctypes.c_uint64(rep0), ctypes.c_uint64(nrep), tfut, threads,
+                          counts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    if rc:
+        raise RuntimeError("orc_future_sim failed")
+    return counts

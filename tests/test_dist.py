@@ -65,3 +65,46 @@ def test_gloo_gather_matches_single_process(golden, tmp_path, world):
     g, _ = oracle.grid(s)
     ref = om.loglik_grid(g, g, threads=1)
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("nsimul", [1, 7, 10000])
+def test_replicate_ranges_partition(world, nsimul):
+    spans = [mdist.replicate_range(r, world, nsimul) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == nsimul
+    assert all(a1 == b0 for (_, a1), (b0, _) in zip(spans, spans[1:]))
+
+
+def _future_worker(rank, world, port, inp, outdir):
+    import torch.distributed as dist
+    sys.path.insert(0, str(ROOT))
+    import oracle
+    from midaspom_amd import dist as md
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _, _, row = oracle.last_row(inp)
+    post = np.load(os.path.join(outdir, "post.npy"))
+    tot = md.distributed_future_counts(
+        5000, rank, world,
+        lambda r0, nr: oracle.future_counts(row, post, tfut=20, nrep=nr, rep0=r0, seed=9, m=400, d=100,
+                                            KS=0.5, threads=1))
+    if rank == 0:
+        np.save(os.path.join(outdir, "tot.npy"), tot)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_future_reduce_matches_single_process(golden, tmp_path, world):
+    """Replicate ranges per rank + one sum-reduce (future_MPI.c:376-383,
+    :432-444) give the single-process counts exactly."""
+    import oracle
+    inp = str(golden / "occupancies.txt")
+    oracle.run(inp, tmp_path / "post.txt", m=400, d=100, s=21)
+    post = oracle.read_posterior(tmp_path / "post.txt") * 0.7  # exercise the carry-over across ranks
+    np.save(tmp_path / "post.npy", post)
+    mp.spawn(_future_worker, args=(world, _free_port(), inp, str(tmp_path)), nprocs=world, join=True)
+    got = np.load(tmp_path / "tot.npy")
+    _, _, row = oracle.last_row(inp)
+    ref = oracle.future_counts(row, post, tfut=20, nrep=5000, seed=9, m=400, d=100, KS=0.5, threads=1)
+    assert np.array_equal(got, ref)
