@@ -172,12 +172,110 @@ def bench_future(args, world, rank, dev):
     return result
 
 
+def bench_dieoff(args, world, rank, dev):
+    """Config 4: MIDASPOM_dieoff likelihood over a 3-D
+    (e, c, K_D) = 256^3 grid -- e, c on [0, 1], K_D log-spaced on [0.1, 100]
+    -- for the first survey row of examples/input (n = 8, 2^8 states),
+    `-b 20 -a 10 -m 400 -d 100`.  The e rows are split into contiguous slabs
+    over the ranks (strong scaling: the grid is fixed) and gathered to rank 0
+    in one RCCL collective.  Units = grid points x (ts + tdis) year
+    transitions."""
+    from midaspom_amd import dist as mdist
+    inp = ROOT / "tests" / "golden" / "occupancies.txt"
+    s, ts, tdis = args.grid4, 20, 10
+    g, _ = mdp.grid(s, 0.0, 1.0)
+    K = mdp.kgrid(s, 0.1, 100.0)
+    r0, r1 = mdist.row_slab(rank, world, s)
+    cap = s // world + s % world
+    row = mdp.first_row(inp)
+    sc = mdp.Scenario(row, "dieoff", m=400.0, d=100.0, device=dev.index)
+    sc.set_grid(g[r0:r1], g, K, ts=ts, tdis=tdis)
+    out = torch.zeros((cap, s, s), dtype=torch.float64, device=dev)
+    gathered = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        sc.run(out.data_ptr(), stream)
+        if world > 1:
+            dist.gather(out, gathered, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    kms = sc.time_kernels(out.data_ptr(), stream, reps=max(1, min(args.steps, 5)))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    n = row.size
+    ns = 1 << n
+    # FP64 work per point per year in the vector-propagation form: the Pc
+    # application (3^n FMAs) + n Pe passes over 2^(n-1) pairs (3 flop each)
+    flop_year = 2 * 3 ** n + 3 * n * (ns // 2)
+    nloc = (r1 - r0) * s * s
+    achieved = flop_year * nloc * ts / (kms["k_scn_lik"] * 1e-3) / 1e12
+    result = {
+        "metric": "grid-point x timestep likelihood evals/sec (MIDASPOM_dieoff 3-D grid)",
+        "value": s ** 3 * (ts + tdis) * args.steps / dt,
+        "unit": "grid-point-timestep evals/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "examples/input first survey row (shipped)",
+        "config": {"workload": f"config4: MIDASPOM_dieoff (e,c,K_D) {s}^3 grid, ts=20, tdis=10, n=8",
+                   "grid": [s, s, s], "patches": int(n), "states": ns,
+                   "parallelism": f"e-row slabs x{world}" + (", RCCL gather" if world > 1 else "")},
+        "kernel_ms": kms,
+        "roofline": {"kernel": "k_scn_lik", "bound": "mfma", "compute_unit": "FP64 VALU",
+                     "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "flop_per_point_year": flop_year},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        rng = np.random.default_rng(0)
+        lik = out[: r1 - r0].cpu().numpy()
+        t0 = time.perf_counter()
+        pts, worst = 0, 0.0
+        while time.perf_counter() - t0 < 10.0:
+            ie, ic = int(rng.integers(0, s)), int(rng.integers(0, s))
+            iK = rng.choice(s, size=4, replace=False)
+            ref = oracle.dieoff_lik(row, K[iK], g[ie], g[ic], ts=ts, tdis=tdis, m=400.0, d=100.0)
+            got = lik[ie, ic, iK]
+            big = ref > 1e-14
+            if big.any():
+                worst = max(worst, float((np.abs(got[big] - ref[big]) / ref[big]).max()))
+            worst = max(worst, float(np.abs(got[~big] - ref[~big]).max(initial=0.0)) * 1e6)
+            pts += iK.size
+        wall = time.perf_counter() - t0
+        result["cpu_baseline"] = {
+            "value": pts * (ts + tdis) / wall, "unit": "grid-point-timestep evals/s", "cores": 1, "kind": "port",
+            "sample": f"{pts} random (e,c,K) points, oracle/spom_dieoff_oracle.c dense matpow formulation, "
+                      f"1 thread, {wall:.1f} s"}
+        result["parity"] = {"points_checked": pts, "max_rel_dlik": worst}
+    sc.close()
+    return result
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [5])
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [4, 5])
+    ap.add_argument("--grid4", type=int, default=256, help="config 4 grid points per axis")
     ap.add_argument("--replicates", type=int, default=1_000_000, help="config 5 ensemble size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -192,8 +290,8 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    if args.config == 5:
-        result = bench_future(args, world, rank, dev)
+    if args.config in (4, 5):
+        result = (bench_future if args.config == 5 else bench_dieoff)(args, world, rank, dev)
         if rank == 0:
             print(json.dumps(result))
         if world > 1:

@@ -240,6 +240,17 @@ int mdp_future_time_kernel(mdp_future *future, uint64_t seed, uint64_t nrep, uin
 /* The generator itself: out[4] = Philox4x32-10(key, ctr[4]) (host). */
 int mdp_future_philox(uint64_t key, const uint32_t *ctr, uint32_t *out);
 
+/* Device-resident form of mdp_scenario_lik (one process per GPU): upload the
+ * grid once (set_grid; ts, tdis and the axes as above), then compute into
+ * caller-owned device memory d_out[ne*nc*nK*nd] (same layout) on `stream`
+ * (NULL = the scenario's stream), asynchronously.  time_kernels: ms[0] =
+ * mean duration of the v = P^tdis w kernel, ms[1] = of the PK^ts kernel,
+ * each launched `reps` times back to back between two events. */
+int mdp_scenario_set_grid(mdp_scenario *scenario, int ts, int tdis, const double *e, uint32_t ne, const double *c,
+                          uint32_t nc, const double *K, uint32_t nK, const double *dsrc, uint32_t nd);
+int mdp_scenario_run(mdp_scenario *scenario, double *d_out, void *stream);
+int mdp_scenario_time_kernels(mdp_scenario *scenario, double *d_out, void *stream, int reps, double *ms);
+
 /* Thread-local description of the last error. */
 const char *mdp_last_error(void);
 

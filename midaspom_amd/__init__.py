@@ -328,6 +328,33 @@ class Scenario:
                                      nd, _dptr(out)))
         return out.reshape(shape)
 
+    def set_grid(self, e, c, K, dsrc=None, ts: int = 20, tdis: int = 10) -> tuple:
+        """Upload an (e, c, K[, d]) grid once for run(); returns the output shape."""
+        e = np.ascontiguousarray(np.atleast_1d(e), dtype=np.float64)
+        c = np.ascontiguousarray(np.atleast_1d(c), dtype=np.float64)
+        K = np.ascontiguousarray(np.atleast_1d(K), dtype=np.float64)
+        if self.kind == "loss":
+            dsrc = np.ascontiguousarray(np.atleast_1d(dsrc), dtype=np.float64)
+            shape = (e.size, c.size, K.size, dsrc.size)
+        else:
+            dsrc = np.zeros(1)
+            shape = (e.size, c.size, K.size)
+        check(lib().mdp_scenario_set_grid(self._h, ts, tdis, _dptr(e), e.size, _dptr(c), c.size, _dptr(K), K.size,
+                                          _dptr(dsrc), dsrc.size))
+        self.shape = shape
+        return shape
+
+    def run(self, d_out: int, stream: int | None = None) -> None:
+        """Compute the set grid into device memory at ``d_out`` (float64, the
+        set_grid shape), asynchronously on hipStream ``stream``."""
+        check(lib().mdp_scenario_run(self._h, ctypes.c_void_p(d_out), ctypes.c_void_p(stream) if stream else None))
+
+    def time_kernels(self, d_out: int, stream: int | None = None, reps: int = 10) -> dict:
+        ms = (ctypes.c_double * 2)()
+        check(lib().mdp_scenario_time_kernels(self._h, ctypes.c_void_p(d_out),
+                                              ctypes.c_void_p(stream) if stream else None, reps, ms))
+        return {"k_scn_v": ms[0], "k_scn_lik": ms[1]}
+
 
 # ---------------------------------------------------------------------------
 # forward simulation of extinction (main_MIDASPOM_future.c, SURVEY.md §8(f) 2)

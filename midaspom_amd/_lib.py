@@ -111,6 +111,12 @@ SIGNATURES = [
     ("mdp_scenario_lik", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_dbl_p, ctypes.c_uint32, c_dbl_p, ctypes.c_uint32, c_dbl_p,
       ctypes.c_uint32, c_dbl_p, ctypes.c_uint32, c_dbl_p]),
+    ("mdp_scenario_set_grid", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_dbl_p, ctypes.c_uint32, c_dbl_p, ctypes.c_uint32, c_dbl_p,
+      ctypes.c_uint32, c_dbl_p, ctypes.c_uint32]),
+    ("mdp_scenario_run", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("mdp_scenario_time_kernels", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, c_dbl_p]),
     ("mdp_future_read_survey", ctypes.c_int,
      [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
       ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))]),

@@ -52,7 +52,7 @@ namespace {
 
 constexpr int kFutBlock = 256;
 constexpr int kFutMaxWG = 4096;         // grid-stride cap (>= 16 workgroups per CU)
-constexpr uint32_t kFutMaxT = 16384;    // LDS year counters (64 KB)
+constexpr uint32_t kFutMaxT = 12288;    // LDS year counters (48 KB; + 16 KB table for n <= 8)
 constexpr uint32_t kLookBack = 1u << 16;
 constexpr double kRandMax = 2147483647.0;  // glibc RAND_MAX
 
@@ -73,8 +73,10 @@ __device__ __forceinline__ u32x4 philox(uint32_t k0, uint32_t k1, u32x4 c)
 {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        // one v_mad_u64_u32 per product (instead of mul_lo + mul_hi)
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -92,6 +94,30 @@ struct FutArgs {
     double K;               // K_D (:67, :93)
 };
 
+// The reference compares u = (double)r / (double)RAND_MAX with a threshold
+// (u > E, u < pC).  r * fl(1/RAND_MAX) is within 3.4e-16 of fl(r/RAND_MAX)
+// (both within ~1.2 ulp of r/RAND_MAX <= 1), so outside a 1e-15 band around
+// the threshold the product decides the comparison; inside it the exact
+// correctly rounded quotient does.  Bit-identical outcomes, ~never divides.
+constexpr double kInvRandMax = 1.0 / 2147483647.0;
+constexpr double kBand = 1e-15;
+
+__device__ __forceinline__ bool u_gt(uint32_t r, double x)  // fl(r/R) > x
+{
+    const double q = (double)r * kInvRandMax;
+    if (q > x + kBand) return true;
+    if (q < x - kBand) return false;
+    return (double)r / kRandMax > x;
+}
+
+__device__ __forceinline__ bool u_lt(uint32_t r, double x)  // fl(r/R) < x
+{
+    const double q = (double)r * kInvRandMax;
+    if (q < x - kBand) return true;
+    if (q > x + kBand) return false;
+    return (double)r / kRandMax < x;
+}
+
 // first i < len with x < pcum[i] (pcum non-decreasing), or len
 __device__ __forceinline__ uint32_t upper_bound(const double *__restrict__ pcum, uint32_t len, double x)
 {
@@ -104,14 +130,38 @@ __device__ __forceinline__ uint32_t upper_bound(const double *__restrict__ pcum,
     return lo;
 }
 
+// colonisation sums of every survivor set of n <= 8 patches:
+// T[surv][k] = (sum_{l in surv, l != k, ascending} M[l][k]*K_D) + M[n][k]*K_S,
+// the reference's s1 of simpij :89-95 (its added zeros change nothing)
+constexpr int kTabN = 8;
+__global__ __launch_bounds__(256) void k_future_table(const double *__restrict__ MK, const double *__restrict__ src,
+                                                      uint32_t n, double *__restrict__ T)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= (1u << kTabN) * kTabN) return;
+    const uint32_t surv = i / kTabN, k = i % kTabN;
+    double s1 = 0.0;
+    for (uint32_t l = 0; l < n; ++l)
+        if (l != k && ((surv >> l) & 1u)) s1 += MK[l * kTabN + k];
+    T[i] = s1 + src[k];
+}
+
 template <int NM>
 __global__ __launch_bounds__(kFutBlock) void k_future(FutArgs a, const double *__restrict__ MK,
                                                       const double *__restrict__ src,
                                                       const double *__restrict__ pcum,
                                                       const uint64_t *__restrict__ missbit,
+                                                      const double *__restrict__ T,
                                                       uint32_t *__restrict__ partial, uint32_t *__restrict__ err)
 {
-    extern __shared__ uint32_t cnt[];  // [tfut] all-extinct replicates of this workgroup per year
+    extern __shared__ __attribute__((aligned(16))) double dyn[];
+    // NM == 8: the colonisation table (16 KB) first, then the year counters
+    double *Ts = dyn;
+    uint32_t *cnt = (uint32_t *)(dyn + (NM == kTabN ? (1 << kTabN) * kTabN : 0));
+    if constexpr (NM == kTabN) {
+        for (uint32_t i = threadIdx.x; i < (1u << kTabN) * kTabN / 2; i += kFutBlock)
+            reinterpret_cast<double2 *>(Ts)[i] = reinterpret_cast<const double2 *>(T)[i];
+    }
     for (uint32_t t = threadIdx.x; t < a.tfut; t += kFutBlock) cnt[t] = 0;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -159,28 +209,39 @@ __global__ __launch_bounds__(kFutBlock) void k_future(FutArgs a, const double *_
                     colw[k0] = w.y >> 1;
                     colw[k1] = w.w >> 1;
                     // extinction: an occupied patch survives if u > E (:75-82)
-                    if (((occ >> k0) & 1u) && (double)(w.x >> 1) / kRandMax > E) surv |= 1ull << k0;
-                    if (((occ >> k1) & 1u) && (double)(w.z >> 1) / kRandMax > E) surv |= 1ull << k1;
+                    if (((occ >> k0) & 1u) && u_gt(w.x >> 1, E)) surv |= 1ull << k0;
+                    if (((occ >> k1) & 1u) && u_gt(w.z >> 1, E)) surv |= 1ull << k1;
                 } else {
                     colw[2 * m] = colw[2 * m + 1] = 0;
                 }
             }
             // colonisation sums, ascending l for every k (:89-95)
             double s1[NM];
+            if constexpr (NM == kTabN) {
+                const double2 *row = reinterpret_cast<const double2 *>(Ts + (uint32_t)surv * kTabN);
 #pragma unroll
-            for (int k = 0; k < NM; ++k) s1[k] = 0.0;
-            for (uint32_t l = 0; l < a.n; ++l) {
-                const bool on = (surv >> l) & 1u;
+                for (int k = 0; k < NM; k += 2) {
+                    const double2 v = row[k / 2];
+                    s1[k] = v.x, s1[k + 1] = v.y;
+                }
+            } else {
 #pragma unroll
-                for (int k = 0; k < NM; ++k) s1[k] += on ? MK[l * NM + k] : 0.0;
+                for (int k = 0; k < NM; ++k) s1[k] = 0.0;
+                for (uint32_t l = 0; l < a.n; ++l) {
+                    const bool on = (surv >> l) & 1u;
+#pragma unroll
+                    for (int k = 0; k < NM; ++k) s1[k] += on ? MK[l * NM + k] : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < NM; ++k) s1[k] += src[k];
             }
             uint64_t nw = surv;
 #pragma unroll
             for (int k = 0; k < NM; ++k) {
                 if ((uint32_t)k < a.n && !((surv >> k) & 1u)) {
-                    double pc = c * (s1[k] + src[k]);  // :95-97
+                    double pc = c * s1[k];  // :95-97
                     if (pc > 1) pc = 1;
-                    if ((double)colw[k] / kRandMax < pc) nw |= 1ull << k;  // :98-101
+                    if (u_lt(colw[k], pc)) nw |= 1ull << k;  // :98-101
                 }
             }
             occ = nw;
@@ -225,7 +286,7 @@ struct mdp_future {
     uint32_t n = 0, nm = 0, nmiss = 0, necstep = 0, lvalid = 0;
     uint64_t occ0 = 0;
     double K = 1.0, pscale = 0.0;
-    double *dMK = nullptr, *dsrc = nullptr, *dpcum = nullptr;
+    double *dMK = nullptr, *dsrc = nullptr, *dpcum = nullptr, *dT = nullptr;
     uint64_t *dmiss = nullptr;
     uint32_t *dpartial = nullptr, *derr = nullptr;
     size_t partial_cap = 0;
@@ -281,12 +342,12 @@ int fut_launch(mdp_future *f, uint64_t seed, uint64_t rep0, uint64_t nrep, uint3
     a.pscale = f->pscale;
     a.K = f->K;
     const int nwg = fut_grid(nrep);
-    const size_t lds = (size_t)tfut * sizeof(uint32_t);
+    const size_t lds = (size_t)tfut * sizeof(uint32_t) + (f->nm == kTabN ? sizeof(double) * (kTabN << kTabN) : 0);
     switch (f->nm) {
 #define FUT_CASE(NMV)                                                                                   \
     case NMV:                                                                                            \
         hipLaunchKernelGGL(k_future<NMV>, dim3(nwg), dim3(kFutBlock), lds, st, a, f->dMK, f->dsrc,    \
-                           f->dpcum, f->dmiss, f->dpartial, f->derr);                                   \
+                           f->dpcum, f->dmiss, f->dT, f->dpartial, f->derr);                            \
         break;
         FUT_CASE(8)
         FUT_CASE(16)
@@ -393,6 +454,18 @@ int mdp_future_create(const int32_t *last_row, uint32_t n, const double *post, u
         mdp_future_destroy(f);
         return rc;
     }
+    if (f->nm == kTabN) {
+        if (hipMalloc((void **)&f->dT, sizeof(double) * (kTabN << kTabN)) != hipSuccess) {
+            mdp_future_destroy(f);
+            return mdp_set_error(MDP_EHIP, "device allocation failed on device %d", device);
+        }
+        hipLaunchKernelGGL(k_future_table, dim3((kTabN << kTabN) / 256), dim3(256), 0, nullptr, f->dMK, f->dsrc, n,
+                           f->dT);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            mdp_future_destroy(f);
+            return mdp_set_error(MDP_EHIP, "colonisation table kernel failed on device %d", device);
+        }
+    }
     if (hipMalloc((void **)&f->derr, sizeof(uint32_t)) != hipSuccess ||
         hipMemset(f->derr, 0, sizeof(uint32_t)) != hipSuccess ||
         hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -412,6 +485,7 @@ void mdp_future_destroy(mdp_future *f)
     (void)hipFree(f->dMK);
     (void)hipFree(f->dsrc);
     (void)hipFree(f->dpcum);
+    (void)hipFree(f->dT);
     (void)hipFree(f->dmiss);
     (void)hipFree(f->dpartial);
     (void)hipFree(f->derr);

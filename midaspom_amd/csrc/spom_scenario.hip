@@ -125,14 +125,12 @@ __global__ __launch_bounds__(kScnBlock) void k_scn_v(ScnArgs a, const double *__
             const uint32_t free = ~j & (a.ns - 1), f = __popc(free);
             const double *tt = T + toff[j];
             double acc = 0.0;
+            // supersets b = j | sub in ascending order: sub runs over the
+            // submasks of `free` by sub <- (sub - free) & free
+            uint32_t sub = 0;
             for (uint32_t r = 0; r < (1u << f); ++r) {
-                uint32_t b = j, xs = free;
-                for (uint32_t q = 0; q < f; ++q) {
-                    const uint32_t low = xs & (0u - xs);
-                    if ((r >> q) & 1u) b |= low;
-                    xs ^= low;
-                }
-                acc += tt[r] * y[b * kE + le];
+                acc += tt[r] * y[(j | sub) * kE + le];
+                sub = (sub - free) & free;
             }
             yb[j * kE + le] = acc;
         }
@@ -185,14 +183,12 @@ __global__ __launch_bounds__(kScnBlock) void k_scn_lik(ScnArgs a, const double *
             const uint32_t free = ~j & (a.ns - 1), f = __popc(free);
             const double *tt = T + toff[j];
             double acc = 0.0;
+            // supersets b = j | sub in ascending order: sub runs over the
+            // submasks of `free` by sub <- (sub - free) & free
+            uint32_t sub = 0;
             for (uint32_t r = 0; r < (1u << f); ++r) {
-                uint32_t b = j, xs = free;
-                for (uint32_t q = 0; q < f; ++q) {
-                    const uint32_t low = xs & (0u - xs);
-                    if ((r >> q) & 1u) b |= low;
-                    xs ^= low;
-                }
-                acc += tt[r] * y[b * kE + le];
+                acc += tt[r] * y[(j | sub) * kE + le];
+                sub = (sub - free) & free;
             }
             yb[j * kE + le] = acc;
         }
@@ -240,7 +236,47 @@ struct mdp_scenario {
     double *dS = nullptr, *dw = nullptr;
     uint32_t *dtoff = nullptr, *djord = nullptr;
     hipStream_t stream = nullptr;
+    // grid set by mdp_scenario_set_grid (device resident)
+    int ts = 0, tdis = 0;
+    uint32_t ne = 0, nc = 0, nK = 0, nd = 0;
+    double *de = nullptr, *dc = nullptr, *dK = nullptr, *dsr = nullptr, *dV = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
+
+namespace {
+
+void scn_free_grid(mdp_scenario *sc)
+{
+    for (double **p : {&sc->de, &sc->dc, &sc->dK, &sc->dsr, &sc->dV}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    sc->ne = sc->nc = sc->nK = sc->nd = 0;
+}
+
+size_t scn_lds(const mdp_scenario *sc) { return (sc->nterm + 2 * (size_t)sc->ns * kE) * sizeof(double); }
+
+// k_scn_v (which = 1), k_scn_lik (which = 2) or both (3) on stream st
+int scn_launch(mdp_scenario *sc, double *dout, hipStream_t st, int which)
+{
+    const uint32_t nchunk = (sc->ne + kE - 1) / kE;
+    ScnArgs a{sc->n, sc->ns, sc->nterm, sc->ts, sc->tdis, sc->kind, sc->ne, sc->nc, sc->nK, sc->nd};
+    const size_t lds = scn_lds(sc);
+    const size_t npt = (size_t)sc->nc * sc->nK * sc->nd;
+    if (which & 1) {
+        hipLaunchKernelGGL(k_scn_v, dim3(nchunk * sc->nc), dim3(kScnBlock), lds, st, a, sc->dS, sc->dtoff,
+                           sc->djord, sc->dw, sc->de, sc->dc, sc->dV);
+        SCN_TRY(hipGetLastError());
+    }
+    if (which & 2) {
+        hipLaunchKernelGGL(k_scn_lik, dim3((uint32_t)(nchunk * npt)), dim3(kScnBlock), lds, st, a, sc->dS,
+                           sc->dtoff, sc->djord, sc->dV, sc->de, sc->dc, sc->dK, sc->dsr, dout);
+        SCN_TRY(hipGetLastError());
+    }
+    return MDP_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -354,65 +390,108 @@ void mdp_scenario_destroy(mdp_scenario *sc)
 {
     if (!sc) return;
     (void)hipSetDevice(sc->device);
+    if (sc->stream) (void)hipStreamSynchronize(sc->stream);
+    scn_free_grid(sc);
     for (void *p : {(void *)sc->dS, (void *)sc->dw, (void *)sc->dtoff, (void *)sc->djord})
         if (p) (void)hipFree(p);
+    if (sc->ev0) (void)hipEventDestroy(sc->ev0);
+    if (sc->ev1) (void)hipEventDestroy(sc->ev1);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
     delete sc;
 }
 
-int mdp_scenario_lik(mdp_scenario *sc, int ts, int tdis, const double *e, uint32_t ne, const double *c,
-                     uint32_t nc, const double *K, uint32_t nK, const double *dsrc, uint32_t nd, double *out)
+int mdp_scenario_set_grid(mdp_scenario *sc, int ts, int tdis, const double *e, uint32_t ne, const double *c,
+                          uint32_t nc, const double *K, uint32_t nK, const double *dsrc, uint32_t nd)
 {
-    if (!sc || !out || (ne && !e) || (nc && !c) || (nK && !K)) return mdp_set_error(MDP_EINVAL, "null argument");
+    if (!sc || (ne && !e) || (nc && !c) || (nK && !K)) return mdp_set_error(MDP_EINVAL, "null argument");
     if (ts < 0 || tdis < 0) return mdp_set_error(MDP_EINVAL, "negative number of years");
     if (sc->kind == 1) {
         if (nd && !dsrc) return mdp_set_error(MDP_EINVAL, "null source distances");
     } else {
         nd = 1;
     }
-    if (!ne || !nc || !nK || !nd) return MDP_OK;
     SCN_TRY(hipSetDevice(sc->device));
+    SCN_TRY(hipStreamSynchronize(sc->stream));
+    scn_free_grid(sc);
+    sc->ts = ts, sc->tdis = tdis;
+    if (!ne || !nc || !nK || !nd) return MDP_OK;
     const uint32_t n = sc->n, ns = sc->ns;
     const uint32_t nchunk = (ne + kE - 1) / kE;
+    if ((size_t)nchunk * nc * nK * nd > 0x7fffffffull)
+        return mdp_set_error(MDP_EUNSUPPORTED, "grid of %zu points too large", (size_t)ne * nc * nK * nd);
     // source terms M[n][k] = exp(-a (k+1) dsrc), loss.c:365
     std::vector<double> src((size_t)nd * n, 0.0);
     if (sc->kind == 1)
         for (uint32_t id = 0; id < nd; ++id)
             for (uint32_t k = 0; k < n; ++k) src[(size_t)id * n + k] = exp(-(1.0 / sc->m) * (k + 1) * dsrc[id]);
-    double *de = nullptr, *dc = nullptr, *dK = nullptr, *dsr = nullptr, *dV = nullptr, *dout = nullptr;
-    const size_t npts = (size_t)ne * nc * nK * nd;
-    auto fail = [&](int code) {
-        for (void *p : {(void *)de, (void *)dc, (void *)dK, (void *)dsr, (void *)dV, (void *)dout})
-            if (p) (void)hipFree(p);
-        return code;
-    };
-    if (hipMalloc((void **)&de, ne * sizeof(double)) != hipSuccess ||
-        hipMalloc((void **)&dc, nc * sizeof(double)) != hipSuccess ||
-        hipMalloc((void **)&dK, nK * sizeof(double)) != hipSuccess ||
-        hipMalloc((void **)&dsr, std::max<size_t>(1, src.size()) * sizeof(double)) != hipSuccess ||
-        hipMalloc((void **)&dV, (size_t)nc * nchunk * ns * kE * sizeof(double)) != hipSuccess ||
-        hipMalloc((void **)&dout, npts * sizeof(double)) != hipSuccess)
-        return fail(mdp_set_error(MDP_ENOMEM, "device allocation failed"));
-    if (hipMemcpy(de, e, ne * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(dc, c, nc * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(dK, K, nK * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
-        (!src.empty() && hipMemcpy(dsr, src.data(), src.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
-        return fail(mdp_set_error(MDP_EHIP, "upload failed"));
-    ScnArgs a{n, ns, sc->nterm, ts, tdis, sc->kind, ne, nc, nK, nd};
-    const size_t lds = (sc->nterm + 2 * (size_t)ns * kE) * sizeof(double);
-    const size_t npt = (size_t)nc * nK * nd;
-    if ((size_t)nchunk * npt > 0x7fffffffull)
-        return fail(mdp_set_error(MDP_EUNSUPPORTED, "grid of %zu points too large", npts));
-    hipLaunchKernelGGL(k_scn_v, dim3(nchunk * nc), dim3(kScnBlock), lds, sc->stream, a, sc->dS, sc->dtoff, sc->djord,
-                       sc->dw, de, dc, dV);
-    if (hipGetLastError() != hipSuccess) return fail(mdp_set_error(MDP_EHIP, "k_scn_v launch failed"));
-    hipLaunchKernelGGL(k_scn_lik, dim3((uint32_t)(nchunk * npt)), dim3(kScnBlock), lds, sc->stream, a, sc->dS,
-                       sc->dtoff, sc->djord, dV, de, dc, dK, dsr, dout);
-    if (hipGetLastError() != hipSuccess) return fail(mdp_set_error(MDP_EHIP, "k_scn_lik launch failed"));
-    if (hipMemcpyAsync(out, dout, npts * sizeof(double), hipMemcpyDeviceToHost, sc->stream) != hipSuccess ||
-        hipStreamSynchronize(sc->stream) != hipSuccess)
-        return fail(mdp_set_error(MDP_EHIP, "scenario run failed"));
-    return fail(MDP_OK);
+    if (hipMalloc((void **)&sc->de, ne * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&sc->dc, nc * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&sc->dK, nK * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&sc->dsr, std::max<size_t>(1, src.size()) * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&sc->dV, (size_t)nc * nchunk * ns * kE * sizeof(double)) != hipSuccess) {
+        scn_free_grid(sc);
+        return mdp_set_error(MDP_ENOMEM, "device allocation failed");
+    }
+    if (hipMemcpy(sc->de, e, ne * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(sc->dc, c, nc * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(sc->dK, K, nK * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        (!src.empty() &&
+         hipMemcpy(sc->dsr, src.data(), src.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)) {
+        scn_free_grid(sc);
+        return mdp_set_error(MDP_EHIP, "upload failed");
+    }
+    sc->ne = ne, sc->nc = nc, sc->nK = nK, sc->nd = nd;
+    return MDP_OK;
+}
+
+int mdp_scenario_run(mdp_scenario *sc, double *d_out, void *stream)
+{
+    if (!sc) return mdp_set_error(MDP_EINVAL, "null scenario");
+    if (!sc->ne) return MDP_OK;
+    if (!d_out) return mdp_set_error(MDP_EINVAL, "null device output");
+    SCN_TRY(hipSetDevice(sc->device));
+    return scn_launch(sc, d_out, stream ? (hipStream_t)stream : sc->stream, 3);
+}
+
+int mdp_scenario_time_kernels(mdp_scenario *sc, double *d_out, void *stream, int reps, double *ms)
+{
+    if (!sc || !ms || reps <= 0) return mdp_set_error(MDP_EINVAL, "bad timing request");
+    if (!sc->ne) return mdp_set_error(MDP_EINVAL, "no grid set");
+    SCN_TRY(hipSetDevice(sc->device));
+    hipStream_t st = stream ? (hipStream_t)stream : sc->stream;
+    if (!sc->ev0) SCN_TRY(hipEventCreate(&sc->ev0));
+    if (!sc->ev1) SCN_TRY(hipEventCreate(&sc->ev1));
+    int rc = scn_launch(sc, d_out, st, 3);
+    if (rc) return rc;
+    for (int which = 1; which <= 2; ++which) {
+        SCN_TRY(hipEventRecord(sc->ev0, st));
+        for (int i = 0; i < reps; ++i)
+            if ((rc = scn_launch(sc, d_out, st, which))) return rc;
+        SCN_TRY(hipEventRecord(sc->ev1, st));
+        SCN_TRY(hipEventSynchronize(sc->ev1));
+        float t = 0;
+        SCN_TRY(hipEventElapsedTime(&t, sc->ev0, sc->ev1));
+        ms[which - 1] = (double)t / reps;
+    }
+    return MDP_OK;
+}
+
+int mdp_scenario_lik(mdp_scenario *sc, int ts, int tdis, const double *e, uint32_t ne, const double *c,
+                     uint32_t nc, const double *K, uint32_t nK, const double *dsrc, uint32_t nd, double *out)
+{
+    if (!sc || !out) return mdp_set_error(MDP_EINVAL, "null argument");
+    int rc = mdp_scenario_set_grid(sc, ts, tdis, e, ne, c, nc, K, nK, dsrc, nd);
+    if (rc || !sc->ne) return rc;
+    const size_t npts = (size_t)sc->ne * sc->nc * sc->nK * sc->nd;
+    double *dout = nullptr;
+    if (hipMalloc((void **)&dout, npts * sizeof(double)) != hipSuccess)
+        return mdp_set_error(MDP_ENOMEM, "device allocation failed");
+    rc = scn_launch(sc, dout, sc->stream, 3);
+    if (!rc && (hipMemcpyAsync(out, dout, npts * sizeof(double), hipMemcpyDeviceToHost, sc->stream) != hipSuccess ||
+                hipStreamSynchronize(sc->stream) != hipSuccess))
+        rc = mdp_set_error(MDP_EHIP, "scenario run failed");
+    (void)hipFree(dout);
+    return rc;
 }
 
 }  // extern "C"

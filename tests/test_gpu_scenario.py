@@ -126,3 +126,22 @@ def test_cli_requires_event_flags(golden, tmp_path):
     r = subprocess.run([str(_lib.DIEOFF_CLI_PATH), "-i", str(golden / "manual_p3_obs.txt")],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "required" in r.stderr
+
+
+@pytest.mark.parametrize("kind", ["dieoff", "loss"])
+def test_device_resident_run_matches_host(golden, kind):
+    import torch
+    row = mdp.first_row(golden / "occupancies.txt")
+    e, c = np.linspace(0.05, 0.95, 19), np.array([0.1, 0.6, 2.0])
+    K, d = mdp.kgrid(6), mdp.dgrid(3)
+    with mdp.Scenario(row, kind, m=400, d=100) as sc:
+        host = sc.lik(e, c, K, d, ts=5, tdis=3)
+        shape = sc.set_grid(e, c, K, d, ts=5, tdis=3)
+        out = torch.empty(shape, dtype=torch.float64, device="cuda:0")
+        sc.run(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), host)
+        ms = sc.time_kernels(out.data_ptr(), torch.cuda.current_stream().cuda_stream, reps=2)
+        assert ms["k_scn_v"] > 0 and ms["k_scn_lik"] > 0
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), host)
