@@ -3,10 +3,15 @@
 
 A "step" = one pass of the hot path over one (e, c) grid slab per rank: the
 per-c coefficient kernels plus the forward-recursion kernel over every grid
-point, and -- with N > 1 ranks -- the single RCCL gather of the log-likelihood
-slabs to rank 0.  Units = grid points x year transitions = s^2 (tmax - 1) per
+point.  Grid points are independent, so steps need no exchange; with N > 1
+ranks the job's single RCCL gather of the log-likelihood slabs to rank 0
+(main_MIDASPOM_MPI.c:482-506) runs once, after the last step, inside the
+timed region.  Units = grid points x year transitions = s^2 (tmax - 1) per
 rank; value = units over all ranks / max-over-ranks wall time (weak scaling:
 each rank owns an s x s slab of an (N s) x s grid).
+Other modes: --config 3 (256 x 200, 1024^2), --config 4 (dieoff 256^3),
+--config 5 (future, 10^6 replicates); --backend gloo rehearses N ranks on
+fewer GPUs (collectives through host memory).
 
 Workload: 64 patches x 50 years (synthetic,
 Appendix C generator, md5-checked), 512 x 512 grid, -m 400 -d 100, FP64.
@@ -86,6 +91,12 @@ def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, budget_s=12.0):
         "points_checked": int(ee.size), "neginf_positions_match": same_inf}
 
 
+def _coll_tensor(t, args):
+    """The tensor a collective runs on: itself under RCCL, a host copy under
+    a rehearsal backend (gloo moves host tensors only)."""
+    return t if args.backend == "nccl" else t.cpu()
+
+
 def bench_future(args, world, rank, dev):
     """Config 5: MIDASPOM_future on examples/input with the
     config-1 posterior (s = 101, computed by the GPU engine before timing),
@@ -106,7 +117,7 @@ def bench_future(args, world, rank, dev):
     def step():
         fut.simulate_device(counts.data_ptr(), r1 - r0, tfut, seed=seed, rep0=r0, stream=stream)
         if world > 1:
-            dist.reduce(counts, dst=0, op=dist.ReduceOp.SUM)
+            dist.reduce(_coll_tensor(counts, args), dst=0, op=dist.ReduceOp.SUM)
 
     for _ in range(args.warmup):
         step()
@@ -124,7 +135,7 @@ def bench_future(args, world, rank, dev):
     dt = time.perf_counter() - t0
     kms = fut.time_kernel(r1 - r0, tfut, seed=seed, reps=args.steps)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = _coll_tensor(torch.tensor([dt], dtype=torch.float64, device=dev), args)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     # FP64 work the model needs per replicate-year (simpij, future.c:64-110):
@@ -196,11 +207,15 @@ def bench_dieoff(args, world, rank, dev):
 
     def step():
         sc.run(out.data_ptr(), stream)
+
+    def gather():  # the job's one gather, after the last pass (as configs 2/3)
         if world > 1:
-            dist.gather(out, gathered, dst=0)
+            src = _coll_tensor(out, args)
+            dist.gather(src, [_coll_tensor(g, args) for g in gathered] if gathered else None, dst=0)
 
     for _ in range(args.warmup):
         step()
+    gather()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -208,6 +223,7 @@ def bench_dieoff(args, world, rank, dev):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    gather()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -216,7 +232,7 @@ def bench_dieoff(args, world, rank, dev):
     kms = sc.time_kernels(out.data_ptr(), stream, reps=max(1, min(args.steps, 5)))
     torch.cuda.synchronize(dev)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = _coll_tensor(torch.tensor([dt], dtype=torch.float64, device=dev), args)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     n = row.size
@@ -278,6 +294,7 @@ def main():
     ap.add_argument("--grid4", type=int, default=256, help="config 4 grid points per axis")
     ap.add_argument("--replicates", type=int, default=1_000_000, help="config 5 ensemble size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -285,8 +302,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev_index = local % max(1, torch.cuda.device_count())  # == local on a full node
+        torch.cuda.set_device(dev_index)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:  # rehearsal of the multi-rank logic (e.g. 2 ranks on a 1-GPU box)
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -317,13 +338,21 @@ def main():
     gathered = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    # A step = one pass of the hot path over this rank's slab (no exchange:
+    # grid points are independent).  The job's single gather of the slabs to
+    # rank 0 (main_MIDASPOM_MPI.c:482-506; RCCL over xGMI) runs once, at the
+    # end of the timed region, on the last pass's output.
     def step():
         eng.run(out.data_ptr(), s, stream)
+
+    def gather():
         if world > 1:
-            dist.gather(out, gathered, dst=0)
+            src = _coll_tensor(out, args)
+            dist.gather(src, [_coll_tensor(g, args) for g in gathered] if gathered else None, dst=0)
 
     for _ in range(args.warmup):
         step()
+    gather()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -331,6 +360,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    gather()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -344,7 +374,7 @@ def main():
     kms = eng.time_kernels(out.data_ptr(), s, stream, reps=args.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = _coll_tensor(torch.tensor([dt], dtype=torch.float64, device=dev), args)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
