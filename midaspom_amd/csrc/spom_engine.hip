@@ -295,7 +295,10 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     }
     __syncthreads();
     MDP_STAMP(stamps, 1);
-    // 2. Pc per (c, item)
+    // 2. Pc per (c, item): Z times the product F of the var-column factors
+    // (pairwise tree over NV slots, 1.0 past nvar and for the bits of j -- the
+    // same tree as the fused kernel's over nvar).  Every operand is loaded
+    // before any arithmetic, so an item costs two LDS round trips.
     double cv[kQrowsMaxC];  // this workgroup's c values, loaded once
 #pragma unroll
     for (uint32_t i = 0; i < kQrowsMaxC; ++i) cv[i] = i < ncb ? cvals[c0 + i] : 0.0;
@@ -306,29 +309,42 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         for (uint32_t i = 1; i < kQrowsMaxC; ++i) c = cl == i ? cv[i] : c;
         const uint2 t = It[it];
         const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;
-        double p = Zl[cl * nrows + r];
-        // branch-free: lanes hold different items; bits of j and past nvar
-        // contribute 1.0
+        const double z = Zl[cl * nrows + r];
+        double sb[NV];
+#pragma unroll
+        for (int b = 0; b < NV; ++b) sb[b] = Sv[((uint32_t)b < nvar ? (uint32_t)b : 0u) * nrows + r];
+        double f[NV];
 #pragma unroll
         for (int b = 0; b < NV; ++b) {
             const bool live = (uint32_t)b < nvar;
             const uint32_t bit = live ? nvar - 1 - (uint32_t)b : 0u;
-            double pc = c * Sv[(live ? (uint32_t)b : 0u) * nrows + r];
+            double pc = c * sb[b];
             pc = pc > 1.0 ? 1.0 : pc;
-            const double f = ((B >> bit) & 1u) ? pc : 1.0 - pc;
-            p *= (!live || ((j >> bit) & 1u)) ? 1.0 : f;
+            const double fb = ((B >> bit) & 1u) ? pc : 1.0 - pc;
+            f[b] = (!live || ((j >> bit) & 1u)) ? 1.0 : fb;
         }
-        Pl[cl * nitems + it] = p;
+#pragma unroll
+        for (int sh = 1; sh < NV; sh *= 2)
+#pragma unroll
+            for (int b = 0; b + sh < NV; b += 2 * sh) f[b] *= f[b + sh];
+        Pl[cl * nitems + it] = z * f[0];
     }
     __syncthreads();
     MDP_STAMP(stamps, 2);
-    // 3. Q rows
+    // 3. Q rows: the entry's items in CSR order, eight loads in flight
     for (uint32_t w = threadIdx.x; w < ncb * ldQ; w += kQrowsBlock) {
         const uint32_t cl = w / ldQ, q = w - cl * ldQ;
         double a = 0.0;
         if (q < ncoef) {
             const double *pl = Pl + (size_t)cl * nitems;
-            for (uint32_t i = Qs[q], i1 = Qs[q + 1]; i < i1; ++i) a += pl[Qi[i]];
+            const uint32_t i0 = Qs[q], i1 = Qs[q + 1];
+            for (uint32_t i = i0; i < i1; i += 8) {
+                double pv[8];
+#pragma unroll
+                for (uint32_t u = 0; u < 8; ++u) pv[u] = pl[Qi[i + u < i1 ? i + u : i]];
+#pragma unroll
+                for (uint32_t u = 0; u < 8; ++u) a = i + u < i1 ? a + pv[u] : a;
+            }
         }
         Q[(size_t)(c0 + cl) * ldQ + q] = a;
     }
@@ -1604,8 +1620,15 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
         !p->short_state || (p->nvar && !p->var_cols))
         return mdp_set_error(MDP_EINVAL, "incomplete problem description");
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
-        return mdp_set_error(MDP_ENODEV, "no HIP device available");
+    // MDP_JIT_CHECK=1 without a device: plan and compile both forward
+    // variants (hipRTC runs offline), then report MDP_ENODEV -- the CPU
+    // test that the generated sources compile for gfx950
+    const char *jcheck = getenv("MDP_JIT_CHECK");
+    const bool jit_check = jcheck && atoi(jcheck) != 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        ndev = 0;
+        if (!jit_check) return mdp_set_error(MDP_ENODEV, "no HIP device available");
+    }
     mdp_engine *eng = new (std::nothrow) mdp_engine();
     if (!eng) return mdp_set_error(MDP_ENOMEM, "out of host memory");
     int rc = build_plan(eng, p);
@@ -1652,6 +1675,10 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             plan.nitems = eng->nitems;
             plan.ncoef = eng->ncoef_d;
             plan.nqi = (uint32_t)eng->qitem.size();
+            plan.kzmax = ((eng->n - eng->nvar) + 7u) & ~7u;
+            plan.qmaxlen = 0;
+            for (size_t q = 0; q + 1 < eng->qstart.size(); ++q)
+                plan.qmaxlen = std::max(plan.qmaxlen, eng->qstart[q + 1] - eng->qstart[q]);
             auto even = [](size_t v) { return (uint32_t)((v + 1) & ~(size_t)1); };
             plan.off_it = even((size_t)eng->nj * eng->nvar);
             plan.off_qs = even(plan.off_it + eng->nitems);
@@ -1660,6 +1687,11 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             const size_t kmax_max = ((size_t)(eng->n - eng->nvar) + 7) & ~(size_t)7;
             plan.ct_max = (uint32_t)std::min<size_t>(((plan.off_zs + kmax_max * eng->nj) + 127) & ~(size_t)127,
                                                      kFusedLdsMax / sizeof(double));
+            if (jit_check && ndev == 0) {
+                const int r0 = jit_build(eng, false), r1 = r0 ? r0 : jit_build(eng, true);
+                delete eng;
+                return r1 ? r1 : mdp_set_error(MDP_ENODEV, "no HIP device available (forward kernels compiled)");
+            }
             if (jit_build(eng, eng->fused_mode == 1) == MDP_OK) eng->jit = true;
             else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the generic kernel:\n%s\n",
                          eng->jit_log.c_str());

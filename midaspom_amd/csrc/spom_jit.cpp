@@ -123,7 +123,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         o << "#define NJ " << pl.nj << "\n#define NVAR " << pl.nvar << "\n#define NITEMS " << pl.nitems
           << "\n#define NCOEF " << pl.ncoef << "\n#define NQI " << (pl.nqi ? pl.nqi : 1) << "\n#define OFF_IT "
           << pl.off_it << "\n#define OFF_QS " << pl.off_qs << "\n#define OFF_QI " << pl.off_qi << "\n#define OFF_ZS "
-          << pl.off_zs << "\n#define NSTG "
+          << pl.off_zs << "\n#define KZ " << std::max<uint32_t>(8u, pl.kzmax) << "\n#define QML "
+          << std::max<uint32_t>(1u, pl.qmaxlen) << "\n#define QUN " << std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)
+          << "\n#define NSTG "
           << std::max<uint32_t>(1u, (pl.ct_max / 2 + 256u * pl.fused_cols - 1) / (256u * pl.fused_cols)) << "\n";
     const int FC = pl.fused ? (pl.fused_cols > 0 ? pl.fused_cols : 1) : 1;
     o << "#define FC " << FC << "\n#define NT (KBLOCK * FC)\n";
@@ -143,7 +145,14 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    const u32 half = threadIdx.x / KBLOCK, tid = threadIdx.x % KBLOCK;\n"
          "    const u32 ic0 = FC == 1 ? lb % nc : lb * FC, by = FC == 1 ? lb / nc : 0u;\n"
          "    const u32 ic = ic0 + half;\n"
-         "    const double *Qh = Ql + half * LDQ;\n";
+         "    const double *Qh = Ql + half * LDQ;\n"
+         // this lane's e values: issued first, their latency hides under the prologue
+         "    u32 ie[EPL];\n    double ev[EPL];\n"
+         "#pragma unroll\n"
+         "    for (int i = 0; i < EPL; ++i) {\n"
+         "        ie[i] = by * (KBLOCK * EPL) + i * KBLOCK + tid;\n"
+         "        ev[i] = ie[i] < ne ? evals[ie[i]] : 0.0;\n"
+         "    }\n";
     // stage n doubles from src (16-byte aligned, n even) into the LDS array dst
     auto stage = [&](const char *dst, const char *src, const char *n) {
         o << "    {\n"
@@ -203,21 +212,69 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    }\n") <<
              "    __syncthreads();\n"
           << stamp(4) <<
+             // operands of the Pc and Q phases that do not depend on Z, read
+             // and combined before the Z phase: per item its Z slot and the
+             // product F of its var-column factors (a fixed pairwise tree),
+             // per Q entry its item count and first QUN item indices
+             "    constexpr int KPC = (FC * NITEMS + NT - 1) / NT;\n"
+             "    constexpr int KQ = (FC * LDQ + NT - 1) / NT;\n"
+             "    double Fp[KPC];\n"
+             "    u32 zi[KPC];\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < KPC; ++k) {\n"
+             "        const u32 w0 = threadIdx.x + k * NT, w = w0 < FC * NITEMS ? w0 : 0u;\n"
+             "        const u32 col = w % FC, it = w / FC;\n"
+             "        const double c = cc[col];\n"
+             "        const uint2 t = Itl[it];\n"
+             "        const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
+             "        double f[NVAR];\n"
+             "#pragma unroll\n"
+             "        for (int b = 0; b < NVAR; ++b) {\n"
+             "            const u32 bit = NVAR - 1 - b;\n"
+             "            double pcv = c * Svl[r * NVAR + b];\n"
+             "            pcv = pcv > 1.0 ? 1.0 : pcv;\n"
+             "            const double fb = ((B >> bit) & 1u) ? pcv : 1.0 - pcv;\n"
+             "            f[b] = ((j >> bit) & 1u) ? 1.0 : fb;\n"
+             "        }\n"
+             "#pragma unroll\n"
+             "        for (int s = 1; s < NVAR; s *= 2)\n"
+             "#pragma unroll\n"
+             "            for (int b = 0; b + s < NVAR; b += 2 * s) f[b] *= f[b + s];\n"
+             "        Fp[k] = f[0];\n"
+             "        zi[k] = col * NJ + r;\n"
+             "    }\n"
+             "    u32 qb[KQ], qn[KQ], qx[KQ][QUN];\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < KQ; ++k) {\n"
+             "        const u32 w = threadIdx.x + k * NT, q = w % LDQ;\n"
+             "        const bool live = w < FC * LDQ && q < NCOEF;\n"
+             "        const u32 q0 = live ? Qsl[q] : 0u, q1 = live ? Qsl[q + 1] : 0u;\n"
+             "        qb[k] = q0;\n"
+             "        qn[k] = q1 - q0;\n"
+             "#pragma unroll\n"
+             "        for (int u = 0; u < QUN; ++u) qx[k][u] = Qil[q0 + u < NQI ? q0 + u : NQI - 1];\n"
+             "    }\n"
+             // Z per (column, row): the row's KZ (compile-time bound) values
+             // all in flight; rows past kmax contribute fma(-c, 0, 1) = 1
              "#pragma unroll\n"
              "    for (int k = 0; k < (FC * NJ + NT - 1) / NT; ++k) {\n"
              "        const u32 w = threadIdx.x + k * NT;\n"
              "        if (w < FC * NJ) {\n"
              "            const u32 col = w % FC, r = w / FC;\n"
              "            const double c = cc[col];\n"
-             "            double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
-             "            for (u32 kk = 0; kk < kmax; kk += 8) {\n"
-             "                double sk[8];\n"
+             "            double sk[KZ];\n"
              "#pragma unroll\n"
-             "                for (int u = 0; u < 8; ++u) sk[u] = zl[(kk + u) * NJ + r];\n"
-             "                za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);\n"
-             "                zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);\n"
-             "                zc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);\n"
-             "                zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);\n"
+             "            for (u32 kk = 0; kk < KZ; ++kk) sk[kk] = zl[(kk < kmax ? kk : kk % 8u) * NJ + r];\n"
+             "            double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
+             "#pragma unroll\n"
+             "            for (u32 kk = 0; kk < KZ; kk += 8) {\n"
+             "                const bool in = kk < kmax;\n"
+             "#pragma unroll\n"
+             "                for (int u = 0; u < 8; ++u) sk[kk + u] = in ? sk[kk + u] : 0.0;\n"
+             "                za *= fma(-c, sk[kk + 0], 1.0) * fma(-c, sk[kk + 4], 1.0);\n"
+             "                zb *= fma(-c, sk[kk + 1], 1.0) * fma(-c, sk[kk + 5], 1.0);\n"
+             "                zc *= fma(-c, sk[kk + 2], 1.0) * fma(-c, sk[kk + 6], 1.0);\n"
+             "                zd *= fma(-c, sk[kk + 3], 1.0) * fma(-c, sk[kk + 7], 1.0);\n"
              "            }\n"
              "            double z = (za * zb) * (zc * zd);\n"
              "            if (kmax && !(fma(-c, zl[r], 1.0) > 0.0)) z = 0.0;\n"
@@ -227,45 +284,36 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    __syncthreads();\n"
           << stamp(5) <<
              "#pragma unroll\n"
-             "    for (int k = 0; k < (FC * NITEMS + NT - 1) / NT; ++k) {\n"
+             "    for (int k = 0; k < KPC; ++k) {\n"
              "        const u32 w = threadIdx.x + k * NT;\n"
-             "        if (w < FC * NITEMS) {\n"
-             "            const u32 col = w % FC, it = w / FC;\n"
-             "            const double c = cc[col];\n"
-             "            const uint2 t = Itl[it];\n"
-             "            const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
-             "            double p = Zl[col * NJ + r];\n"
-             "#pragma unroll\n"
-             "            for (int b = 0; b < NVAR; ++b) {\n"
-             "                const u32 bit = NVAR - 1 - b;\n"
-             "                double pcv = c * Svl[r * NVAR + b];\n"
-             "                pcv = pcv > 1.0 ? 1.0 : pcv;\n"
-             "                const double f = ((B >> bit) & 1u) ? pcv : 1.0 - pcv;\n"
-             "                p *= ((j >> bit) & 1u) ? 1.0 : f;\n"
-             "            }\n"
-             "            Pl[col * NITEMS + it] = p;\n"
-             "        }\n"
+             "        if (w < FC * NITEMS) Pl[(w % FC) * NITEMS + w / FC] = Zl[zi[k]] * Fp[k];\n"
              "    }\n"
              "    __syncthreads();\n"
           << stamp(1) <<
+             // Q entries: the items in CSR (ascending j) order
              "#pragma unroll\n"
-             "    for (int k = 0; k < (FC * LDQ + NT - 1) / NT; ++k) {\n"
+             "    for (int k = 0; k < KQ; ++k) {\n"
              "        const u32 w = threadIdx.x + k * NT;\n"
              "        if (w < FC * LDQ) {\n"
-             "            const u32 col = w / LDQ, q = w - col * LDQ;\n"
+             "            const double *pl = Pl + (w / LDQ) * NITEMS;\n"
              "            double a = 0.0;\n"
-             "            if (q < NCOEF)\n"
-             "                for (u32 i = Qsl[q]; i < Qsl[q + 1]; ++i) a += Pl[col * NITEMS + Qil[i]];\n"
+             "#pragma unroll\n"
+             "            for (int u = 0; u < QUN; ++u) {\n"
+             "                const double pv = pl[qx[k][u]];\n"
+             "                a = (u32)u < qn[k] ? a + pv : a;\n"
+             "            }\n"
+             "#if QML > QUN\n"
+             "            for (u32 i = qb[k] + QUN; i < qb[k] + qn[k]; ++i) a += pl[Qil[i]];\n"
+             "#endif\n"
              "            Ql[w] = a;\n"
              "        }\n"
              "    }\n";
     }
     o <<
-         "    u32 ie[EPL];\n    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n"
+         "    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n"
          "#pragma unroll\n"
          "    for (int i = 0; i < EPL; ++i) {\n"
-         "        ie[i] = by * (KBLOCK * EPL) + i * KBLOCK + tid;\n"
-         "        const double e = ie[i] < ne ? evals[ie[i]] : 0.0;\n"
+         "        const double e = ev[i];\n"
          "        const double x = e > 1.0 ? 1.0 : e;\n"
          "        const double y = 1.0 - x;\n"
          "        double xp[DMAX + 1], yp[DMAX + 1];\n        xp[0] = 1.0;\n        yp[0] = 1.0;\n"

@@ -18,7 +18,9 @@ struct MdpJitPlan {
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
     // items, qstart, qitem, then zs[kmax][nj]
     uint32_t off_it = 0, off_qs = 0, off_qi = 0, off_zs = 0;
-    bool glds = false;  // stage the column tables with global_load_lds (else registers)
+    bool glds = true;   // stage the column tables with global_load_lds (else registers)
+    uint32_t kzmax = 0;    // bound on the zs rows of any grid: n - nvar rounded up to 8
+    uint32_t qmaxlen = 0;  // most items of one Q entry
     uint32_t ct_max = 0;  // largest column-table image (doubles), for the register staging
     int epl = 0;                  // grid points per lane (0: 2 unless the weight table is large)
     int window = 8;               // transitions per scheduling region
