@@ -35,7 +35,8 @@
 
 namespace {
 
-constexpr int kScnBlock = 256;        // 4 waves
+constexpr int kScnBlock = 1024;       // 16 waves: four per SIMD
+constexpr bool kPingPong = kScnBlock <= 768;  // register double-buffering (needs > 128 VGPRs)
 constexpr int kE = 32;                 // e values per workgroup (lanes mod 32)
 constexpr int kWaves = kScnBlock / 64;
 constexpr uint32_t kMaxN = 8;          // 2 x 2^8 x 32 state values + factor tables in LDS
@@ -87,6 +88,16 @@ __host__ __device__ constexpr int sup_rank(int NL, int jl, int bl)
     for (int b = NL - 1; b >= 0; --b)
         if (!((jl >> b) & 1)) r = 2 * r + ((bl >> b) & 1);
     return r;
+}
+
+// v(lane) + v(lane ^ 32) in every lane, by two v_permlane32_swap (VALU; no
+// LDS traffic); both halves add the same two values, so they agree bitwise
+__device__ __forceinline__ double half_sum(double v)
+{
+    const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+    const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return __hiloint2double(h2[0], l2[0]) + __hiloint2double(h2[1], l2[1]);
 }
 
 __device__ __forceinline__ uint32_t deposit(uint32_t r, uint32_t mask)  // r's bits into mask, ascending
@@ -196,6 +207,7 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
             dst[i] = v;
         }
     }
+    if (tid < (uint32_t)NLO) Bt[a.btot + tid] = 0.0;  // zero block (upper half, no free hi bit)
     // initial states
     for (uint32_t i = tid; i < (uint32_t)(NS * kE); i += kScnBlock) {
         const uint32_t x = i / kE, le = i % kE, st = ((x % NHI) << NL) | (x / NHI);
@@ -212,7 +224,6 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
             const uint32_t fr = ~jh & (NHI - 1), f = __popc(fr);
             const uint32_t top = f ? 1u << (31 - __clz(fr)) : 0u, frp = fr & ~top;
             const uint32_t units = f ? 1u << (f - 1) : 1u;
-            const bool active = g == 0 || f > 0;
             double A[NA];
             {
                 const double2 *ap = (const double2 *)(At + jh * NAP);
@@ -224,7 +235,9 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
                 }
                 if (NA & 1) A[NA - 1] = At[jh * NAP + NA - 1];
             }
-            const double *bt = Bt + boff[jh] + (size_t)(g && f ? units : 0u) * NLO;
+            // the upper half takes the supersets with the top free bit; with
+            // no free bit it reads the zero block past the table (acc = 0)
+            const double *bt = g ? (f ? Bt + boff[jh] + (size_t)units * NLO : Bt + a.btot) : Bt + boff[jh];
             double acc[NLO];
 #pragma unroll
             for (int l = 0; l < NLO; ++l) acc[l] = 0.0;
@@ -252,27 +265,40 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
                     acc[jl] = fma(bv[jl], in, acc[jl]);
                 }
             };
-            double ya[NLO], ba[NLO], yb2[NLO], bb[NLO];
             uint32_t sub = 0;
+            if (!kPingPong) {  // latency hidden by the other waves of the SIMD
+                for (uint32_t it = 0; it < units; ++it) {
+                    double ya[NLO], ba[NLO];
+                    load(it, sub, ya, ba);
+                    accumulate(ya, ba);
+                    sub = (sub - frp) & frp;
+                }
+            } else {
+            double ya[NLO], ba[NLO], yb2[NLO], bb[NLO];
             load(0, 0, ya, ba);
             if (units == 1) {
                 accumulate(ya, ba);
-            } else {  // units even
+            } else {  // units even; the last pair's look-ahead reloads it (in range)
                 for (uint32_t it = 0; it < units; it += 2) {
                     const uint32_t s1 = (sub - frp) & frp;
                     load(it + 1, s1, yb2, bb);
                     accumulate(ya, ba);
-                    const uint32_t s2 = (s1 - frp) & frp;
-                    if (it + 2 < units) load(it + 2, s2, ya, ba);
+                    const bool more = it + 2 < units;
+                    const uint32_t s2 = more ? (s1 - frp) & frp : s1;
+                    load(more ? it + 2 : it + 1, s2, ya, ba);
                     accumulate(yb2, bb);
                     sub = s2;
+                    // keep each buffer's loads ahead of the other buffer's FMAs
+                    // (the default schedule interleaves them and waits early)
+                    __builtin_amdgcn_sched_group_barrier(0x100, 3 * NLO / 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, NA + NLO + 8, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 3 * NLO / 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, NA + NLO + 8, 0);
                 }
             }
-#pragma unroll
-            for (int l = 0; l < NLO; ++l) {
-                const double v = active ? acc[l] : 0.0;
-                acc[l] = v + __shfl_xor(v, 32);
             }
+#pragma unroll
+            for (int l = 0; l < NLO; ++l) acc[l] = half_sum(acc[l]);
             // extinction on the lo patches, ascending patch
 #pragma unroll
             for (int k = NH; k < N; ++k) {
@@ -397,7 +423,7 @@ size_t scn_lds(const mdp_scenario *sc)
 {
     const uint32_t nl = scn_nl(sc->n), nh = sc->n - nl;
     const size_t na = (size_t)((pow3((int)nl) + 1) & ~1) << nh;
-    return (2 * ((size_t)sc->ns * kE + (2u << nl)) + na + sc->btot) * sizeof(double);
+    return (2 * ((size_t)sc->ns * kE + (2u << nl)) + na + sc->btot + (1u << nl)) * sizeof(double);
 }
 
 // v = P^tdis w (which = 1), L = 1^T PK^ts v (which = 2) or both (3) on stream st
