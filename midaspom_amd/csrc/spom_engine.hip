@@ -1198,8 +1198,8 @@ int jit_build(mdp_engine *eng, bool fused)
     const std::string src = mdp_jit_forward_source(plan);
     eng->jit_epl = plan.epl;
     eng->jit_flops_pt = plan.flops_pt;
-    if (const char *dump = getenv("MDP_JIT_DUMP")) {
-        if (FILE *f = fopen(dump, "w")) {
+    if (const char *dump = getenv("MDP_JIT_DUMP")) {  // <path>.hip (reading) / <path>.fused.hip
+        if (FILE *f = fopen((std::string(dump) + (fused ? ".fused.hip" : ".hip")).c_str(), "w")) {
             fputs(src.c_str(), f);
             fclose(f);
         }
