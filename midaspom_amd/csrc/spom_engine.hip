@@ -1040,6 +1040,10 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
         if (it == group.end()) {
             it = group.emplace(key, (uint32_t)groups.size()).first;
             groups.push_back({X, B});
+            // even start: the forward kernels read a group's coefficients
+            // pairwise as 16-byte aligned ds_read_b128 (an unaligned pair
+            // becomes a ds_read2_b64, twice the LDS cycles per byte)
+            off = (off + 1u) & ~1u;
             goff.push_back(off);
             off += (uint32_t)__builtin_popcount(X) + 1u;
         }
@@ -1088,6 +1092,7 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
     eng->qitem.clear();
     for (auto &g : groups) {
         const uint32_t nX = (uint32_t)__builtin_popcount(g.first);
+        if ((eng->qstart.size() - 1) & 1u) eng->qstart.push_back((uint32_t)eng->qitem.size());  // pad slot
         for (uint32_t m = 0; m <= nX; ++m) {
             for_subsets(g.first, [&](uint32_t j) {
                 if ((uint32_t)__builtin_popcount(j) == m)

@@ -218,11 +218,18 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              // per Q entry its item count and first QUN item indices
              "    constexpr int KPC = (FC * NITEMS + NT - 1) / NT;\n"
              "    constexpr int KQ = (FC * LDQ + NT - 1) / NT;\n"
+             // item w of pass k: odd passes run from the last thread down, so
+             // the partial last pass lands on the waves without Z rows; a wave
+             // with no item in a pass skips it (exec-empty branch)
              "    double Fp[KPC];\n"
              "    u32 zi[KPC];\n"
+             "#define ITEM_W(k) ((k) * NT + (((k) & 1) ? NT - 1 - threadIdx.x : threadIdx.x))\n"
              "#pragma unroll\n"
              "    for (int k = 0; k < KPC; ++k) {\n"
-             "        const u32 w0 = threadIdx.x + k * NT, w = w0 < FC * NITEMS ? w0 : 0u;\n"
+             "        const u32 w = ITEM_W(k);\n"
+             "        Fp[k] = 0.0;\n"
+             "        zi[k] = 0u;\n"
+             "        if (w >= FC * NITEMS) continue;\n"
              "        const u32 col = w % FC, it = w / FC;\n"
              "        const double c = cc[col];\n"
              "        const uint2 t = Itl[it];\n"
@@ -285,7 +292,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
           << stamp(5) <<
              "#pragma unroll\n"
              "    for (int k = 0; k < KPC; ++k) {\n"
-             "        const u32 w = threadIdx.x + k * NT;\n"
+             "        const u32 w = ITEM_W(k);\n"
              "        if (w < FC * NITEMS) Pl[(w % FC) * NITEMS + w / FC] = Zl[zi[k]] * Fp[k];\n"
              "    }\n"
              "    __syncthreads();\n"
