@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
 // full ones.
 constexpr int kQrowsBlock = 1024;
 constexpr uint32_t kQrowsMaxC = 4;
-template <int NV>
+template <int NV, bool EXACT>  // EXACT: nvar == NV (no padded factor slots)
 __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     const double *__restrict__ cvals, uint32_t nc, uint32_t cb, uint32_t nvar, uint32_t nrows,
     const double *__restrict__ Zg, const double *__restrict__ sv,
@@ -276,52 +276,73 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     MDP_STAMP(stamps, 0);
     const uint32_t c0 = blockIdx.x * cb, ncb = min(cb, nc - c0);
     double *Zl = lds;                                  // [cb][nrows]
-    double *Sv = Zl + (size_t)cb * nrows;              // [nrows][nvar]
-    double *Pl = Sv + (size_t)nrows * nvar;            // [cb][nitems]
+    double *Pr = Zl + (size_t)cb * nrows;              // [cb][nrows][NV] row colonisation pressures
+    double *Pl = Pr + (size_t)cb * nrows * NV;         // [cb][nitems]
     uint2 *It = (uint2 *)(Pl + (size_t)cb * nitems);   // [nitems] {B, j}, row in the top bytes
     uint32_t *Qs = (uint32_t *)(It + nitems);          // [ncoef + 1]
     uint32_t *Qi = Qs + ncoef + 1;                     // [nqi]
-    // var-column S transposed to [b][row]: lanes holding items of different
-    // rows read different banks
-    for (uint32_t i = threadIdx.x; i < nrows * nvar; i += kQrowsBlock) Sv[(i % nvar) * nrows + i / nvar] = sv[i];
     for (uint32_t i = threadIdx.x; i < nitems; i += kQrowsBlock) It[i] = items[i];
     for (uint32_t i = threadIdx.x; i <= ncoef; i += kQrowsBlock) Qs[i] = qstart[i];
     for (uint32_t i = threadIdx.x; i < nqi; i += kQrowsBlock) Qi[i] = qitem[i];
-    // 1. Z per (c, row), computed by k_zrows
     const uint32_t lcb = cb == 4 ? 2u : cb == 2 ? 1u : 0u;  // cb is 1, 2 or 4
+    double cv[kQrowsMaxC];  // this workgroup's c values, loaded once
+#pragma unroll
+    for (uint32_t i = 0; i < kQrowsMaxC; ++i) cv[i] = i < ncb ? cvals[c0 + i] : 0.0;
+    // 1. Z per (c, row), computed by k_zrows; per (c, row, var column b) the
+    // pressure pC = min(1, c S[j][b]), 1.0 for the columns of j (sv holds
+    // -1 there) and past nvar
     for (uint32_t w = threadIdx.x; w < (nrows << lcb); w += kQrowsBlock) {
         const uint32_t cl = w & (cb - 1), r = w >> lcb;
         if (cl < ncb) Zl[cl * nrows + r] = Zg[(size_t)r * nc + c0 + cl];
     }
-    __syncthreads();
-    MDP_STAMP(stamps, 1);
-    // 2. Pc per (c, item): Z times the product F of the var-column factors
-    // (pairwise tree over NV slots, 1.0 past nvar and for the bits of j -- the
-    // same tree as the fused kernel's over nvar).  Every operand is loaded
-    // before any arithmetic, so an item costs two LDS round trips.
-    double cv[kQrowsMaxC];  // this workgroup's c values, loaded once
-#pragma unroll
-    for (uint32_t i = 0; i < kQrowsMaxC; ++i) cv[i] = i < ncb ? cvals[c0 + i] : 0.0;
-    for (uint32_t w = threadIdx.x; w < (nitems << lcb); w += kQrowsBlock) {
-        const uint32_t cl = w & (cb - 1), it = w >> lcb;
+    for (uint32_t w = threadIdx.x; w < (nrows << lcb); w += kQrowsBlock) {  // a row's NV loads in flight
+        const uint32_t cl = w / nrows, r = w - cl * nrows;
         double c = cv[0];
 #pragma unroll
         for (uint32_t i = 1; i < kQrowsMaxC; ++i) c = cl == i ? cv[i] : c;
-        const uint2 t = It[it];
-        const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;
-        const double z = Zl[cl * nrows + r];
         double sb[NV];
 #pragma unroll
-        for (int b = 0; b < NV; ++b) sb[b] = Sv[((uint32_t)b < nvar ? (uint32_t)b : 0u) * nrows + r];
+        for (int b = 0; b < NV; ++b) sb[b] = EXACT || (uint32_t)b < nvar ? sv[(size_t)r * nvar + b] : -1.0;
+        double2 *pr = (double2 *)(Pr + (size_t)w * NV);
+#pragma unroll
+        for (int b = 0; b < NV; b += 2) {
+            double p2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                double pcv = c * sb[b + u];
+                pcv = pcv > 1.0 ? 1.0 : pcv;
+                p2[u] = sb[b + u] < 0.0 ? 1.0 : pcv;
+            }
+            pr[b / 2] = make_double2(p2[0], p2[1]);
+        }
+    }
+    __syncthreads();
+    MDP_STAMP(stamps, 1);
+    // 2. Pc per (c, item): Z times the product F of the var-column factors
+    // f_b = B_b ? pC_b : 1 - pC_b = fma(s_b, pC_b, n_b), (s_b, n_b) = (1, 0) or
+    // (-1, 1) built from the bit (j <= B, so j's columns give pC = 1.0), in
+    // the pairwise tree over NV slots -- the fused kernel's tree over nvar.
+    for (uint32_t w = threadIdx.x; w < (nitems << lcb); w += kQrowsBlock) {
+        const uint32_t cl = w & (cb - 1), it = w >> lcb;
+        const uint2 t = It[it];
+        const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), nB = ~t.x;
+        const double z = Zl[cl * nrows + r];
+        const double2 *pr = (const double2 *)(Pr + ((size_t)cl * nrows + r) * NV);
         double f[NV];
 #pragma unroll
+        for (int b = 0; b < NV / 2; ++b) {
+            const double2 p2 = pr[b];
+            f[2 * b] = p2.x;
+            f[2 * b + 1] = p2.y;
+        }
+#pragma unroll
         for (int b = 0; b < NV; ++b) {
-            const bool live = (uint32_t)b < nvar;
-            const uint32_t bit = live ? nvar - 1 - (uint32_t)b : 0u;
-            double pc = c * sb[b];
-            pc = pc > 1.0 ? 1.0 : pc;
-            const double fb = ((B >> bit) & 1u) ? pc : 1.0 - pc;
-            f[b] = (!live || ((j >> bit) & 1u)) ? 1.0 : fb;
+            // bit of B for slot b; slots past nvar read as set (pC = 1.0 there)
+            const uint32_t nbit = EXACT ? (nB >> (NV - 1 - b)) & 1u
+                                        : ((uint32_t)b < nvar ? (nB >> (nvar - 1 - (uint32_t)b)) & 1u : 0u);
+            const double sg = __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
+            const double nb = __hiloint2double((int)(nbit * 0x3ff00000u), 0);
+            f[b] = fma(sg, f[b], nb);
         }
 #pragma unroll
         for (int sh = 1; sh < NV; sh *= 2)
@@ -1135,7 +1156,8 @@ constexpr size_t kFusedLdsMax = 64 * 1024;  // fused forward kernel: every table
 // k_qrows LDS for cb c values per workgroup: Z, var-column S, Pc, Q CSR
 size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
 {
-    return ((size_t)cb * eng->nj + (size_t)eng->nj * eng->nvar + (size_t)cb * eng->nitems) * sizeof(double) +
+    const size_t nv = eng->nvar <= 8 ? 8 : eng->nvar <= 16 ? 16 : 24;  // k_qrows NV
+    return ((size_t)cb * eng->nj + (size_t)cb * eng->nj * nv + (size_t)cb * eng->nitems) * sizeof(double) +
            (size_t)eng->nitems * sizeof(uint2) + ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);
 }
 
@@ -1281,7 +1303,9 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
         std::vector<double> sv((size_t)eng->nj * eng->nvar + 1, 0.0);
         for (uint32_t js = 0; js < eng->nj; ++js)
             for (uint32_t b = 0; b < eng->nvar; ++b)
-                sv[(size_t)js * eng->nvar + b] = eng->Sj[(size_t)js * eng->n + eng->var_cols[b]];
+                sv[(size_t)js * eng->nvar + b] = ((eng->cj_bits[js] >> (eng->nvar - 1 - b)) & 1u)
+                                                      ? -1.0  // column of j: k_qrows sets pC = 1.0
+                                                      : eng->Sj[(size_t)js * eng->n + eng->var_cols[b]];
         std::vector<uint2> items(eng->nitems + 1, make_uint2(0u, 0u));
         for (uint32_t i = 0; i < eng->nitems; ++i) {
             const uint32_t r = eng->itemRow[i];
@@ -1294,7 +1318,8 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
             return rc;
         const size_t lds_max = qrows_lds(eng, kQrowsMaxC);
         if (lds_max > 64 * 1024)
-            for (const void *fn : {(const void *)k_qrows<8>, (const void *)k_qrows<16>, (const void *)k_qrows<24>})
+            for (const void *fn : {(const void *)k_qrows<8, true>, (const void *)k_qrows<8, false>,
+                                   (const void *)k_qrows<16, false>, (const void *)k_qrows<24, false>})
                 HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)std::min(lds_max, kQrowsLdsMax)));
         if ((rc = jit_load(eng, d, eng->fused_mode == 1))) return rc;
@@ -1504,13 +1529,14 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
         const uint32_t cb = d.qrows_cb;
         const dim3 grid((d.nc + cb - 1) / cb);
         const size_t lds = qrows_lds(eng, cb);
-#define MDP_QROWS(NV)                                                                                  \
-    MDP_LAUNCH(k_qrows<NV>, grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj, d.Zg,    \
+#define MDP_QROWS(NV, EX)                                                                              \
+    MDP_LAUNCH((k_qrows<NV, EX>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj, d.Zg,    \
                d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart, (uint32_t)eng->qitem.size(),        \
                d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1])
-        if (eng->nvar <= 8) MDP_QROWS(8);
-        else if (eng->nvar <= 16) MDP_QROWS(16);
-        else MDP_QROWS(24);
+        if (eng->nvar == 8) MDP_QROWS(8, true);
+        else if (eng->nvar < 8) MDP_QROWS(8, false);
+        else if (eng->nvar <= 16) MDP_QROWS(16, false);
+        else MDP_QROWS(24, false);
 #undef MDP_QROWS
         HIP_TRY(hipGetLastError());
         return MDP_OK;
