@@ -327,3 +327,19 @@ def test_cli_all_nan_file(tmp_path):
     assert r.returncode == 0
     assert "Total log-likelihood=-inf" in r.stdout
     assert out.read_text() == "-nan\t-nan\t-nan\t\n" * 3
+
+
+@pytest.mark.gpu
+def test_config1_after_other_kernels(golden):
+    """Stale LDS / device memory from earlier kernels must not leak into the
+    result: the scenario engine (154 KB of LDS per workgroup) runs first, then
+    the config-1 grid (n = nvar = 8, no always-zero column) is checked.  This
+    caught a staging race of the global_load_lds variant (now off by default)."""
+    row = mdp.first_row(golden / "occupancies.txt")
+    with mdp.Scenario(row, "dieoff", m=400, d=100) as sc:
+        sc.lik(np.linspace(0.0, 1.0, 64), np.array([0.3, 0.7]), mdp.kgrid(4), ts=5, tdis=3)
+    g, _ = mdp.grid(50)
+    model = mdp.Model.load(golden / "occupancies.txt", m=400, d=100)
+    got = gpu_grid(model, g)
+    ref = oracle.OracleModel.load(golden / "occupancies.txt", 400, 0.5, 100).loglik_grid(g, g)
+    assert_loglik_close(got, ref)
