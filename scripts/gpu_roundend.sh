@@ -3,6 +3,7 @@
 #   tests : the whole GPU test suite + smoke()
 #   prof  : rocprofv3 --kernel-trace --stats of every bench config, the
 #           FETCH/WRITE PMC passes of configs 2 and 3, the default bench line
+#   pmc   : only the PMC passes and the default bench line
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/roundend
@@ -15,8 +16,9 @@ if [ "$1" = tests ]; then
   cat $O/smoke.log
   exit 0
 fi
+mkdir -p $O/pmc
 cd /tmp && export TMPDIR=/tmp
-for spec in "2:--steps 50 --warmup 5" "3:--steps 20 --warmup 3" "4:--steps 3 --warmup 1" "5:--steps 20 --warmup 3"; do
+[ "$1" = pmc ] || for spec in "2:--steps 50 --warmup 5" "3:--steps 20 --warmup 3" "4:--steps 3 --warmup 1" "5:--steps 20 --warmup 3"; do
   CFG=${spec%%:*}; ARGS=${spec#*:}
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_cfg$CFG -o run -- python3 $R/bench.py --config $CFG $ARGS > $O/bench_cfg$CFG.json 2> $O/bench_cfg$CFG.err || { echo "prof cfg$CFG failed"; tail $O/bench_cfg$CFG.err; exit 1; }
   echo "prof cfg$CFG ok"
