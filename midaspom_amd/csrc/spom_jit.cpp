@@ -129,7 +129,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
           << std::max<uint32_t>(1u, (pl.ct_max / 2 + 256u * pl.fused_cols - 1) / (256u * pl.fused_cols)) << "\n";
     const int FC = pl.fused ? (pl.fused_cols > 0 ? pl.fused_cols : 1) : 1;
     o << "#define FC " << FC << "\n#define NT (KBLOCK * FC)\n";
-    o << "extern \"C\" __global__ __launch_bounds__(NT) void mdp_fwd_jit(\n"
+    o << "extern \"C\" __global__ __launch_bounds__(NT) "
+      << (pl.wpe > 0 ? "__attribute__((amdgpu_waves_per_eu(" + std::to_string(pl.wpe) + "))) " : std::string())
+      << "void mdp_fwd_jit(\n"
          "    const double *__restrict__ Qrow, double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
          "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps,\n"
          "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax)\n{\n"
