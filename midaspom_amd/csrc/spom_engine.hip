@@ -215,15 +215,26 @@ __global__ __launch_bounds__(kBlock) void k_zpv(
 // is FP64-VALU bound.  Same multiplication order as the fused forward kernel
 // (four chains over k mod 8), so both variants give identical bits.
 constexpr uint32_t kZRows = kBlock / 64;  // rows per workgroup
+constexpr uint32_t kZStage = 4;           // staging loads in flight per thread
 __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cvals, uint32_t nc,
                                                   uint32_t nrows, uint32_t kmax,
-                                                  const double *__restrict__ zs, double *__restrict__ Zg)
+                                                  const double *__restrict__ zsT, double *__restrict__ Zg)
 {
     extern __shared__ __attribute__((aligned(16))) double zl[];  // [kZRows][kmax]
     const uint32_t r0 = blockIdx.y * kZRows, nr = min(kZRows, nrows - r0);
-    for (uint32_t i = threadIdx.x; i < kZRows * kmax; i += kBlock) {
-        const uint32_t w = i % kZRows, k = i / kZRows;
-        zl[w * kmax + k] = w < nr ? zs[(size_t)k * nrows + r0 + w] : 0.0;
+    // the workgroup's rows are contiguous in the row-major copy zsT[row][k]:
+    // coalesced loads, kZStage in flight per thread before any store
+    const uint32_t nst = nr * kmax;
+    for (uint32_t i0 = threadIdx.x; i0 < kZRows * kmax; i0 += kZStage * kBlock) {
+        double t[kZStage];
+#pragma unroll
+        for (uint32_t u = 0; u < kZStage; ++u) {
+            const uint32_t i = i0 + u * kBlock;
+            t[u] = i < nst ? zsT[(size_t)r0 * kmax + i] : 0.0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kZStage; ++u)
+            if (i0 + u * kBlock < kZRows * kmax) zl[i0 + u * kBlock] = t[u];
     }
     __syncthreads();
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
@@ -232,14 +243,25 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
     const double c = ic < nc ? cvals[ic] : 0.0;
     const double *z = zl + w * kmax;
     double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;
-    for (uint32_t k = 0; k < kmax; k += 8) {
-        double sk[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) sk[u] = z[k + u];
+    auto chunk = [&](const double *sk) {
         za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
         zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);
         zc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);
         zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
+    };
+    uint32_t k = 0;
+    for (; k + 16 <= kmax; k += 16) {  // two chunks' reads in flight
+        double sk[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) sk[u] = z[k + u];
+        chunk(sk);
+        chunk(sk + 8);
+    }
+    if (k < kmax) {  // kmax is a multiple of 8
+        double sk[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sk[u] = z[k + u];
+        chunk(sk);
     }
     double zz = (za * zb) * (zc * zd);
     if (kmax && !(fma(-c, z[0], 1.0) > 0.0)) zz = 0.0;
@@ -845,7 +867,8 @@ struct DevCtx {
     unsigned long long *stamps[3] = {nullptr, nullptr, nullptr};  // k_zpv, k_coefs, k_forward
     size_t cap_st[3] = {0, 0, 0};
     size_t nst[3] = {0, 0, 0};
-    // direct path: k_qrows tables (zs depends on the grid's c range)
+    // direct path: k_zrows / k_qrows tables (zs, row-major [row][k], depends
+    // on the grid's c range)
     double *zs = nullptr, *sv = nullptr, *Qrow = nullptr, *Zg = nullptr;
     uint2 *items = nullptr;  // per item {B | row << 24, j | (row >> 8) << 24}
     uint32_t *itemB = nullptr, *qstart = nullptr, *qitem = nullptr;
@@ -1187,12 +1210,15 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
         kmax = std::max(kmax, r.size());
     }
     kmax = (kmax + 7) & ~(size_t)7;
-    std::vector<double> zs(kmax * nj + 1, 0.0);
+    std::vector<double> zs(kmax * nj + 1, 0.0);  // [k][row]: the fused kernel's image
     for (uint32_t js = 0; js < nj; ++js)
         for (size_t k = 0; k < rows[js].size(); ++k) zs[k * nj + js] = rows[js][k];
+    std::vector<double> zsT(kmax * nj + 1, 0.0);  // [row][k]: k_zrows (device copy)
+    for (uint32_t js = 0; js < nj; ++js)
+        for (size_t k = 0; k < rows[js].size(); ++k) zsT[js * kmax + k] = rows[js][k];
     int rc;
-    if ((rc = dev_reserve(&d.zs, &d.cap_zs, zs.size()))) return rc;
-    HIP_TRY(hipMemcpy(d.zs, zs.data(), zs.size() * sizeof(double), hipMemcpyHostToDevice));
+    if ((rc = dev_reserve(&d.zs, &d.cap_zs, zsT.size()))) return rc;
+    HIP_TRY(hipMemcpy(d.zs, zsT.data(), zsT.size() * sizeof(double), hipMemcpyHostToDevice));
     d.zs_cmax = cmax;
     d.zs_len = (uint32_t)(kmax * nj);
     d.zs_kmax = (uint32_t)kmax;
