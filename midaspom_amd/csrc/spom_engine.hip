@@ -303,13 +303,34 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     uint2 *It = (uint2 *)(Pl + (size_t)cb * nitems);   // [nitems] {B, j}, row in the top bytes
     uint32_t *Qs = (uint32_t *)(It + nitems);          // [ncoef + 1]
     uint32_t *Qi = Qs + ncoef + 1;                     // [nqi]
-    for (uint32_t i = threadIdx.x; i < nitems; i += kQrowsBlock) It[i] = items[i];
-    for (uint32_t i = threadIdx.x; i <= ncoef; i += kQrowsBlock) Qs[i] = qstart[i];
-    for (uint32_t i = threadIdx.x; i < nqi; i += kQrowsBlock) Qi[i] = qitem[i];
     const uint32_t lcb = cb == 4 ? 2u : cb == 2 ? 1u : 0u;  // cb is 1, 2 or 4
     double cv[kQrowsMaxC];  // this workgroup's c values, loaded once
 #pragma unroll
     for (uint32_t i = 0; i < kQrowsMaxC; ++i) cv[i] = i < ncb ? cvals[c0 + i] : 0.0;
+    // items and the Q CSR: every thread's loads of all three tables in flight
+    // before its stores (one global round trip instead of one per pass)
+    {
+        constexpr uint32_t kSt = 4;
+        const uint32_t nmax = max(max(nitems, ncoef + 1), nqi);
+        for (uint32_t i0 = threadIdx.x; i0 < nmax; i0 += kSt * kQrowsBlock) {
+            uint2 ti[kSt];
+            uint32_t ts[kSt], tq[kSt];
+#pragma unroll
+            for (uint32_t u = 0; u < kSt; ++u) {
+                const uint32_t i = i0 + u * kQrowsBlock;
+                ti[u] = i < nitems ? items[i] : make_uint2(0u, 0u);
+                ts[u] = i <= ncoef ? qstart[i] : 0u;
+                tq[u] = i < nqi ? qitem[i] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kSt; ++u) {
+                const uint32_t i = i0 + u * kQrowsBlock;
+                if (i < nitems) It[i] = ti[u];
+                if (i <= ncoef) Qs[i] = ts[u];
+                if (i < nqi) Qi[i] = tq[u];
+            }
+        }
+    }
     // 1. Z per (c, row), computed by k_zrows; per (c, row, var column b) the
     // pressure pC = min(1, c S[j][b]), 1.0 for the columns of j (sv holds
     // -1 there) and past nvar
