@@ -1244,8 +1244,10 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     d.zs_len = (uint32_t)(kmax * nj);
     d.zs_kmax = (uint32_t)kmax;
     // the fused kernel's column tables: one contiguous image it copies to LDS
+    // (with zpad, all KZ zs rows, zero past kmax: the kernel reads them unmasked)
     const MdpJitPlan &pl = eng->jit_plan;
-    const size_t ct = ((size_t)pl.off_zs + kmax * nj + 127) & ~(size_t)127;
+    const size_t kimg = pl.zpad ? std::max<size_t>(kmax, std::max<uint32_t>(8u, pl.kzmax)) : kmax;
+    const size_t ct = ((size_t)pl.off_zs + kimg * nj + 127) & ~(size_t)127;
     std::vector<double> img(ct, 0.0);
     for (uint32_t js = 0; js < nj; ++js)
         for (uint32_t b = 0; b < eng->nvar; ++b)
@@ -1768,6 +1770,10 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             const size_t kmax_max = ((size_t)(eng->n - eng->nvar) + 7) & ~(size_t)7;
             plan.ct_max = (uint32_t)std::min<size_t>(((plan.off_zs + kmax_max * eng->nj) + 127) & ~(size_t)127,
                                                      kFusedLdsMax / sizeof(double));
+            {   // zero-padded zs image when the largest one fits the fused kernel's LDS
+                const size_t kz = std::max<size_t>(8, kmax_max);
+                plan.zpad = fused_lds(eng, ((plan.off_zs + kz * eng->nj) + 127) & ~(size_t)127) <= kFusedLdsMax;
+            }
             if (jit_check && ndev == 0) {
                 const int r0 = jit_build(eng, false), r1 = r0 ? r0 : jit_build(eng, true);
                 delete eng;

@@ -123,7 +123,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         o << "#define NJ " << pl.nj << "\n#define NVAR " << pl.nvar << "\n#define NITEMS " << pl.nitems
           << "\n#define NCOEF " << pl.ncoef << "\n#define NQI " << (pl.nqi ? pl.nqi : 1) << "\n#define OFF_IT "
           << pl.off_it << "\n#define OFF_QS " << pl.off_qs << "\n#define OFF_QI " << pl.off_qi << "\n#define OFF_ZS "
-          << pl.off_zs << "\n#define KZ " << std::max<uint32_t>(8u, pl.kzmax) << "\n#define QML "
+          << pl.off_zs << "\n#define KZ " << std::max<uint32_t>(8u, pl.kzmax) << "\n#define ZPAD " << (pl.zpad ? 1 : 0)
+          << "\n#define QML "
           << std::max<uint32_t>(1u, pl.qmaxlen) << "\n#define QUN " << std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)
           << "\n#define NSTG "
           << std::max<uint32_t>(1u, (pl.ct_max / 2 + 256u * pl.fused_cols - 1) / (256u * pl.fused_cols)) << "\n";
@@ -264,7 +265,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        for (int u = 0; u < QUN; ++u) qx[k][u] = Qil[q0 + u < NQI ? q0 + u : NQI - 1];\n"
              "    }\n"
              // Z per (column, row): the row's KZ (compile-time bound) values
-             // all in flight; rows past kmax contribute fma(-c, 0, 1) = 1
+             // all in flight; rows past kmax contribute fma(-c, 0, 1) = 1 (with
+             // ZPAD the image holds those zero rows, so no per-value select)
              "#pragma unroll\n"
              "    for (int k = 0; k < (FC * NJ + NT - 1) / NT; ++k) {\n"
              "        const u32 w = threadIdx.x + k * NT;\n"
@@ -273,11 +275,11 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "            const double c = cc[col];\n"
              "            double sk[KZ];\n"
              "#pragma unroll\n"
-             "            for (u32 kk = 0; kk < KZ; ++kk) sk[kk] = zl[(kk < kmax ? kk : kk % 8u) * NJ + r];\n"
+             "            for (u32 kk = 0; kk < KZ; ++kk) sk[kk] = zl[(ZPAD || kk < kmax ? kk : kk % 8u) * NJ + r];\n"
              "            double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
              "#pragma unroll\n"
              "            for (u32 kk = 0; kk < KZ; kk += 8) {\n"
-             "                const bool in = kk < kmax;\n"
+             "                const bool in = ZPAD || kk < kmax;\n"
              "#pragma unroll\n"
              "                for (int u = 0; u < 8; ++u) sk[kk + u] = in ? sk[kk + u] : 0.0;\n"
              "                za *= fma(-c, sk[kk + 0], 1.0) * fma(-c, sk[kk + 4], 1.0);\n"

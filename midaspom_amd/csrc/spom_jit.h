@@ -24,6 +24,7 @@ struct MdpJitPlan {
     // root cause not found -- register staging is the validated default
     bool glds = false;
     uint32_t kzmax = 0;    // bound on the zs rows of any grid: n - nvar rounded up to 8
+    bool zpad = false;     // the fused image always holds kzmax zs rows (zero past kmax)
     uint32_t qmaxlen = 0;  // most items of one Q entry
     uint32_t ct_max = 0;  // largest column-table image (doubles), for the register staging
     int epl = 0;                  // grid points per lane (0: 2 unless the weight table is large)
