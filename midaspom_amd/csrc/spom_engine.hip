@@ -1260,7 +1260,8 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     memcpy(img.data() + pl.off_qs, eng->qstart.data(), eng->qstart.size() * sizeof(uint32_t));
     if (!eng->qitem.empty())
         memcpy(img.data() + pl.off_qi, eng->qitem.data(), eng->qitem.size() * sizeof(uint32_t));
-    std::copy(zs.begin(), zs.begin() + kmax * nj, img.begin() + pl.off_zs);
+    for (size_t k = 0; k < kmax; ++k)  // zs pairs (k, k+1) of a row adjacent: one ds_read_b128
+        for (uint32_t js = 0; js < nj; ++js) img[pl.off_zs + ((k / 2) * nj + js) * 2 + (k & 1)] = zs[k * nj + js];
     if ((rc = dev_reserve(&d.coltab, &d.cap_coltab, ct))) return rc;
     HIP_TRY(hipMemcpy(d.coltab, img.data(), ct * sizeof(double), hipMemcpyHostToDevice));
     d.ct_len = (uint32_t)ct;

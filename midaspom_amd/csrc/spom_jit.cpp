@@ -177,8 +177,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         // the k_qrows phases for this one c value (spom_engine.hip k_qrows):
         // Z per hidden-state row, Pc per item, Q per entry -- all in LDS.
         // The column tables (host-built, 1 KiB-padded: var-column S, items,
-        // CSR, then zs[k][row]) are copied to LDS by global_load_lds_dwordx4
-        // -- every wave-instruction 1 KiB, all in flight, one barrier.
+        // CSR, then zs as [k/2][row][k%2]) are copied to LDS through registers
+        // (or global_load_lds_dwordx4 with MDP_JIT_GLDS), all in flight, one barrier.
         o << "    extern __shared__ __attribute__((aligned(16))) double ct[];\n"
              "    __shared__ double Zl[FC * NJ];\n"
              "    __shared__ double Pl[FC * NITEMS];\n"
@@ -237,14 +237,19 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        const double c = cc[col];\n"
              "        const uint2 t = Itl[it];\n"
              "        const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
+             // f_b = j_b ? 1 : B_b ? p_b : 1 - p_b with p_b = min(1, c S): one
+             // select for the clamp and j (j <= B, so B_b is set there), then
+             // fma(s, p, n) with (s, n) = (1, 0) or (-1, 1) from B_b -- the
+             // same bits as the select form (k_qrows uses the same fold)
              "        double f[NVAR];\n"
+             "        const u32 nB = ~B;\n"
              "#pragma unroll\n"
              "        for (int b = 0; b < NVAR; ++b) {\n"
              "            const u32 bit = NVAR - 1 - b;\n"
-             "            double pcv = c * Svl[r * NVAR + b];\n"
-             "            pcv = pcv > 1.0 ? 1.0 : pcv;\n"
-             "            const double fb = ((B >> bit) & 1u) ? pcv : 1.0 - pcv;\n"
-             "            f[b] = ((j >> bit) & 1u) ? 1.0 : fb;\n"
+             "            const double pcv = c * Svl[r * NVAR + b];\n"
+             "            const double p = (pcv > 1.0) | ((j >> bit) & 1u) ? 1.0 : pcv;\n"
+             "            const double sg = __hiloint2double((int)(0x3ff00000u | ((nB << (31 - bit)) & 0x80000000u)), 0);\n"
+             "            f[b] = fma(sg, p, fma(-0.5, sg, 0.5));\n"
              "        }\n"
              "#pragma unroll\n"
              "        for (int s = 1; s < NVAR; s *= 2)\n"
@@ -275,7 +280,11 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "            const double c = cc[col];\n"
              "            double sk[KZ];\n"
              "#pragma unroll\n"
-             "            for (u32 kk = 0; kk < KZ; ++kk) sk[kk] = zl[(ZPAD || kk < kmax ? kk : kk % 8u) * NJ + r];\n"
+             "            for (u32 kk = 0; kk < KZ; kk += 2) {\n"
+             "                const double2 t2 = ((const double2 *)zl)[(ZPAD || kk < kmax ? kk : kk % 8u) / 2 * NJ + r];\n"
+             "                sk[kk] = t2.x;\n"
+             "                sk[kk + 1] = t2.y;\n"
+             "            }\n"
              "            double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
              "#pragma unroll\n"
              "            for (u32 kk = 0; kk < KZ; kk += 8) {\n"
@@ -288,7 +297,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "                zd *= fma(-c, sk[kk + 3], 1.0) * fma(-c, sk[kk + 7], 1.0);\n"
              "            }\n"
              "            double z = (za * zb) * (zc * zd);\n"
-             "            if (kmax && !(fma(-c, zl[r], 1.0) > 0.0)) z = 0.0;\n"
+             "            if (kmax && !(fma(-c, sk[0], 1.0) > 0.0)) z = 0.0;\n"
              "            Zl[col * NJ + r] = z;\n"
              "        }\n"
              "    }\n"
