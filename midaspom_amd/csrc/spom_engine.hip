@@ -1306,7 +1306,7 @@ int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 size_t fused_lds(const mdp_engine *eng, size_t ct_len)
 {
     const size_t fc = (size_t)eng->jit_plan.fused_cols;
-    return (ct_len + fc * (eng->nj + eng->nitems + eng->ldQ)) * sizeof(double);
+    return (ct_len + 2 + fc * (eng->nj + eng->nitems + eng->ldQ)) * sizeof(double);  // + staging scratch
 }
 
 int upload_binomials()  // into the current device's constant bank
@@ -1513,7 +1513,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
         const uint64_t nb = d.fused ? (d.nc + fc - 1) / fc : gy * d.nc;
         if (nb * kBlock * fc > 0xffffffffull)
             return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
-        const uint32_t dyn = d.fused ? d.ct_len * (uint32_t)sizeof(double) : 0u;
+        const uint32_t dyn = d.fused ? (d.ct_len + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch
         HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kBlock * fc), 1, 1, kBlock * fc, 1, 1, dyn, s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));
         return MDP_OK;

@@ -136,7 +136,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    const double *__restrict__ Qrow, double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
          "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps,\n"
          "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax)\n{\n"
-         "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ];\n"
+         "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ + 2];\n"
       << stamp(6) << stamp(0) <<
          // XCD-aware order: the dispatcher deals blocks round-robin over the 8
          // XCDs, so consecutive logical blocks (adjacent c columns of the
@@ -156,17 +156,48 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "        ie[i] = by * (KBLOCK * EPL) + i * KBLOCK + tid;\n"
          "        ev[i] = ie[i] < ne ? evals[ie[i]] : 0.0;\n"
          "    }\n";
-    // stage n doubles from src (16-byte aligned, n even) into the LDS array dst
+    // per point: the weight table W[|A|][m] = x^(|A|-m) y^m and the state
+    // vector (emitted before the final prologue barrier; placing it between
+    // the table loads and stores made no difference: the compiler sinks it)
+    std::string wblock;
+    {
+        std::ostringstream w;
+        w << "#pragma unroll\n"
+             "    for (int i = 0; i < EPL; ++i) {\n"
+             "        const double e = ev[i];\n"
+             "        const double x = e > 1.0 ? 1.0 : e;\n"
+             "        const double y = 1.0 - x;\n"
+             "        double xp[DMAX + 1], yp[DMAX + 1];\n        xp[0] = 1.0;\n        yp[0] = 1.0;\n"
+             "#pragma unroll\n        for (int r = 1; r <= DMAX; ++r) { xp[r] = xp[r - 1] * x; yp[r] = yp[r - 1] * y; }\n";
+        for (auto &kv : widx)
+            w << "        W[i][" << kv.second << "] = xp[" << (kv.first.first - kv.first.second) << "] * yp["
+              << kv.first.second << "];\n";
+        w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < " << np0
+          << " ? 1.0 : 0.0;\n"
+             "    }\n";
+        wblock = w.str();
+    }
+    o << "    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n";
+    // stage n (compile-time, even) doubles from src (16-byte aligned) into the
+    // LDS array dst, which has a double2 of scratch past n: every load is
+    // issued before any store, and the stores are unconditional, so the
+    // compiler cannot sink each load into its own guarded store (that
+    // serialised the staging into one global round trip per load)
     auto stage = [&](const char *dst, const char *src, const char *n) {
         o << "    {\n"
              "        const double2 *src_ = (const double2 *)(" << src << ");\n"
              "        double2 *dst_ = (double2 *)" << dst << ";\n"
-             "        for (u32 i0 = threadIdx.x; i0 < " << n << " / 2; i0 += 2 * KBLOCK) {\n"
-             "            const u32 i1 = i0 + KBLOCK;\n"
-             "            const double2 t0 = src_[i0];\n"
-             "            const double2 t1 = src_[i1 < " << n << " / 2 ? i1 : i0];\n"
-             "            dst_[i0] = t0;\n"
-             "            if (i1 < " << n << " / 2) dst_[i1] = t1;\n"
+             "        constexpr u32 N2 = (" << n << ") / 2, NK = (N2 + NT - 1) / NT;\n"
+             "        double2 t_[NK];\n"
+             "#pragma unroll\n"
+             "        for (u32 k = 0; k < NK; ++k) {\n"
+             "            const u32 i = threadIdx.x + k * NT;\n"
+             "            t_[k] = src_[i < N2 ? i : 0];\n"
+             "        }\n"
+             "#pragma unroll\n"
+             "        for (u32 k = 0; k < NK; ++k) {\n"
+             "            const u32 i = threadIdx.x + k * NT;\n"
+             "            dst_[i < N2 ? i : N2] = t_[k];\n"
              "        }\n"
              "    }\n";
     };
@@ -210,7 +241,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "#pragma unroll\n"
              "        for (int k = 0; k < NSTG; ++k) {\n"
              "            const u32 i = threadIdx.x + k * NT;\n"
-             "            if (i < n2) dst[i] = t[k];\n"
+             // unconditional: lanes past the image write a scratch slot, so the
+             // loads are not sunk into per-load branches (load, wait, store x NSTG)
+             "            dst[i < n2 ? i : n2] = t[k];\n"
              "        }\n"
              "    }\n") <<
              "    __syncthreads();\n"
@@ -329,22 +362,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        }\n"
              "    }\n";
     }
-    o <<
-         "    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n"
-         "#pragma unroll\n"
-         "    for (int i = 0; i < EPL; ++i) {\n"
-         "        const double e = ev[i];\n"
-         "        const double x = e > 1.0 ? 1.0 : e;\n"
-         "        const double y = 1.0 - x;\n"
-         "        double xp[DMAX + 1], yp[DMAX + 1];\n        xp[0] = 1.0;\n        yp[0] = 1.0;\n"
-         "#pragma unroll\n        for (int r = 1; r <= DMAX; ++r) { xp[r] = xp[r - 1] * x; yp[r] = yp[r - 1] * y; }\n";
-    for (auto &kv : widx)
-        o << "        W[i][" << kv.second << "] = xp[" << (kv.first.first - kv.first.second) << "] * yp["
-          << kv.first.second << "];\n";
-    o << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < " << np0
-      << " ? 1.0 : 0.0;\n"
-         "    }\n"
-         "    __syncthreads();\n"
+    o << wblock;
+    o << "    __syncthreads();\n"
       << stamp(2);
     // P = sum_m Q[off+m] W[|A|][m] as an expression for point i
     auto pexpr = [&](uint32_t d) {
