@@ -343,3 +343,24 @@ def test_config1_after_other_kernels(golden):
     got = gpu_grid(model, g)
     ref = oracle.OracleModel.load(golden / "occupancies.txt", 400, 0.5, 100).loglik_grid(g, g)
     assert_loglik_close(got, ref)
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_grid_dropping_columns_then_full_grid(monkeypatch, fused):
+    """A c grid so small that every always-zero column's factor rounds to 1.0
+    (all of them are dropped: kmax = 0, the fused image holds only zero Z
+    rows), then a full grid on the same engine (the image is rebuilt with
+    every column).  Both variants against the oracle."""
+    monkeypatch.setenv("MDP_FUSED", fused)
+    rng = np.random.default_rng(77)
+    obs = synth.random_obs(rng, 24, 12, 4, pmiss=0.1, max_missing=3, p1=0.9)
+    model = mdp.Model.from_obs(obs, m=400.0, p=0.5, d=100.0)
+    ref_model = oracle.OracleModel.from_obs(obs, 400.0, 0.5, 100.0)
+    e, _ = mdp.grid(9, 0.0, 1.0)
+    tiny = np.array([0.0, 1e-30, 3e-25, 1e-21], dtype=np.float64)
+    full, _ = mdp.grid(7, 0.0, 1.0)
+    with mdp.Engine(model) as eng:
+        for c in (tiny, full, tiny):
+            ref = ref_model.loglik_grid(e, c)
+            assert np.isfinite(ref).sum() >= 20  # not only impossible points
+            assert_loglik_close(eng.loglik_grid(e, c), ref)
