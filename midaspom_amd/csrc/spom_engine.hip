@@ -210,12 +210,16 @@ __global__ __launch_bounds__(kBlock) void k_zpv(
 
 // Z rows of the direct path: Zg[row][c] = prod over the always-zero columns k
 // of 1 - min(1, c S[j][k]) for every needed hidden state j ("row").  Lanes run
-// over 64 c values and each wave over one row, so the S values are LDS
-// broadcasts (the workgroup's rows staged once from zs[k][row]); the product
-// is FP64-VALU bound.  Same multiplication order as the fused forward kernel
-// (four chains over k mod 8), so both variants give identical bits.
+// over c values and each wave over one row, so the S values are LDS
+// broadcasts (the workgroup's rows staged once from zs[k][row]).  A broadcast
+// read still returns 8 bytes per lane, so with one c per lane the kernel was
+// bound by LDS return bandwidth rather than by its FMAs: each lane now
+// carries kZC c values that share every read.  Same multiplication order as
+// the fused forward kernel (four chains over k mod 8), so both variants give
+// identical bits.
 constexpr uint32_t kZRows = kBlock / 64;  // rows per workgroup
 constexpr uint32_t kZStage = 4;           // staging loads in flight per thread
+constexpr uint32_t kZC = 2;               // c values per lane
 __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cvals, uint32_t nc,
                                                   uint32_t nrows, uint32_t kmax,
                                                   const double *__restrict__ zsT, double *__restrict__ Zg)
@@ -239,15 +243,23 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
     __syncthreads();
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
     if (w >= nr) return;
-    const uint32_t ic = blockIdx.x * 64 + (threadIdx.x & 63);
-    const double c = ic < nc ? cvals[ic] : 0.0;
+    uint32_t ic[kZC];
+    double c[kZC], za[kZC], zb[kZC], zc[kZC], zd[kZC];
+#pragma unroll
+    for (uint32_t x = 0; x < kZC; ++x) {
+        ic[x] = blockIdx.x * (64 * kZC) + x * 64 + (threadIdx.x & 63);
+        c[x] = ic[x] < nc ? cvals[ic[x]] : 0.0;
+        za[x] = zb[x] = zc[x] = zd[x] = 1.0;
+    }
     const double *z = zl + w * kmax;
-    double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;
     auto chunk = [&](const double *sk) {
-        za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
-        zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);
-        zc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);
-        zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
+#pragma unroll
+        for (uint32_t x = 0; x < kZC; ++x) {
+            za[x] *= fma(-c[x], sk[0], 1.0) * fma(-c[x], sk[4], 1.0);
+            zb[x] *= fma(-c[x], sk[1], 1.0) * fma(-c[x], sk[5], 1.0);
+            zc[x] *= fma(-c[x], sk[2], 1.0) * fma(-c[x], sk[6], 1.0);
+            zd[x] *= fma(-c[x], sk[3], 1.0) * fma(-c[x], sk[7], 1.0);
+        }
     };
     uint32_t k = 0;
     for (; k + 16 <= kmax; k += 16) {  // two chunks' reads in flight
@@ -263,9 +275,12 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
         for (int u = 0; u < 8; ++u) sk[u] = z[k + u];
         chunk(sk);
     }
-    double zz = (za * zb) * (zc * zd);
-    if (kmax && !(fma(-c, z[0], 1.0) > 0.0)) zz = 0.0;
-    if (ic < nc) Zg[(size_t)(r0 + w) * nc + ic] = zz;
+#pragma unroll
+    for (uint32_t x = 0; x < kZC; ++x) {
+        double zz = (za[x] * zb[x]) * (zc[x] * zd[x]);
+        if (kmax && !(fma(-c[x], z[0], 1.0) > 0.0)) zz = 0.0;
+        if (ic[x] < nc) Zg[(size_t)(r0 + w) * nc + ic[x]] = zz;
+    }
 }
 
 // Transition coefficients of the direct path, one workgroup per kQrowsMaxC
@@ -1571,7 +1586,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
     if (k == 2) return launch_forward(eng, d, out, ld, s);
     if (eng->jit && k == 0) {  // Z rows
         const uint32_t kmax = d.zs_kmax;
-        const dim3 grid((d.nc + 63) / 64, (eng->nj + kZRows - 1) / kZRows);
+        const dim3 grid((d.nc + 64 * kZC - 1) / (64 * kZC), (eng->nj + kZRows - 1) / kZRows);
         MDP_LAUNCH(k_zrows, grid, dim3(kBlock), (size_t)kZRows * kmax * sizeof(double), s, d.c, d.nc, eng->nj,
                    kmax, d.zs, d.Zg);
         HIP_TRY(hipGetLastError());
