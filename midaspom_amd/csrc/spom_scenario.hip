@@ -92,11 +92,12 @@ __host__ __device__ constexpr int sup_rank(int NL, int jl, int bl)
 
 // v(lane) + v(lane ^ 32) in every lane, by two v_permlane32_swap (VALU; no
 // LDS traffic); both halves add the same two values, so they agree bitwise
-__device__ __forceinline__ double half_sum(double v)
+// lanes 0-31: a[lane] + a[lane + 32]; lanes 32-63: b[lane - 32] + b[lane]
+// (one v_permlane32_swap per 32-bit word, no copies: both outputs are used)
+__device__ __forceinline__ double pair_sum(double a, double b)
 {
-    const unsigned lo = __double2loint(v), hi = __double2hiint(v);
-    const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const auto l2 = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto h2 = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
     return __hiloint2double(h2[0], l2[0]) + __hiloint2double(h2[1], l2[1]);
 }
 
@@ -297,9 +298,8 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
                 }
             }
             }
-#pragma unroll
-            for (int l = 0; l < NLO; ++l) acc[l] = half_sum(acc[l]);
-            // extinction on the lo patches, ascending patch
+            // extinction on the lo patches, ascending patch -- linear, so it
+            // is applied to each half's partial sums before they are combined
 #pragma unroll
             for (int k = NH; k < N; ++k) {
                 const int m = 1 << (N - 1 - k);
@@ -307,10 +307,12 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
                 for (int l = 0; l < NLO; ++l)
                     if (l & m) acc[l] = E * acc[l ^ m] + E1 * acc[l];
             }
+            // halves combined: one swap per row pair (l, l + NLO/2) leaves row
+            // l's total in the lower half and row l + NLO/2's in the upper
+            // half, each the row that half writes
 #pragma unroll
-            for (int l = 0; l < NLO; ++l)
-                if ((NLO == 1 && g == 0) || (NLO > 1 && (uint32_t)(l >= NLO / 2) == g))
-                    yb[l * LS + jh * kE + le] = acc[l];
+            for (int l = 0; l < NLO / 2; ++l)
+                yb[(l + g * (NLO / 2)) * LS + jh * kE + le] = pair_sum(acc[l], acc[l + NLO / 2]);
         }
         __syncthreads();
         // extinction on the hi patches: thread (lo, e) holds the 2^NH states
