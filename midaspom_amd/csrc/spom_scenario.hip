@@ -220,7 +220,9 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
     for (int t = 0; t < a.years; ++t) {
         // colonisation: rows (jh, .) of this wave's hi rows, into yb
         for (uint32_t slot = 0; slot < a.nsched; ++slot) {
-            const uint32_t jh = jsched[w * a.nsched + slot];
+            // wave-uniform (readfirstlane): the row's loop bounds, free-patch
+            // masks and superset walk stay in scalar registers
+            const uint32_t jh = __builtin_amdgcn_readfirstlane(jsched[w * a.nsched + slot]);
             if (jh >= (uint32_t)NHI) break;  // wave-uniform
             const uint32_t fr = ~jh & (NHI - 1), f = __popc(fr);
             const uint32_t top = f ? 1u << (31 - __clz(fr)) : 0u, frp = fr & ~top;
