@@ -246,10 +246,12 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
             for (int l = 0; l < NLO; ++l) acc[l] = 0.0;
             // supersets in pairs, ping-pong register buffers: the next
             // superset's states and factors load under this one's FMAs
+            // superset bh = jh | sub | (upper half ? top : 0): the bits are
+            // disjoint, so its states sit at yrow + sub kE (sub wave-uniform)
+            const double *yrow = y + (jh | (g ? top : 0u)) * kE + le;
             auto load = [&](uint32_t it, uint32_t sub, double (&yc)[NLO], double (&bv)[NLO]) {
-                const uint32_t bh = jh | sub | (g ? top : 0u);
 #pragma unroll
-                for (int l = 0; l < NLO; ++l) yc[l] = y[l * LS + bh * kE + le];
+                for (int l = 0; l < NLO; ++l) yc[l] = yrow[l * LS + sub * kE];
                 const double2 *bp = (const double2 *)(bt + it * NLO);
 #pragma unroll
                 for (int l = 0; l < NLO / 2; ++l) {
