@@ -271,12 +271,29 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
                 }
             };
             uint32_t sub = 0;
-            if (!kPingPong) {  // latency hidden by the other waves of the SIMD
+            if (!kPingPong) {
+                // the next superset's states load under this one's FMAs (its
+                // hi factors are first needed at the end of each row's chain,
+                // so they load in place)
+                double yn[NLO];
+#pragma unroll
+                for (int l = 0; l < NLO; ++l) yn[l] = yrow[l * LS];
                 for (uint32_t it = 0; it < units; ++it) {
                     double ya[NLO], ba[NLO];
-                    load(it, sub, ya, ba);
+#pragma unroll
+                    for (int l = 0; l < NLO; ++l) ya[l] = yn[l];
+                    const uint32_t sn = (sub - frp) & frp;  // wraps to 0 after the last
+#pragma unroll
+                    for (int l = 0; l < NLO; ++l) yn[l] = yrow[l * LS + sn * kE];
+                    const double2 *bp = (const double2 *)(bt + it * NLO);
+#pragma unroll
+                    for (int l = 0; l < NLO / 2; ++l) {
+                        const double2 t2 = bp[l];
+                        ba[2 * l] = t2.x;
+                        ba[2 * l + 1] = t2.y;
+                    }
                     accumulate(ya, ba);
-                    sub = (sub - frp) & frp;
+                    sub = sn;
                 }
             } else {
             double ya[NLO], ba[NLO], yb2[NLO], bb[NLO];
