@@ -90,8 +90,6 @@ __host__ __device__ constexpr int sup_rank(int NL, int jl, int bl)
     return r;
 }
 
-// v(lane) + v(lane ^ 32) in every lane, by two v_permlane32_swap (VALU; no
-// LDS traffic); both halves add the same two values, so they agree bitwise
 // lanes 0-31: a[lane] + a[lane + 32]; lanes 32-63: b[lane - 32] + b[lane]
 // (one v_permlane32_swap per 32-bit word, no copies: both outputs are used)
 __device__ __forceinline__ double pair_sum(double a, double b)
