@@ -242,8 +242,6 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
             double acc[NLO];
 #pragma unroll
             for (int l = 0; l < NLO; ++l) acc[l] = 0.0;
-            // supersets in pairs, ping-pong register buffers: the next
-            // superset's states and factors load under this one's FMAs
             // superset bh = jh | sub | (upper half ? top : 0): the bits are
             // disjoint, so its states sit at yrow + sub kE (sub wave-uniform)
             const double *yrow = y + (jh | (g ? top : 0u)) * kE + le;
@@ -294,6 +292,8 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
                     sub = sn;
                 }
             } else {
+            // supersets in pairs, ping-pong register buffers: the next
+            // superset's states and factors load under this one's FMAs
             double ya[NLO], ba[NLO], yb2[NLO], bb[NLO];
             load(0, 0, ya, ba);
             if (units == 1) {
