@@ -156,14 +156,25 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
     const double *src = a.mode && a.loss ? srcv + (size_t)id * N : nullptr;
     const double Kpc = a.mode && !a.loss ? K : 1.0;
     // pC for every (j, k), k not in j: dieoff.c:78 (c S) K, loss.c:98 c (S + src Ks)
-    for (uint32_t i = tid; i < (uint32_t)(NS * N); i += kScnBlock) {
-        const uint32_t j = i / N, k = i - j * N;
-        double v = 0.0;
-        if (!((j >> (N - 1 - k)) & 1u)) {
-            v = src ? c * (S[i] + src[k] * K) : c * S[i] * Kpc;
-            v = v > 1.0 ? 1.0 : v;
+    {  // every S (and source) load of the thread in flight before the first store
+        constexpr int kPC = (NS * N + kScnBlock - 1) / kScnBlock;
+        double sv[kPC], sr[kPC];
+#pragma unroll
+        for (int u = 0; u < kPC; ++u) {
+            const uint32_t i = tid + u * kScnBlock, ii = i < (uint32_t)(NS * N) ? i : 0u;
+            sv[u] = S[ii];
+            sr[u] = src ? src[ii % N] : 0.0;
         }
-        pc[i] = v;
+#pragma unroll
+        for (int u = 0; u < kPC; ++u) {
+            const uint32_t i = tid + u * kScnBlock, j = i / N, k = i - j * N;
+            double v = 0.0;
+            if (!((j >> (N - 1 - k)) & 1u)) {
+                v = src ? c * (sv[u] + sr[u] * K) : c * sv[u] * Kpc;
+                v = v > 1.0 ? 1.0 : v;
+            }
+            if (i < (uint32_t)(NS * N)) pc[i] = v;
+        }
     }
     if (tid < (uint32_t)kE) {
         const double x = e0 + tid < a.ne ? ev[e0 + tid] : 0.0;
@@ -207,10 +218,25 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
         }
     }
     if (tid < (uint32_t)NLO) Bt[a.btot + tid] = 0.0;  // zero block (upper half, no free hi bit)
-    // initial states
-    for (uint32_t i = tid; i < (uint32_t)(NS * kE); i += kScnBlock) {
-        const uint32_t x = i / kE, le = i % kE, st = ((x % NHI) << NL) | (x / NHI);
-        y[(x / NHI) * LS + (x % NHI) * kE + le] = a.mode ? (e0 + le < a.ne ? y0src[((size_t)ic * NS + st) * a.ne + e0 + le] : 0.0) : y0src[st];
+    // initial states: every load of the thread issued (unconditionally, to
+    // a valid address) before the first LDS store, one global round trip
+    {
+        constexpr int kIS = (NS * kE + kScnBlock - 1) / kScnBlock;
+        double t0[kIS];
+#pragma unroll
+        for (int u = 0; u < kIS; ++u) {
+            const uint32_t i = tid + u * kScnBlock, x = (i / kE) % NS, le = i % kE;
+            const uint32_t st = ((x % NHI) << NL) | (x / NHI);
+            const bool ok = !a.mode || e0 + le < a.ne;
+            const size_t idx = a.mode ? ((size_t)ic * NS + st) * a.ne + e0 + le : st;
+            const double v = y0src[ok ? idx : 0];
+            t0[u] = ok ? v : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kIS; ++u) {
+            const uint32_t i = tid + u * kScnBlock, x = i / kE, le = i % kE;
+            if (i < (uint32_t)(NS * kE)) y[(x / NHI) * LS + (x % NHI) * kE + le] = t0[u];
+        }
     }
     __syncthreads();
     const uint32_t w = tid / 64, g = (tid >> 5) & 1u, le = tid & 31u;
