@@ -8,7 +8,9 @@
  *
  * Conventions
  *  - plain pointers and sizes only; no torch / HIP types in signatures
- *    (streams are passed as void*, i.e. a hipStream_t or NULL);
+ *    (streams are passed as void*, i.e. a hipStream_t; it is used exactly as
+ *    given, so NULL is HIP's null stream -- the stream torch's default
+ *    `torch.cuda.current_stream().cuda_stream == 0` names);
  *  - every int-returning function returns MDP_OK (0) or a negative MDP_E*
  *    code; the reason is in mdp_last_error() (thread-local).  Nothing aborts
  *    or exits across the ABI;
@@ -34,7 +36,7 @@ extern "C" {
 #define MDP_ENODEV (-5)       /* no usable GPU                             */
 #define MDP_EUNSUPPORTED (-6) /* problem outside the engine's limits       */
 
-#define MDP_ABI_VERSION 3
+#define MDP_ABI_VERSION 4
 
 /* ------------------------------------------------------------------ */
 /* Host model: parse + state enumeration (the reference's L2 layer)    */
@@ -118,7 +120,7 @@ int mdp_loglik_grid(mdp_engine *engine, const double *e, uint32_t ne, const doub
 
 /* Device-resident variant for single-device engines (one process per GPU):
  * upload the grid once, then compute into caller-owned device memory
- * d_out[ie*ld_out + ic] on `stream` (hipStream_t, NULL = engine stream).
+ * d_out[ie*ld_out + ic] on `stream` (hipStream_t; NULL = HIP's null stream).
  * mdp_engine_run is asynchronous w.r.t. the host. */
 int mdp_engine_set_grid(mdp_engine *engine, const double *e, uint32_t ne, const double *c,
                         uint32_t nc);
@@ -231,9 +233,15 @@ void mdp_future_destroy(mdp_future *future);
 int mdp_future_simulate(mdp_future *future, uint64_t seed, uint64_t rep0, uint64_t nrep, uint32_t tfut,
                         uint64_t *counts);
 /* Same into caller-owned device memory d_counts[tfut] (overwritten, not
- * accumulated) on `stream` (NULL = engine stream); asynchronous. */
+ * accumulated) on `stream` (NULL = HIP's null stream); asynchronous.  A
+ * replicate whose posterior draw needs more look-back than the engine holds
+ * raises a device error flag (cleared by each call in stream order);
+ * mdp_future_check waits for `stream` and returns MDP_EUNSUPPORTED when it
+ * is set -- the counts of those launches are then not valid (the host form
+ * mdp_future_simulate does this check itself). */
 int mdp_future_simulate_device(mdp_future *future, uint64_t seed, uint64_t rep0, uint64_t nrep, uint32_t tfut,
                                uint64_t *d_counts, void *stream);
+int mdp_future_check(mdp_future *future, void *stream);
 /* Mean duration (ms) of the simulation kernel over `reps` back-to-back
  * launches of replicates [0, nrep) between two events. */
 int mdp_future_time_kernel(mdp_future *future, uint64_t seed, uint64_t nrep, uint32_t tfut, int reps, double *ms);
@@ -243,7 +251,7 @@ int mdp_future_philox(uint64_t key, const uint32_t *ctr, uint32_t *out);
 /* Device-resident form of mdp_scenario_lik (one process per GPU): upload the
  * grid once (set_grid; ts, tdis and the axes as above), then compute into
  * caller-owned device memory d_out[ne*nc*nK*nd] (same layout) on `stream`
- * (NULL = the scenario's stream), asynchronously.  time_kernels: ms[0] =
+ * (NULL = HIP's null stream), asynchronously.  time_kernels: ms[0] =
  * mean duration of the v = P^tdis w kernel, ms[1] = of the PK^ts kernel,
  * each launched `reps` times back to back between two events. */
 int mdp_scenario_set_grid(mdp_scenario *scenario, int ts, int tdis, const double *e, uint32_t ne, const double *c,

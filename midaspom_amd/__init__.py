@@ -172,11 +172,11 @@ class Engine:
         check(lib().mdp_engine_set_grid(self._h, _dptr(e), e.size, _dptr(c), c.size))
         self.ne, self.nc = e.size, c.size
 
-    def run(self, d_out: int, ld_out: int, stream: int | None = None) -> None:
+    def run(self, d_out: int, ld_out: int, stream: int = 0) -> None:
         """Compute into device memory at address ``d_out`` (e.g. a torch
-        tensor's data_ptr()) on hipStream ``stream`` (None = engine stream)."""
-        check(lib().mdp_engine_run(self._h, ctypes.c_void_p(d_out), ld_out,
-                                   ctypes.c_void_p(stream) if stream else None))
+        tensor's data_ptr()) on hipStream ``stream``, used as given: 0 is
+        HIP's null stream, which is torch's default stream."""
+        check(lib().mdp_engine_run(self._h, ctypes.c_void_p(d_out), ld_out, ctypes.c_void_p(stream)))
 
     def set_profiling(self, on: bool = True) -> None:
         check(lib().mdp_engine_set_profiling(self._h, int(bool(on))))
@@ -344,15 +344,15 @@ class Scenario:
         self.shape = shape
         return shape
 
-    def run(self, d_out: int, stream: int | None = None) -> None:
+    def run(self, d_out: int, stream: int = 0) -> None:
         """Compute the set grid into device memory at ``d_out`` (float64, the
-        set_grid shape), asynchronously on hipStream ``stream``."""
-        check(lib().mdp_scenario_run(self._h, ctypes.c_void_p(d_out), ctypes.c_void_p(stream) if stream else None))
+        set_grid shape), asynchronously on hipStream ``stream`` (0 = HIP's
+        null stream, torch's default)."""
+        check(lib().mdp_scenario_run(self._h, ctypes.c_void_p(d_out), ctypes.c_void_p(stream)))
 
-    def time_kernels(self, d_out: int, stream: int | None = None, reps: int = 10) -> dict:
+    def time_kernels(self, d_out: int, stream: int = 0, reps: int = 10) -> dict:
         ms = (ctypes.c_double * 2)()
-        check(lib().mdp_scenario_time_kernels(self._h, ctypes.c_void_p(d_out),
-                                              ctypes.c_void_p(stream) if stream else None, reps, ms))
+        check(lib().mdp_scenario_time_kernels(self._h, ctypes.c_void_p(d_out), ctypes.c_void_p(stream), reps, ms))
         return {"k_scn_v": ms[0], "k_scn_lik": ms[1]}
 
 
@@ -423,10 +423,17 @@ class Future:
         return counts
 
     def simulate_device(self, d_counts: int, nrep: int, tfut: int, seed: int = 0, rep0: int = 0,
-                        stream: int | None = None) -> None:
-        """Into device memory at ``d_counts`` (uint64[tfut]), asynchronously."""
+                        stream: int = 0) -> None:
+        """Into device memory at ``d_counts`` (uint64[tfut]), asynchronously
+        on hipStream ``stream`` (0 = HIP's null stream, torch's default).
+        Call check() before trusting the counts."""
         check(lib().mdp_future_simulate_device(self._h, seed, rep0, nrep, tfut, ctypes.c_void_p(d_counts),
-                                               ctypes.c_void_p(stream) if stream else None))
+                                               ctypes.c_void_p(stream)))
+
+    def check(self, stream: int = 0) -> None:
+        """Wait for ``stream``; raise if a device launch since the last
+        simulate_device on it overflowed the posterior look-back."""
+        check(lib().mdp_future_check(self._h, ctypes.c_void_p(stream)))
 
     def time_kernel(self, nrep: int, tfut: int, seed: int = 0, reps: int = 10) -> float:
         ms = ctypes.c_double()

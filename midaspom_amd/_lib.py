@@ -133,6 +133,7 @@ SIGNATURES = [
     ("mdp_future_simulate_device", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
       ctypes.c_void_p]),
+    ("mdp_future_check", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     ("mdp_future_time_kernel", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, c_dbl_p]),
     ("mdp_future_philox", ctypes.c_int,

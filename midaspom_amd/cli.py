@@ -33,13 +33,15 @@ def parse_args(argv):
     return ap.parse_args(argv)
 
 
-def _print_problem(model, out):
+def _print_problem(model, out, mpi=False):
     pb = model
     out(f"Number of habitat patches: {pb.n}\nNumber of sampled years: {pb.tmax}\n")
     out("Dispersal matrix:\n")
     M = pb.M
     for i in range(pb.n):
         out("".join(f"{M[i, j]:.3f} " for j in range(pb.n)) + "\n")
+    if mpi:  # every rank, right after its state enumeration (main_MIDASPOM_MPI.c:301)
+        out(f"nextid={pb.nextid}\n", all_ranks=True)
     out("Input occupancy data:\n")
     obs = pb.obs
     for t in range(pb.tmax):
@@ -65,8 +67,9 @@ def main(argv=None) -> int:
             sys.stdout.write(text)
             sys.stdout.flush()
 
-    if world > 1:
-        out("------ MIDASPOM, beta MPI version ------\n-> N. Alcala, E. M. Cole, and N. A. Rosenberg <-\n")
+    if world > 1:  # unguarded in the MPI build: every rank prints it (:78)
+        out("------ MIDASPOM, beta MPI version ------\n-> N. Alcala, E. M. Cole, and N. A. Rosenberg <-\n",
+            all_ranks=True)
     else:
         out("------ MIDASPOM, beta version ------\n-> N. Alcala, E. M. Cole, and N. A. Rosenberg <-\n")
     if a.s < 2:
@@ -82,7 +85,7 @@ def main(argv=None) -> int:
         sys.stderr.write(f"\nmidaspom: {exc}\n")
         return 2
     out("done\n")
-    _print_problem(model, out)
+    _print_problem(model, out, mpi=world > 1)
     start = time.time()
 
     if world == 1:
@@ -97,15 +100,15 @@ def main(argv=None) -> int:
         import torch.distributed as dist
 
         backend = a.backend or "nccl"
+        # one process per GPU; a rehearsal backend may run more ranks than
+        # GPUs (ranks then share devices round-robin)
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
         if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            compute = mdist.gpu_slab_compute(model, local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
-            torch.cuda.set_device(local)
             dist.init_process_group(backend)
-            compute = mdist.gpu_slab_compute(model, local)
-        out(f"nextid={model.nextid}\n", all_ranks=True)
+        compute = mdist.gpu_slab_compute(model, dev)
         out(f"Starting parallel likelihood computation process {rank + 1}/{world}\n", all_ranks=True)
         r0, r1 = mdist.row_slab(rank, world, a.s)
         local_lik = compute(g[r0:r1], g)
@@ -124,14 +127,22 @@ def main(argv=None) -> int:
         if not root:
             return 0
 
-    ltot = mdp.log_total(lik, win)
-    out(f"Total log-likelihood={ltot:.5f}\n")
-    out(f"Writing output in file {a.o}... ")
-    # the MPI build writes raw log-likelihoods when Ltot == 0 (:527)
-    mdp.write_posterior(a.o, lik, ltot, raw=(world > 1 and ltot == 0))
+    finish(lik, win, a.o, world, out)
     elapsed = int(time.time()) - int(start)
     out(f"done\n Total running time: {elapsed / 60.0:.2f} min\n")
     return 0
+
+
+def finish(lik, win, path, world, out):
+    """Normalise and write (main_MIDASPOM.c:413-436); the MPI build writes
+    raw log-likelihoods instead when Ltot == 0 (main_MIDASPOM_MPI.c:527)."""
+    import midaspom_amd as mdp
+
+    ltot = mdp.log_total(lik, win)
+    out(f"Total log-likelihood={ltot:.5f}\n")
+    out(f"Writing output in file {path}... ")
+    mdp.write_posterior(path, lik, ltot, raw=(world > 1 and ltot == 0))
+    return ltot
 
 
 if __name__ == "__main__":

@@ -1767,7 +1767,6 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
             // compile the variant a small grid uses now (the other on demand)
             if (const char *fv = getenv("MDP_FUSED")) eng->fused_mode = atoi(fv) != 0;
-            if (const char *gv = getenv("MDP_JIT_GLDS")) plan.glds = atoi(gv) != 0;
             if (const char *cv = getenv("MDP_FUSED_COLS")) plan.fused_cols = std::max(1, std::min(4, atoi(cv)));
             plan.nj = eng->nj;
             plan.nvar = eng->nvar;
@@ -1848,8 +1847,9 @@ int mdp_engine_run(mdp_engine *eng, double *d_out, uint32_t ld_out, void *stream
         return mdp_set_error(MDP_EINVAL, "mdp_engine_run needs a single-device engine");
     DevCtx &d = eng->devs[0];
     if (ld_out < d.nc) return mdp_set_error(MDP_EINVAL, "ld_out %u < nc %u", ld_out, d.nc);
-    hipStream_t s = stream ? (hipStream_t)stream : d.stream;
-    return run_dev(eng, d, d_out, ld_out, s);
+    // the caller's stream as given: NULL is HIP's null stream (torch's default
+    // stream), never the engine's private non-blocking stream
+    return run_dev(eng, d, d_out, ld_out, (hipStream_t)stream);
 }
 
 int mdp_loglik_grid(mdp_engine *eng, const double *e, uint32_t ne, const double *c, uint32_t nc,
@@ -1975,7 +1975,7 @@ int mdp_engine_time_kernels(mdp_engine *eng, double *d_out, uint32_t ld_out, voi
     double t[3];
     const int saved = eng->profiling;
     eng->profiling = 0;
-    int rc = time_kernels(eng, d, d_out, ld_out, stream ? (hipStream_t)stream : d.stream, reps, t);
+    int rc = time_kernels(eng, d, d_out, ld_out, (hipStream_t)stream, reps, t);
     eng->profiling = saved;
     if (rc) return rc;
     const int k = std::min(max_k, 3);

@@ -503,9 +503,28 @@ int mdp_future_simulate_device(mdp_future *f, uint64_t seed, uint64_t rep0, uint
     if (rc) return rc;
     if (!d_counts) return mdp_set_error(MDP_EINVAL, "null device counts");
     FUT_TRY(hipSetDevice(f->device));
-    hipStream_t st = stream ? (hipStream_t)stream : f->stream;
+    hipStream_t st = (hipStream_t)stream;  // as given: NULL is HIP's null stream
     if ((rc = fut_reserve(f, fut_grid(nrep), tfut))) return rc;
+    // the look-back overflow flag is cleared in stream order, so
+    // mdp_future_check reports exactly the launches since this one
+    FUT_TRY(hipMemsetAsync(f->derr, 0, sizeof(uint32_t), st));
     return fut_launch(f, seed, rep0, nrep, tfut, (unsigned long long *)d_counts, st, true);
+}
+
+int mdp_future_check(mdp_future *f, void *stream)
+{
+    if (!f) return mdp_set_error(MDP_EINVAL, "null future engine");
+    FUT_TRY(hipSetDevice(f->device));
+    hipStream_t st = (hipStream_t)stream;
+    uint32_t err = 0;
+    FUT_TRY(hipMemcpyAsync(&err, f->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    FUT_TRY(hipStreamSynchronize(st));
+    if (err)
+        return mdp_set_error(MDP_EUNSUPPORTED,
+                             "a posterior draw needed more than %u look-back replicates (posterior mass far "
+                             "below the (necstep-1)^2 scale): the device counts are not valid",
+                             kLookBack);
+    return MDP_OK;
 }
 
 int mdp_future_simulate(mdp_future *f, uint64_t seed, uint64_t rep0, uint64_t nrep, uint32_t tfut,

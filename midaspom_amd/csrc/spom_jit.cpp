@@ -208,8 +208,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         // the k_qrows phases for this one c value (spom_engine.hip k_qrows):
         // Z per hidden-state row, Pc per item, Q per entry -- all in LDS.
         // The column tables (host-built, 1 KiB-padded: var-column S, items,
-        // CSR, then zs as [k/2][row][k%2]) are copied to LDS through registers
-        // (or global_load_lds_dwordx4 with MDP_JIT_GLDS), all in flight, one barrier.
+        // CSR, then zs as [k/2][row][k%2]) are copied to LDS through registers,
+        // all in flight, one barrier.
         o << "    extern __shared__ __attribute__((aligned(16))) double ct[];\n"
              "    __shared__ double Zl[FC * NJ];\n"
              "    __shared__ double Pl[FC * NITEMS];\n"
@@ -221,13 +221,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    double cc[FC];\n"
              "#pragma unroll\n"
              "    for (int f = 0; f < FC; ++f) cc[f] = ic0 + f < nc ? cvals[ic0 + f] : 0.0;\n"
-          << (pl.glds ?
-             "    {\n"
-             "        typedef __attribute__((address_space(3))) void lds_void;\n"
-             "        const u32 w = threadIdx.x >> 6, l = threadIdx.x & 63;\n"
-             "        for (u32 i = w * 128; i < ct_len; i += NT * 2)\n"
-             "            __builtin_amdgcn_global_load_lds((const void *)(coltab + i + 2 * l), (lds_void *)(ct + i), 16, 0, 0);\n"
-             "    }\n" :
+          <<
              "    {\n"
              "        const double2 *src = (const double2 *)coltab;\n"
              "        double2 *dst = (double2 *)ct;\n"
@@ -245,7 +239,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              // loads are not sunk into per-load branches (load, wait, store x NSTG)
              "            dst[i < n2 ? i : n2] = t[k];\n"
              "        }\n"
-             "    }\n") <<
+             "    }\n"
              "    __syncthreads();\n"
           << stamp(4) <<
              // operands of the Pc and Q phases that do not depend on Z, read

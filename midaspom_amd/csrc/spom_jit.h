@@ -22,7 +22,6 @@ struct MdpJitPlan {
     // with one DMA per wave the staged image was intermittently wrong after
     // vmcnt(0) + barrier (config-1 input; correct with >= 2 DMAs per wave),
     // root cause not found -- register staging is the validated default
-    bool glds = false;
     uint32_t kzmax = 0;    // bound on the zs rows of any grid: n - nvar rounded up to 8
     bool zpad = false;     // the fused image always holds kzmax zs rows (zero past kmax)
     uint32_t qmaxlen = 0;  // most items of one Q entry

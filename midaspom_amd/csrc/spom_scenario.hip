@@ -687,7 +687,7 @@ int mdp_scenario_run(mdp_scenario *sc, double *d_out, void *stream)
     if (!sc->ne) return MDP_OK;
     if (!d_out) return mdp_set_error(MDP_EINVAL, "null device output");
     SCN_TRY(hipSetDevice(sc->device));
-    return scn_launch(sc, d_out, stream ? (hipStream_t)stream : sc->stream, 3);
+    return scn_launch(sc, d_out, (hipStream_t)stream, 3);
 }
 
 int mdp_scenario_time_kernels(mdp_scenario *sc, double *d_out, void *stream, int reps, double *ms)
@@ -695,7 +695,7 @@ int mdp_scenario_time_kernels(mdp_scenario *sc, double *d_out, void *stream, int
     if (!sc || !ms || reps <= 0) return mdp_set_error(MDP_EINVAL, "bad timing request");
     if (!sc->ne) return mdp_set_error(MDP_EINVAL, "no grid set");
     SCN_TRY(hipSetDevice(sc->device));
-    hipStream_t st = stream ? (hipStream_t)stream : sc->stream;
+    hipStream_t st = (hipStream_t)stream;
     if (!sc->ev0) SCN_TRY(hipEventCreate(&sc->ev0));
     if (!sc->ev1) SCN_TRY(hipEventCreate(&sc->ev1));
     int rc = scn_launch(sc, d_out, st, 3);

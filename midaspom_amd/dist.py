@@ -130,8 +130,9 @@ def gpu_future_compute(fut, tfut: int, seed: int, device_index: int):
     def compute(rep0, nrep):
         out = torch.zeros(tfut, dtype=torch.int64, device=f"cuda:{device_index}")
         if nrep:
-            fut.simulate_device(out.data_ptr(), nrep, tfut, seed=seed, rep0=rep0,
-                                stream=torch.cuda.current_stream(device_index).cuda_stream)
+            st = torch.cuda.current_stream(device_index).cuda_stream
+            fut.simulate_device(out.data_ptr(), nrep, tfut, seed=seed, rep0=rep0, stream=st)
+            fut.check(st)  # raises if a draw overflowed the posterior look-back
         return out
 
     return compute

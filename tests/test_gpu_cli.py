@@ -1,0 +1,84 @@
+"""The command-line drop-ins run end to end: `python -m midaspom_amd` against
+the compiled `midaspom` (MIDASPOM.out drop-in), and the torchrun form that
+replaces `mpirun -np N MIDASPOM_MPI.out` (main_MIDASPOM_MPI.c:78,301,356,463,
+479,484-506).  The torchrun test uses the gloo backend with both ranks on
+cuda:0 (the launcher starts the rank processes before any GPU call); its
+posterior file must equal the single-process file byte for byte (grid points
+are independent, so the slab partition does not change a bit).  Nothing here
+calls torch.cuda.synchronize(): the slab -> gather ordering is the engine's
+stream contract."""
+from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from midaspom_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FLAGS = ["-m", "400", "-d", "100", "-s", "101"]
+
+
+def _env():
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return env
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _strip_time(text):
+    return [ln for ln in text.splitlines() if "Total running time" not in ln]
+
+
+def test_python_cli_matches_compiled_cli(golden, tmp_path):
+    a, b = tmp_path / "py.txt", tmp_path / "c.txt"
+    inp = str(golden / "occupancies.txt")
+    rp = subprocess.run([sys.executable, "-m", "midaspom_amd", *FLAGS, "-i", inp, "-o", str(a)],
+                        capture_output=True, text=True, timeout=180, env=_env(), cwd=ROOT)
+    assert rp.returncode == 0, rp.stderr
+    rc = subprocess.run([str(_lib.CLI_PATH), *FLAGS, "-i", inp, "-o", str(b)],
+                        capture_output=True, text=True, timeout=180)
+    assert rc.returncode == 0, rc.stderr
+    assert a.read_bytes() == b.read_bytes()
+    assert _strip_time(rp.stdout) == _strip_time(rc.stdout)
+    assert "Total log-likelihood=-39.34251" in rp.stdout
+
+
+def test_torchrun_cli_two_ranks(golden, tmp_path):
+    single, multi = tmp_path / "single.txt", tmp_path / "multi.txt"
+    inp = str(golden / "occupancies.txt")
+    r1 = subprocess.run([sys.executable, "-m", "midaspom_amd", *FLAGS, "-i", inp, "-o", str(single)],
+                        capture_output=True, text=True, timeout=180, env=_env(), cwd=ROOT)
+    assert r1.returncode == 0, r1.stderr
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "midaspom_amd", "--backend", "gloo", *FLAGS, "-i", inp, "-o", str(multi)]
+    r2 = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    assert multi.read_bytes() == single.read_bytes()
+    out = r2.stdout
+    # unguarded lines: once per rank (:78, :301, :356, :479)
+    assert out.count("------ MIDASPOM, beta MPI version ------") == 2
+    assert out.count("nextid=40\n") == 2
+    for r in (1, 2):
+        assert f"Starting parallel likelihood computation process {r}/2\n" in out
+        assert f"end likelihood computation process {r}/2\n" in out
+    # send / gather lines (:484-506); root-only progress over its 51 rows (:463)
+    assert "Sending data (proc 1)... " in out and "Gathering data from 1 proc... " in out
+    assert out.count("done\n") >= 4
+    assert sum(1 for ln in out.splitlines() if ln.endswith("% done")) == 51
+    assert out.count("Dispersal matrix:") == 1 and out.count("Total log-likelihood=-39.34251") == 1
+    # per-rank order: nextid comes after the dispersal matrix, before the data dump
+    i_disp, i_obs = out.index("Dispersal matrix:"), out.index("Input occupancy data:")
+    assert i_disp < out.index("nextid=40") < i_obs

@@ -334,7 +334,7 @@ def test_config1_after_other_kernels(golden):
     """Stale LDS / device memory from earlier kernels must not leak into the
     result: the scenario engine (154 KB of LDS per workgroup) runs first, then
     the config-1 grid (n = nvar = 8, no always-zero column) is checked.  This
-    caught a staging race of the global_load_lds variant (now off by default)."""
+    caught a staging race of a global_load_lds staging variant (since removed)."""
     row = mdp.first_row(golden / "occupancies.txt")
     with mdp.Scenario(row, "dieoff", m=400, d=100) as sc:
         sc.lik(np.linspace(0.0, 1.0, 64), np.array([0.3, 0.7]), mdp.kgrid(4), ts=5, tdis=3)

@@ -145,3 +145,41 @@ def test_device_resident_run_matches_host(golden, kind):
         assert ms["k_scn_v"] > 0 and ms["k_scn_lik"] > 0
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy(), host)
+
+
+def test_config4_full_workload(golden):
+    """BASELINE config 4 at its workload: examples/input row 1 (n = 8), e and c
+    = grid(256) on [0, 1], K = kgrid(256, 0.1, 100), ts = 20, tdis = 10 --
+    the call bench.py --config 4 times (main_MIDASPOM_dieoff.c:307-351 for
+    every (e, c, K)).  All 256^3 values finite and >= 0; the 8 (e, c, K)
+    corners and 64 random (e, c) pairs x 8 K each against the oracle (one
+    oracle call per (e, c), so its P^tdis is shared by the K values; the
+    calls run on a thread pool -- the C oracle releases the GIL)."""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+    s, ts, tdis = 256, 20, 10
+    row = mdp.first_row(golden / "occupancies.txt")
+    g, _ = mdp.grid(s, 0.0, 1.0)
+    K = mdp.kgrid(s, 0.1, 100.0)
+    with mdp.Scenario(row, "dieoff", m=400.0, d=100.0) as sc:
+        shape = sc.set_grid(g, g, K, ts=ts, tdis=tdis)
+        assert shape == (s, s, s)
+        out = torch.empty(shape, dtype=torch.float64, device="cuda:0")
+        sc.run(out.data_ptr())
+        lik = out.cpu().numpy()  # ordered after the kernel: both on the null stream
+    assert np.isfinite(lik).all() and (lik >= 0).all()
+    rng = np.random.default_rng(4)
+    jobs = [(ie, ic, np.array([0, s - 1])) for ie in (0, s - 1) for ic in (0, s - 1)]
+    for ie, ic in zip(rng.integers(0, s, 64), rng.integers(0, s, 64)):
+        jobs.append((int(ie), int(ic), np.sort(rng.choice(s, size=8, replace=False))))
+
+    def ref(job):
+        ie, ic, iK = job
+        return oracle.dieoff_lik(row, K[iK], g[ie], g[ic], ts=ts, tdis=tdis, m=400.0, d=100.0)
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        refs = list(ex.map(ref, jobs))
+    got = np.concatenate([lik[ie, ic, iK] for ie, ic, iK in jobs])
+    close(got, np.concatenate(refs))
