@@ -847,6 +847,140 @@ __global__ __launch_bounds__(kBlock) void k_forward_lds(
 }
 
 // ---------------------------------------------------------------------------
+// wide path: years with more observed states than the register-resident
+// forward kernels hold (npmax > 16, i.e. more than 4 missing patches in one
+// year; main_MIDASPOM.c:225-251 expands 2^k states for any k and propagates
+// them with dgemm, :371-384).  Same direct-path algebra (Q per (X, B) group,
+// DESIGN.md §3), but nothing has to fit a workgroup: the item factors and Q
+// rows go through HBM/L2, and the state vectors live in an HBM scratch laid
+// out [state][point] so every lane's access is coalesced.
+// ---------------------------------------------------------------------------
+
+// Pg[cl][it] = Pc[j][B] of item `it` at c = cvals[c0 + cl]: Z_row(c) times the
+// var-column factors f_b = B_b ? pC_b : 1 - pC_b, pC_b = min(1, c S[j][b])
+// (1.0 for the columns of j, marked -1 in sv), combined in k_qrows' pairwise
+// tree over NV slots -- the same bits k_qrows produces.
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_witems(const double *__restrict__ cvals, uint32_t nc, uint32_t c0,
+                                                   uint32_t nvar, const double *__restrict__ Zg,
+                                                   const double *__restrict__ sv, uint32_t nitems,
+                                                   const uint2 *__restrict__ items, double *__restrict__ Pg)
+{
+    const uint32_t it = blockIdx.x * kBlock + threadIdx.x, cl = blockIdx.y;
+    if (it >= nitems) return;
+    const double c = cvals[c0 + cl];
+    const uint2 t = items[it];
+    const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), nB = ~t.x;
+    double f[NV];
+#pragma unroll
+    for (int b = 0; b < NV; ++b) {
+        const double sb = (uint32_t)b < nvar ? sv[(size_t)r * nvar + b] : -1.0;
+        double pcv = c * sb;
+        pcv = pcv > 1.0 ? 1.0 : pcv;
+        const double p = sb < 0.0 ? 1.0 : pcv;
+        const uint32_t nbit = (uint32_t)b < nvar ? (nB >> (nvar - 1 - (uint32_t)b)) & 1u : 0u;
+        const double sg = __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
+        const double nb = __hiloint2double((int)(nbit * 0x3ff00000u), 0);
+        f[b] = fma(sg, p, nb);
+    }
+#pragma unroll
+    for (int sh = 1; sh < NV; sh *= 2)
+#pragma unroll
+        for (int b = 0; b + sh < NV; b += 2 * sh) f[b] *= f[b + sh];
+    Pg[(size_t)cl * nitems + it] = Zg[(size_t)r * nc + c0 + cl] * f[0];
+}
+
+// Q[c0 + cl][q] = the q-th entry's items summed in CSR (ascending j) order,
+// as k_qrows sums them; zero in the padding slots up to ldQ.
+__global__ __launch_bounds__(kBlock) void k_wq(uint32_t c0, uint32_t nitems, const double *__restrict__ Pg,
+                                               uint32_t ncoef, const uint32_t *__restrict__ qstart,
+                                               const uint32_t *__restrict__ qitem, double *__restrict__ Q,
+                                               uint32_t ldQ)
+{
+    const uint32_t q = blockIdx.x * kBlock + threadIdx.x, cl = blockIdx.y;
+    if (q >= ldQ) return;
+    double a = 0.0;
+    if (q < ncoef) {
+        const double *pl = Pg + (size_t)cl * nitems;
+        const uint32_t i1 = qstart[q + 1];
+        for (uint32_t i = qstart[q]; i < i1; ++i) a = a + pl[qitem[i]];
+    }
+    Q[(size_t)(c0 + cl) * ldQ + q] = a;
+}
+
+typedef const __attribute__((address_space(4))) uint32_t cuint;
+
+// Forward recursion with the state vectors in HBM: lane per e value, one c
+// per workgroup row (blockIdx.y = c0 + row).  Year t's vector is formed
+// kWideLB target states at a time, each source state's probability loaded
+// once per block of targets; a transition's coefficients (its group's Q
+// entries) and its use descriptor are wave-uniform scalar loads.  The weight
+// x^(|A|-m) y^m is xp[|A|-m] yp[m] from per-lane power tables in LDS.  Q3
+// semantics (:368-369, :386-392): ones over the year-0 states, L = prior0 sum v.
+constexpr uint32_t kWideLB = 4;
+__global__ __launch_bounds__(kBlock) void k_fwd_wide(
+    const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ udesc,
+    const uint32_t *__restrict__ np, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
+    uint32_t c0, uint32_t maxA, double *__restrict__ V, uint32_t npmax, double *__restrict__ out, uint32_t ld_out)
+{
+    extern __shared__ double xy[];  // [2][maxA + 1][kBlock]: x^r, y^r per lane
+    const uint32_t ie = blockIdx.x * kBlock + threadIdx.x, cl = blockIdx.y, ic = c0 + cl;
+    const double e = ie < ne ? evals[ie] : 0.0;
+    const double x = e > 1.0 ? 1.0 : e, y = 1.0 - x;
+    double *xp = xy + threadIdx.x, *yp = xy + (size_t)(maxA + 1) * kBlock + threadIdx.x;
+    {
+        double a = 1.0, b = 1.0;
+        for (uint32_t r = 0; r <= maxA; ++r) {
+            xp[r * kBlock] = a;
+            yp[r * kBlock] = b;
+            a *= x;
+            b *= y;
+        }
+    }
+    cdouble *q = (cdouble *)(Q + (size_t)ic * ldQ);
+    cuint *ud = (cuint *)udesc;
+    cuint *npc_ = (cuint *)np;
+    // V[buf][state][row][lane]: rows of this launch x the padded e extent
+    const size_t cs = (size_t)gridDim.y * gridDim.x * kBlock;  // one state's stride
+    double *va = V + (size_t)cl * gridDim.x * kBlock + ie;
+    double *vb = va + (size_t)npmax * cs;
+    const uint32_t np0 = npc_[0];
+    for (uint32_t k = 0; k < np0; ++k) va[k * cs] = 1.0;
+    uint32_t ubase = 0, npp = np0;
+    for (uint32_t t = 1; t < tmax; ++t) {
+        const uint32_t npc = npc_[t];
+        for (uint32_t l0 = 0; l0 < npc; l0 += kWideLB) {
+            double acc[kWideLB];
+#pragma unroll
+            for (uint32_t i = 0; i < kWideLB; ++i) acc[i] = 0.0;
+            for (uint32_t k = 0; k < npp; ++k) {
+                const double vk = va[k * cs];
+#pragma unroll
+                for (uint32_t i = 0; i < kWideLB; ++i) {
+                    if (l0 + i >= npc) break;
+                    const uint32_t d = ud[ubase + (l0 + i) * npp + k];
+                    const uint32_t off = d & kOffMask, nX = (d >> kOffBits) & 31u, nA = d >> 27;
+                    double P = 0.0;
+                    for (uint32_t m = 0; m <= nX; ++m) P = fma(q[off + m], xp[(nA - m) * kBlock] * yp[m * kBlock], P);
+                    acc[i] = fma(vk, P, acc[i]);
+                }
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < kWideLB; ++i)
+                if (l0 + i < npc) vb[(l0 + i) * cs] = acc[i];
+        }
+        ubase += npp * npc;
+        npp = npc;
+        double *tmp = va;
+        va = vb;
+        vb = tmp;
+    }
+    double L = 0.0;
+    for (uint32_t l = 0; l < npp; ++l) L += va[l * cs] * prior0;
+    if (ie < ne) out[(size_t)ie * ld_out + ic] = log(L);
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 
@@ -885,8 +1019,9 @@ int dev_reserve(T **p, size_t *cap, size_t count)
 }
 
 constexpr int kNumEv = 6;  // start/stop per kernel: k_zpv, k_coefs, k_forward
-const char *const kKernelNames[2][3] = {{"k_zpv", "k_coefs", "k_forward"},
-                                        {"k_zrows", "k_qrows", "k_forward"}};
+const char *const kKernelNames[3][3] = {{"k_zpv", "k_coefs", "k_forward"},
+                                        {"k_zrows", "k_qrows", "k_forward"},
+                                        {"k_zrows", "k_wq", "k_forward"}};
 
 struct DevCtx {
     int device = 0;
@@ -919,6 +1054,11 @@ struct DevCtx {
     hipModule_t jit_mod[2] = {nullptr, nullptr};  // problem-specialised forward kernel [fused]
     hipFunction_t jit_fn[2] = {nullptr, nullptr};
     bool fused = false;  // this grid runs the fused forward kernel (no k_qrows)
+    // wide path: per-chunk item factors, state-vector scratch, tables
+    double *Pg = nullptr, *V = nullptr;
+    size_t cap_pg = 0, cap_v = 0;
+    uint32_t *np_d = nullptr, *udesc_w = nullptr;
+    uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     std::vector<uint8_t> ev_mask;  // per profiled run: slots whose kernel was launched
     size_t ev_used = 0;          // event sets recorded since the last collect
@@ -938,6 +1078,8 @@ struct mdp_engine {
     bool lds_part = true;     // k_coefs keeps subset partial sums in LDS
     bool diag = false;        // MDP_DIAG: record phase stamps
     bool jit = false;         // forward kernel specialised with hipRTC (spom_jit.cpp)
+    bool wide = false;        // wide path (k_witems + k_wq + k_fwd_wide): npmax > 16 or MDP_WIDE=1
+    double wide_flops_pt = 0; // its FP64 flops per grid point
     int jit_epl = 1;          // its grid points per lane
     double jit_flops_pt = 0;  // its FP64 flops per grid point (counted by the generator)
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
@@ -972,16 +1114,15 @@ int select_variant(mdp_engine *eng)
     uint32_t np = 0;
     for (uint32_t b : {1u, 2u, 4u, 8u, 16u})
         if (eng->npmax <= b) { np = b; break; }
-    if (!np)
-        return mdp_set_error(MDP_EUNSUPPORTED,
-                             "a year with %u possible states (more than 4 missing patches) "
-                             "exceeds the register-resident forward kernel (max 16)", eng->npmax);
+    // a year with more than 16 states (over 4 missing patches) exceeds the
+    // register-resident forward kernels: the wide path takes the problem
+    if (!np) eng->wide = true;
     uint32_t deg = 0;
     for (int b : kDegBuckets)
         if (eng->maxA <= (uint32_t)b) { deg = (uint32_t)b; break; }
     if (!deg) return mdp_set_error(MDP_EUNSUPPORTED, "%u occupied patches in one state (max %d)", eng->maxA, kMaxDeg);
     eng->deg = deg;
-    eng->variant = np * 100 + deg;
+    eng->variant = eng->wide ? 20000u + deg : np * 100 + deg;
     return MDP_OK;
 }
 
@@ -998,6 +1139,7 @@ int build_plan(mdp_engine *eng, const mdp_problem *p)
         return mdp_set_error(MDP_EUNSUPPORTED, "%u variable columns (engine limit 24)", p->nvar);
     eng->nstates = 1u << p->nvar;
     eng->prior0 = (double)p->prior[0];
+    if (const char *wv = getenv("MDP_WIDE")) eng->wide = atoi(wv) != 0;
     eng->np.resize(p->tmax);
     eng->npmax = 1;
     for (uint32_t t = 0; t < p->tmax; ++t) {
@@ -1067,6 +1209,7 @@ int build_plan(mdp_engine *eng, const mdp_problem *p)
     eng->ncoef = off;
     int rc = select_variant(eng);
     if (rc) return rc;
+    if (eng->wide) return MDP_OK;  // no step program / k_coefs plan: build_wide_plan
     // step program
     for (uint32_t t = 1; t < p->tmax;) {
         if (eng->np[t - 1] == 1 && eng->np[t] == 1) {
@@ -1211,6 +1354,21 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
     return MDP_OK;
 }
 
+// Wide-path plan: the direct plan's groups, items and per-use descriptors,
+// plus the FP64 work per grid point of k_fwd_wide (every use a (nX+1)-term
+// dot product with a weight multiply per term, one FMA into the state
+// vector; the per-lane power tables; the final prior sum).
+int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
+{
+    int rc = build_direct_plan(eng, p);
+    if (rc) return rc;
+    eng->ldQ = ((size_t)eng->ncoef_d + 1) & ~(size_t)1;
+    double f = 2.0 * (eng->maxA + 1) + 2.0 * eng->np[eng->tmax - 1];
+    for (uint32_t d : eng->udesc_d) f += 3.0 * (((d >> kOffBits) & 31u) + 1.0) + 2.0;
+    eng->wide_flops_pt = f;
+    return MDP_OK;
+}
+
 constexpr size_t kQrowsLdsMax = 160 * 1024;
 constexpr size_t kFusedLdsMax = 64 * 1024;  // fused forward kernel: every table of one column
 
@@ -1258,6 +1416,7 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     d.zs_cmax = cmax;
     d.zs_len = (uint32_t)(kmax * nj);
     d.zs_kmax = (uint32_t)kmax;
+    if (eng->wide) return MDP_OK;  // no fused kernel on the wide path
     // the fused kernel's column tables: one contiguous image it copies to LDS
     // (with zpad, all KZ zs rows, zero past kmax: the kernel reads them unmasked)
     const MdpJitPlan &pl = eng->jit_plan;
@@ -1324,6 +1483,12 @@ size_t fused_lds(const mdp_engine *eng, size_t ct_len)
     return (ct_len + 2 + fc * (eng->nj + eng->nitems + eng->ldQ)) * sizeof(double);  // + staging scratch
 }
 
+constexpr size_t kWidePgBytes = 256ull << 20;  // wide path: item-factor chunk
+constexpr size_t kWideVBytes = 1ull << 30;     // wide path: state-vector scratch
+
+// k_fwd_wide: per-lane x^r, y^r tables, r <= maxA
+size_t wide_lds(const mdp_engine *eng) { return 2 * ((size_t)eng->maxA + 1) * kBlock * sizeof(double); }
+
 int upload_binomials()  // into the current device's constant bank
 {
     double h[kMaxDeg + 1][kMaxDeg + 1] = {};
@@ -1366,7 +1531,7 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(d.stream));
     (void)hipFree(dM);
-    if (eng->jit) {
+    if (eng->jit || eng->wide) {
         std::vector<double> sv((size_t)eng->nj * eng->nvar + 1, 0.0);
         for (uint32_t js = 0; js < eng->nj; ++js)
             for (uint32_t b = 0; b < eng->nvar; ++b)
@@ -1383,6 +1548,12 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
         if ((rc = dev_upload(&d.sv, sv)) || (rc = dev_upload(&d.items, items)) ||
             (rc = dev_upload(&d.qstart, eng->qstart)) || (rc = dev_upload(&d.qitem, qitem)))
             return rc;
+        if (eng->wide) {
+            if ((rc = dev_upload(&d.np_d, eng->np)) || (rc = dev_upload(&d.udesc_w, eng->udesc_d))) return rc;
+            HIP_TRY(hipFuncSetAttribute((const void *)k_fwd_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)wide_lds(eng)));
+            return MDP_OK;
+        }
         const size_t lds_max = qrows_lds(eng, kQrowsMaxC);
         if (lds_max > 64 * 1024)
             for (const void *fn : {(const void *)k_qrows<8, true>, (const void *)k_qrows<8, false>,
@@ -1411,6 +1582,7 @@ void free_device(DevCtx &d)
     void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog,
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
                     d.zs, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
+                    d.Pg, d.V, d.np_d, d.udesc_w,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -1431,7 +1603,28 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     HIP_TRY(hipSetDevice(d.device));
     int rc;
     if ((rc = dev_reserve(&d.e, &d.cap_e, ne)) || (rc = dev_reserve(&d.c, &d.cap_c, nc))) return rc;
-    if (eng->jit) {
+    if (eng->wide) {
+        double cmax = 0.0;
+        for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
+        if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ)) ||
+            (rc = dev_reserve(&d.Zg, &d.cap_zg, (size_t)nc * eng->nj + 1)))
+            return rc;
+        if (!(d.zs_cmax == cmax) && (rc = upload_qrows_tables(eng, d, cmax))) return rc;
+        // c values per launch: item factors within kWidePgBytes, the two state
+        // vectors of every point of a launch within kWideVBytes
+        const size_t ne_pad = (size_t)std::max<uint32_t>(1u, (ne + kBlock - 1) / kBlock) * kBlock;
+        const size_t cap_c = std::max<size_t>(1, std::min<size_t>(nc, 65535));
+        d.wide_cb_items = (uint32_t)std::min(cap_c, std::max<size_t>(1, kWidePgBytes / 8 / std::max<size_t>(1, eng->nitems)));
+        d.wide_cb_fwd = (uint32_t)std::min(cap_c, std::max<size_t>(1, kWideVBytes / 8 / (2 * (size_t)eng->npmax * ne_pad)));
+        if (const char *cv = getenv("MDP_WIDE_CB")) {  // tests: force several launches per slot
+            const uint32_t v = (uint32_t)std::max(1, atoi(cv));
+            d.wide_cb_items = std::min(d.wide_cb_items, v);
+            d.wide_cb_fwd = std::min(d.wide_cb_fwd, v);
+        }
+        if ((rc = dev_reserve(&d.Pg, &d.cap_pg, (size_t)d.wide_cb_items * eng->nitems + 1)) ||
+            (rc = dev_reserve(&d.V, &d.cap_v, 2 * (size_t)eng->npmax * d.wide_cb_fwd * ne_pad)))
+            return rc;
+    } else if (eng->jit) {
         double cmax = 0.0;
         for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
         if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ)) ||
@@ -1452,7 +1645,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
                (rc = dev_reserve(&d.R, &d.cap_r, (size_t)nc * ldR_of(eng)))) {
         return rc;
     }
-    if (!eng->jit && !eng->lds_part &&
+    if (!eng->jit && !eng->wide && !eng->lds_part &&
         (rc = dev_reserve(&d.gpart, &d.cap_gpart, (size_t)nc * eng->partP.size() * (eng->nvar + 1))))
         return rc;
     if (eng->diag) {
@@ -1573,9 +1766,47 @@ int launch_coefs(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
     return MDP_OK;
 }
 
+// Wide path, slot 1 (k_witems + k_wq per chunk of c values) or slot 2
+// (k_fwd_wide per chunk).  A profiled run times the slot as a whole: events
+// recorded around its launches.
+int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, uint32_t ld, hipStream_t s)
+{
+    const KernelEvents ev = t_kev;
+    t_kev = KernelEvents{};
+    if (ev.start) HIP_TRY(hipEventRecord(ev.start, s));
+    if (k == 1) {
+        const uint32_t cb = d.wide_cb_items;
+        for (uint32_t c0 = 0; c0 < d.nc; c0 += cb) {
+            const uint32_t n = std::min(cb, d.nc - c0);
+            const dim3 gi((eng->nitems + kBlock - 1) / kBlock, n);
+#define MDP_WITEMS(NV) \
+    hipLaunchKernelGGL((k_witems<NV>), gi, dim3(kBlock), 0, s, d.c, d.nc, c0, eng->nvar, d.Zg, d.sv, eng->nitems, d.items, d.Pg)
+            if (eng->nvar <= 8) MDP_WITEMS(8);
+            else if (eng->nvar <= 16) MDP_WITEMS(16);
+            else MDP_WITEMS(24);
+#undef MDP_WITEMS
+            const dim3 gq((uint32_t)((eng->ldQ + kBlock - 1) / kBlock), n);
+            hipLaunchKernelGGL(k_wq, gq, dim3(kBlock), 0, s, c0, eng->nitems, d.Pg, eng->ncoef_d, d.qstart, d.qitem,
+                               d.Qrow, (uint32_t)eng->ldQ);
+        }
+    } else {
+        const uint32_t cb = d.wide_cb_fwd;
+        for (uint32_t c0 = 0; c0 < d.nc; c0 += cb) {
+            const uint32_t n = std::min(cb, d.nc - c0);
+            const dim3 g((d.ne + kBlock - 1) / kBlock, n);
+            hipLaunchKernelGGL(k_fwd_wide, g, dim3(kBlock), wide_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.udesc_w,
+                               d.np_d, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, d.V, eng->npmax, out, ld);
+        }
+    }
+    HIP_TRY(hipGetLastError());
+    if (ev.stop) HIP_TRY(hipEventRecord(ev.stop, s));
+    return MDP_OK;
+}
+
 // Does kernel slot k (0: Q rows / k_zpv, 1: k_coefs, 2: forward) run on this path?
 bool slot_active(const mdp_engine *eng, const DevCtx &d, int k)
 {
+    if (eng->wide) return k == 2 || eng->nitems;
     if (eng->jit) return k == 2 || (k < 2 && eng->nitems && !d.fused);
     return k != 1 || eng->nuses;
 }
@@ -1583,8 +1814,9 @@ bool slot_active(const mdp_engine *eng, const DevCtx &d, int k)
 int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hipStream_t s)
 {
     if (!slot_active(eng, d, k)) return MDP_OK;
+    if (eng->wide && k > 0) return launch_wide(eng, d, k, out, ld, s);
     if (k == 2) return launch_forward(eng, d, out, ld, s);
-    if (eng->jit && k == 0) {  // Z rows
+    if ((eng->jit || eng->wide) && k == 0) {  // Z rows
         const uint32_t kmax = d.zs_kmax;
         const dim3 grid((d.nc + 64 * kZC - 1) / (64 * kZC), (eng->nj + kZRows - 1) / kZRows);
         MDP_LAUNCH(k_zrows, grid, dim3(kBlock), (size_t)kZRows * kmax * sizeof(double), s, d.c, d.nc, eng->nj,
@@ -1745,7 +1977,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
     if (const char *ev = getenv("MDP_DIAG")) eng->diag = atoi(ev) != 0;
     {
         const char *jv = getenv("MDP_JIT");
-        const bool want = !(jv && !strcmp(jv, "0"));
+        const bool want = !eng->wide && !(jv && !strcmp(jv, "0"));
         bool want_jit = want && build_direct_plan(eng, p) == MDP_OK;
         if (want_jit) {  // colonisation rows without pruning must fit the LDS
             const uint32_t z = ((eng->n - eng->nvar) + 7u) & ~7u;
@@ -1797,6 +2029,16 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (jit_build(eng, eng->fused_mode == 1) == MDP_OK) eng->jit = true;
             else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the generic kernel:\n%s\n",
                          eng->jit_log.c_str());
+        }
+    }
+    if (eng->wide) {
+        if ((rc = build_wide_plan(eng, p))) {
+            delete eng;
+            return rc;
+        }
+        if (jit_check && ndev == 0) {
+            delete eng;
+            return mdp_set_error(MDP_ENODEV, "no HIP device available (wide path planned)");
         }
     }
     std::vector<int> ids;
@@ -1998,6 +2240,7 @@ int mdp_engine_kernel_ms(mdp_engine *eng, double *ms, int max_k)
 const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
     if (!eng || k < 0 || k >= 3) return "";
+    if (eng->wide) return k < 2 && !eng->nitems ? "" : kKernelNames[2][k];
     if (eng->jit && k < 2 && (eng->devs.empty() || eng->devs[0].fused)) return "";  // fused: one kernel
     return kKernelNames[eng->jit ? 1 : 0][k];
 }
@@ -2026,6 +2269,7 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     double per_pt = (double)eng->nuses * (2.0 * (D + 1.0) + 2.0) + 3.0 * (D + 1.0) +
                     2.0 * (double)eng->npmax;
     if (eng->jit) per_pt = eng->jit_flops_pt;  // the generated code's own count
+    if (eng->wide) per_pt = eng->wide_flops_pt;
     if (flop_impl) *flop_impl = per_pt * pts;
     // SURVEY.md §8(d) F_alg (dense-in-j formulation)
     double fwd = 0;
@@ -2036,7 +2280,7 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     // compulsory bytes of k_forward: its coefficient stream once per c, the
     // e values, the output
     if (bytes_min)
-        *bytes_min = 8.0 * ((double)nc * (eng->jit ? eng->ldQ : ldR_of(eng)) + (double)ne + pts);
+        *bytes_min = 8.0 * ((double)nc * (eng->jit || eng->wide ? eng->ldQ : ldR_of(eng)) + (double)ne + pts);
     return MDP_OK;
 }
 

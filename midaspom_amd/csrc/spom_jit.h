@@ -18,10 +18,6 @@ struct MdpJitPlan {
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
     // items, qstart, qitem, then zs[kmax][nj]
     uint32_t off_it = 0, off_qs = 0, off_qi = 0, off_zs = 0;
-    // stage the column tables with global_load_lds (else registers).  Off:
-    // with one DMA per wave the staged image was intermittently wrong after
-    // vmcnt(0) + barrier (config-1 input; correct with >= 2 DMAs per wave),
-    // root cause not found -- register staging is the validated default
     uint32_t kzmax = 0;    // bound on the zs rows of any grid: n - nvar rounded up to 8
     bool zpad = false;     // the fused image always holds kzmax zs rows (zero past kmax)
     uint32_t qmaxlen = 0;  // most items of one Q entry

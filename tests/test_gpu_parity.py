@@ -123,16 +123,21 @@ def test_q5_impossible_transition(tmp_path):
 # ---------------------------------------------------------------------------
 # fuzzing: random problems covering every forward-kernel variant
 # ---------------------------------------------------------------------------
-@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic"])
+@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic", "wide", "wide-chunked"])
 def engine_path(request, monkeypatch):
     """Every engine path: the direct one (the hipRTC-specialised forward
     kernel; on these small grids it computes its column's Q itself), the same
     with Q rows from k_qrows (MDP_FUSED=0), the direct path with the
     transition cache and XCD ordering off (MDP_JIT_SLOTS=0, MDP_JIT_XCD=0), and
-    the generic kernels (MDP_JIT=0)."""
-    for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED"):
+    the generic kernels (MDP_JIT=0), and the wide path that years with more
+    than 16 states need (MDP_WIDE=1; chunked: one c value per launch)."""
+    for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB"):
         monkeypatch.delenv(k, raising=False)
-    if request.param == "generic":
+    if request.param.startswith("wide"):
+        monkeypatch.setenv("MDP_WIDE", "1")
+        if request.param == "wide-chunked":
+            monkeypatch.setenv("MDP_WIDE_CB", "1")
+    elif request.param == "generic":
         monkeypatch.setenv("MDP_JIT", "0")
     elif request.param == "direct-qrows":
         monkeypatch.setenv("MDP_FUSED", "0")
@@ -171,11 +176,66 @@ def test_single_year_and_constant_series(engine_path):
         assert_loglik_close(gpu_grid(model, g), ref)
 
 
-def test_too_many_missing_fails_loudly():
-    obs = np.array([[1, -1, -1, -1, -1, -1, 1], [1, 1, 0, 1, 0, 1, 1]])
+def _wide_obs(rng, n, T, missing):
+    """n patches x T years, every year occupied; `missing` = {year: k} puts k
+    unvisited (-1) patches into that year (2^k possible states)."""
+    obs = (rng.random((T, n)) < 0.6).astype(np.int32)
+    obs[:, 0] = 1
+    for yr, k in missing.items():
+        obs[yr, rng.choice(np.arange(1, n), size=k, replace=False)] = -1
+    return obs
+
+
+@pytest.mark.parametrize("missing", [{0: 5}, {3: 5}, {2: 6}, {4: 6}, {0: 8}, {3: 8}, {1: 5, 2: 6}, {0: 6, 4: 7}])
+def test_wide_years_vs_oracle(missing):
+    """Years with more than 4 missing patches (> 16 states), in year 0, in
+    later years, in consecutive years: the reference expands 2^k states for
+    any k (main_MIDASPOM.c:225-251) and propagates them (:371-384); the engine
+    routes such problems to the wide path."""
+    rng = np.random.default_rng(sum(100 * y + k for y, k in missing.items()))
+    obs = _wide_obs(rng, 12, 5, missing)
     model = mdp.Model.from_obs(obs)
-    with pytest.raises(mdp.MidaspomError, match="UNSUPPORTED"):
-        mdp.Engine(model)
+    assert model.npstates.max() == 2 ** max(missing.values())
+    g, _ = mdp.grid(5)
+    with mdp.Engine(model) as eng:
+        assert eng.info()["variant"] >= 20000  # the wide path
+        got = eng.loglik_grid(g, g)
+    ref = oracle.OracleModel.from_obs(obs).loglik_grid(g, g, threads=16)
+    assert np.isfinite(ref).sum() >= 9
+    assert_loglik_close(got, ref)
+
+
+def test_wide_survey_series_sampled(tmp_path):
+    """A survey-like series (the Appendix C generator, config-2 shape, 45 %
+    of the variable patches unvisited in each year: 2-64 states per year,
+    wide years back to back) on a 128 x 128 grid, sampled against the oracle."""
+    cfg = dict(synth.CONFIG2, pmiss=0.45, seed=5, T=30)
+    f = synth.write(tmp_path / "wide.txt", **cfg)
+    model = mdp.Model.load(f)
+    assert model.npstates.max() == 64
+    g, _ = mdp.grid(128)
+    got = gpu_grid(model, g)
+    rng = np.random.default_rng(3)
+    ie, ic = rng.integers(0, 128, 64), rng.integers(0, 128, 64)
+    ie[:4], ic[:4] = [0, 127, 0, 127], [0, 0, 127, 127]
+    ref = oracle.OracleModel.load(f).loglik_points(g[ie], g[ic], threads=16)
+    assert np.isfinite(ref).sum() >= 48
+    assert_loglik_close(got[ie, ic], ref)
+
+
+@pytest.mark.parametrize("fname,s", [("config2_64x50.txt", 64), ("occupancies.txt", 33)])
+def test_wide_path_matches_direct_path(golden, monkeypatch, fname, s):
+    """Forced onto the wide path, a problem the register kernels also run
+    gives the same log-likelihoods (sums reordered: ~1e-13)."""
+    model = mdp.Model.load(golden / fname)
+    g, _ = mdp.grid(s)
+    a = gpu_grid(model, g)
+    monkeypatch.setenv("MDP_WIDE", "1")
+    with mdp.Engine(model) as eng:
+        assert eng.info()["variant"] >= 20000
+        b = eng.loglik_grid(g, g)
+        assert set(eng.kernel_ms()) <= {"k_zrows", "k_wq", "k_forward"}
+    assert_loglik_close(b, a, atol=1e-11)
 
 
 # ---------------------------------------------------------------------------

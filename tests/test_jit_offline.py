@@ -55,3 +55,17 @@ def test_forward_kernels_compile_offline(src, tmp_path):
     code = SCRIPT.format(root=str(ROOT), src=src, tmp=str(tmp_path))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(gpu_available(), reason="offline planning check runs on CPU-only hosts")
+def test_wide_years_plan_offline():
+    """A year with 6 missing patches (64 states) plans onto the wide path
+    instead of being refused (main_MIDASPOM.c:225-251 takes any count)."""
+    code = (f"import sys; sys.path.insert(0, {str(ROOT)!r})\n"
+            "import numpy as np, midaspom_amd as mdp\n"
+            "obs = np.array([[1, -1, -1, -1, -1, -1, -1, 1], [1, 1, 0, 1, 0, 1, 1, 0], [1, 0, 0, 1, 1, 1, 0, 1]])\n"
+            "try:\n    mdp.Engine(mdp.Model.from_obs(obs), devices=[0])\n"
+            "except mdp.MidaspomError as ex:\n    assert 'wide path planned' in str(ex), str(ex); print('ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, MDP_JIT_CHECK="1"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
