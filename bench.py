@@ -24,6 +24,7 @@ import argparse
 import json
 import os
 import sys
+import subprocess
 import tempfile
 import time
 from pathlib import Path
@@ -47,24 +48,35 @@ CONFIGS = {
 }
 
 
-def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, budget_s=12.0):
-    """Oracle (CPU restatement of the reference dense CBLAS path, naive dgemm)
-    on a bounded, evenly strided sample of the same grid points; also the
-    parity of the GPU run at those points."""
-    import oracle
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-                         os.cpu_count() or 1))
-    om = oracle.OracleModel.load(input_path, 400.0, 0.5, 100.0)
+def host_info():
+    """nproc, the cores this process may use, and the CPU model."""
+    model = "unknown"
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"nproc": os.cpu_count() or 1, "usable_cores": usable, "cpu_model": model}
+
+
+def _all_threads():
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                      host_info()["usable_cores"]))
+
+
+def _oracle_leg(om, g_e, g_c, lik_gpu, ltot_gpu, tmax, threads, budget_s, per_pt):
+    """Time the oracle on an evenly strided sample of the grid sized for
+    ~budget_s of wall on `threads` threads; parity of the GPU run there."""
     ne, nc = lik_gpu.shape
-    # calibrate single-point cost, then size the sample for ~budget_s of wall
-    t0 = time.perf_counter()
-    om.loglik_points(g_e[:4], g_c[:4], threads=1)
-    per_pt = (time.perf_counter() - t0) / 4
     npts = int(min(ne * nc, max(threads * 8, budget_s * threads / per_pt)))
-    stride = max(1, int(np.floor(np.sqrt(ne * nc / npts))))
-    ie = np.arange(0, ne, stride)
-    ic = np.arange(0, nc, stride)
-    ee, cc = np.meshgrid(ie, ic, indexing="ij")
+    stride = max(1, int(np.ceil(np.sqrt(ne * nc / npts))))
+    ee, cc = np.meshgrid(np.arange(0, ne, stride), np.arange(0, nc, stride), indexing="ij")
     ee, cc = ee.ravel(), cc.ravel()
     t0 = time.perf_counter()
     ref = om.loglik_points(g_e[ee], g_c[cc], threads=threads)
@@ -73,22 +85,67 @@ def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, budget_s=12.0):
     with np.errstate(invalid="ignore", over="ignore"):
         pg, pr = np.exp(got - ltot_gpu), np.exp(ref - ltot_gpu)
     fin = np.isfinite(pr) & np.isfinite(pg)
-    same_inf = bool(np.array_equal(np.isneginf(got), np.isneginf(ref)))
-    dabs = float(np.abs(pg[fin] - pr[fin]).max()) if fin.any() else 0.0
     big = fin & (pr > 1e-14)
-    drel = float((np.abs(pg[big] - pr[big]) / pr[big]).max()) if big.any() else 0.0
     fl = np.isfinite(got) & np.isfinite(ref)
-    dlog = float(np.abs(got[fl] - ref[fl]).max()) if fl.any() else 0.0
-    return {
-        "value": ee.size * (tmax - 1) / wall,
-        "unit": "grid-point-timestep evals/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{ee.size} grid points (every {stride}th e and c of the {ne}x{nc} grid), "
-                  f"oracle/spom_oracle.c dense formulation with naive dgemm, {threads} threads, "
-                  f"{wall:.1f} s",
-    }, {"max_abs_dposterior": dabs, "max_rel_dposterior": drel, "max_abs_dloglik": dlog,
-        "points_checked": int(ee.size), "neginf_positions_match": same_inf}
+    parity = {"max_abs_dposterior": float(np.abs(pg[fin] - pr[fin]).max()) if fin.any() else 0.0,
+              "max_rel_dposterior": float((np.abs(pg[big] - pr[big]) / pr[big]).max()) if big.any() else 0.0,
+              "max_abs_dloglik": float(np.abs(got[fl] - ref[fl]).max()) if fl.any() else 0.0,
+              "points_checked": int(ee.size),
+              "neginf_positions_match": bool(np.array_equal(np.isneginf(got), np.isneginf(ref)))}
+    return {"value": ee.size * (tmax - 1) / wall, "cores": threads, "wall_s": wall,
+            "sample": f"{ee.size} grid points (every {stride}th e and c of the {ne}x{nc} grid)"}, parity
+
+
+def cli_walls(cfg_inputs, tmpdir):
+    """End-to-end wall time of the drop-in CLI (parse -> hipRTC -> grid -> Ltot
+    -> write; main_MIDASPOM.c:330,437-439 time the same span) with a cold
+    (fresh) and a warm hipRTC code-object cache, and of the oracle's own CLI
+    (the reference formulation, naive dgemm, 1 core) on config 1."""
+    from midaspom_amd import _lib
+    out = {}
+    cache = Path(tempfile.mkdtemp(prefix="mdp_jitcache_", dir=tmpdir))
+    for name, (inp, s) in cfg_inputs.items():
+        for leg in ("cold", "warm"):
+            env = dict(os.environ, MDP_JIT_CACHE=str(cache / name))
+            t0 = time.perf_counter()
+            r = subprocess.run([str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", str(s), "-i", str(inp),
+                                "-o", str(Path(tmpdir) / f"{name}.post")], env=env, capture_output=True)
+            out[f"{name}_cli_{leg}_s"] = time.perf_counter() - t0 if r.returncode == 0 else None
+    orc = ROOT / "oracle" / "_build" / "orc_main"
+    if orc.exists() and "config1" in cfg_inputs:
+        inp, s = cfg_inputs["config1"]
+        t0 = time.perf_counter()
+        r = subprocess.run([str(orc), "-m", "400", "-d", "100", "-s", str(s), "-i", str(inp),
+                            "-o", str(Path(tmpdir) / "orc.post")], capture_output=True,
+                           env=dict(os.environ, OMP_NUM_THREADS="1"))
+        out["config1_oracle_cli_1core_s"] = time.perf_counter() - t0 if r.returncode == 0 else None
+    return out
+
+
+def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, tmpdir, budget_s=10.0):
+    """The oracle (oracle/spom_oracle.c: the reference's dense CBLAS
+    formulation restated in C with a naive row-major dgemm) on the host
+    cores: a 1-core leg and an all-cores leg over bounded strided samples of
+    the same grid, plus end-to-end CLI walls (configs 1 and 2)."""
+    import oracle
+    om = oracle.OracleModel.load(input_path, 400.0, 0.5, 100.0)
+    t0 = time.perf_counter()
+    om.loglik_points(g_e[:4], g_c[:4], threads=1)
+    per_pt = (time.perf_counter() - t0) / 4
+    threads = _all_threads()
+    one, _ = _oracle_leg(om, g_e, g_c, lik_gpu, ltot_gpu, tmax, 1, budget_s, per_pt)
+    allc, parity = _oracle_leg(om, g_e, g_c, lik_gpu, ltot_gpu, tmax, threads, budget_s, per_pt)
+    cfg1 = ROOT / "tests" / "golden" / "occupancies.txt"
+    res = {
+        "value": allc["value"], "unit": "grid-point-timestep evals/s", "cores": threads, "kind": "port",
+        "sample": f"{allc['sample']}, {threads} threads, {allc['wall_s']:.1f} s",
+        "one_core": {"value": one["value"], "sample": f"{one['sample']}, 1 thread, {one['wall_s']:.1f} s"},
+        "dgemm": "naive row-major triple loop (oracle/spom_oracle.c); the reference itself needs CBLAS, "
+                 "which this image lacks (DESIGN.md §7)",
+        **host_info(),
+        "end_to_end": cli_walls({"config1": (cfg1, 50), "config2": (input_path, 512)}, tmpdir),
+    }
+    return res, parity
 
 
 def _coll_tensor(t, args):
@@ -133,18 +190,30 @@ def bench_future(args, world, rank, dev):
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    fut.check(stream)  # no replicate overflowed the posterior look-back
     kms = fut.time_kernel(r1 - r0, tfut, seed=seed, reps=args.steps)
     if world > 1:
         t = _coll_tensor(torch.tensor([dt], dtype=torch.float64, device=dev), args)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    # FP64 work the model needs per replicate-year (simpij, future.c:64-110):
-    # n^2 colonisation-sum adds + n source adds + n products c*s1, and one
-    # division per draw (n draws at least: every patch draws once).  The
-    # Philox integer work is not counted.
+    # The kernel is bound by integer VALU issue (Philox4x32-10: 4 calls per
+    # replicate-year), not by FP64: its roofline is vector-instruction issue,
+    # 256 CUs x 4 SIMDs x one wave64 VALU instruction per 2 cycles at 2.4 GHz
+    # (MI355X_MICROARCH.md), against the VALU instructions per launch counted
+    # by rocprofv3 (SQ_INSTS_VALU, profiles/pmc_valu_cfg5.json) for the
+    # same replicate count.  The FP64 work the model itself needs (n^2
+    # colonisation-sum adds + n source adds + n products c*s1 per
+    # replicate-year, simpij future.c:64-110) is reported beside it.
     n = row.size
     flop_per_ry = n * n + 2 * n + n
-    achieved = flop_per_ry * (r1 - r0) * tfut / (kms * 1e-3) / 1e12
+    valu_issue_peak = 256 * 4 * 2.4e9 / 2 / 1e9  # G wave-instructions/s
+    achieved, valu_src = None, None
+    vf = ROOT / "profiles" / "pmc_valu_cfg5.json"
+    if vf.exists():
+        pv = json.loads(vf.read_text())
+        if pv.get("replicates") == r1 - r0 and pv.get("years") == tfut:
+            achieved = pv["valu_insts_per_launch"] / (kms * 1e-3) / 1e9
+            valu_src = str(vf.relative_to(ROOT))
     result = {
         "metric": "replicate-year simulations/sec (MIDASPOM_future ensemble)",
         "value": nsim * tfut * args.steps / dt,
@@ -157,9 +226,11 @@ def bench_future(args, world, rank, dev):
                    "patches": int(n), "replicates": nsim, "years": tfut,
                    "parallelism": f"replicate ranges x{world}" + (", RCCL reduce" if world > 1 else "")},
         "kernel_ms": {"k_future": kms},
-        "roofline": {"kernel": "k_future", "bound": "mfma", "compute_unit": "FP64 VALU",
-                     "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+        "roofline": {"kernel": "k_future", "bound": "valu-issue", "compute_unit": "VALU issue (Philox integer work)",
+                     "achieved": achieved, "peak": valu_issue_peak, "unit": "G VALU wave-instructions/s",
+                     "frac": achieved / valu_issue_peak if achieved else None, "traffic": None,
+                     "valu_source": valu_src,
+                     "fp64_tflops": flop_per_ry * (r1 - r0) * tfut / (kms * 1e-3) / 1e12,
                      "flop_per_replicate_year": flop_per_ry},
         "cpu_baseline": None,
     }
@@ -229,6 +300,7 @@ def bench_dieoff(args, world, rank, dev):
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    job_ms = time_job(step, gather, dev, world, reps=1)
     kms = sc.time_kernels(out.data_ptr(), stream, reps=max(1, min(args.steps, 5)))
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -253,8 +325,9 @@ def bench_dieoff(args, world, rank, dev):
         "config": {"workload": f"config4: MIDASPOM_dieoff (e,c,K_D) {s}^3 grid, ts=20, tdis=10, n=8",
                    "grid": [s, s, s], "patches": int(n), "states": ns,
                    "parallelism": f"e-row slabs x{world}" + (", RCCL gather" if world > 1 else "")},
+        "job": {"ms": job_ms, "what": "one pass + one gather to rank 0" if world > 1 else "one pass"},
         "kernel_ms": kms,
-        "roofline": {"kernel": "k_scn_lik", "bound": "mfma", "compute_unit": "FP64 VALU",
+        "roofline": {"kernel": "k_scn_lik", "bound": "fp64-valu", "compute_unit": "FP64 VALU",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "flop_per_point_year": flop_year},
         "cpu_baseline": None,
@@ -283,6 +356,30 @@ def bench_dieoff(args, world, rank, dev):
         result["parity"] = {"points_checked": pts, "max_rel_dlik": worst}
     sc.close()
     return result
+
+
+def time_job(step, gather, dev, world, reps=3):
+    """Median wall (ms) of the reference's job shape: one pass of the path
+    plus the single gather, bracketed by barrier + synchronize."""
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        step()
+        gather()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        ts.append(time.perf_counter() - t0)
+    ms = float(np.median(ts)) * 1e3
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    return ms
 
 
 def main():
@@ -366,7 +463,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    # Kernel durations, measured live with HIP events on the engine's stream:
+    job_ms = time_job(step, gather, dev, world)
+    # Kernel durations, measured live with HIP events on the stream the path
+    # runs on (torch's current stream):
     # each kernel of the path launched K times back to back between two
     # events (mdp_engine_time_kernels; no per-launch events, whose completion
     # signals would add microseconds to every launch).  They agree with
@@ -388,9 +487,12 @@ def main():
         traffic_src = str(tf.relative_to(ROOT))
     units = world * s * s * (tmax - 1) * args.steps
     work = eng.work(s, s)
+    fact = eng.work_fact(s, s)
     info = eng.info()
     fwd_ms = kms.get("k_forward", float("nan"))
-    achieved_tf = work["flop_impl"] / (fwd_ms * 1e-3) / 1e12
+    fused = "k_qrows" not in kms  # the fused forward kernel does the per-c work too
+    flop_fwd = fact["flop"] if fused else s * s * (fact["weight_pt"] + fact["use_pt"] + fact["final_pt"])
+    achieved_tf = flop_fwd / (fwd_ms * 1e-3) / 1e12
     result = {
         "metric": "grid-point x timestep likelihood evals/sec",
         "value": units / dt,
@@ -407,10 +509,14 @@ def main():
         "config": {"workload": cfg["name"], "patches": model.n, "years": tmax, "grid": [world * s, s],
                    "per_rank_grid": [s, s], "nvar": model.nvar, "nstates": model.nstates,
                    "nextid": model.nextid, "parallelism": f"e-row slabs x{world}" + (", RCCL gather" if world > 1 else "")},
+        # the reference's job shape: ONE pass over the grid plus the single
+        # gather of the slabs (main_MIDASPOM_MPI.c:361-368, 482-506), median of 3
+        "job": {"ms": job_ms, "value": world * s * s * (tmax - 1) / (job_ms * 1e-3),
+                "what": "one pass + one gather to rank 0" if world > 1 else "one pass"},
         "kernel_ms": kms,
         "roofline": {
             "kernel": "k_forward",
-            "bound": "mfma",
+            "bound": "fp64-valu",
             "compute_unit": "FP64 VALU (MI355X FP64 vector peak = FP64 matrix peak)",
             "achieved": achieved_tf,
             "peak": FP64_PEAK_TFLOPS,
@@ -419,10 +525,18 @@ def main():
             "traffic": traffic,
             "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src,
-            "flop_per_launch": work["flop_impl"],
+            # closed-form factorised count from the plan's dimensions
+            # (mdp_engine_work_fact): the kernel's share of it
+            "flop_per_launch": flop_fwd,
+            "flop_basis": "closed-form factorised count, " + ("per-c + per-point terms (fused kernel)" if fused
+                                                              else "per-point terms (k_qrows does the per-c work)"),
+            "work_fact": fact,
+            "step_tflops_fact": fact["flop"] / (dt / args.steps) / 1e12,
+            # the hipRTC generator's count of the code it emitted (transition caching included)
+            "flop_per_launch_generated": work["flop_impl"],
+            # SURVEY §8(d) F_alg (dense-in-j form): exceeds the FP64 peak as a
+            # rate because the factorised path never performs most of it
             "flop_per_launch_survey_dense": work["flop_survey"],
-            # SURVEY §8(d) F_alg over the whole step: exceeds the FP64 peak
-            # because the factorised path never performs most of F_alg
             "falg_step_equiv_tflops": work["flop_survey"] / (dt / args.steps) / 1e12,
             "uses_per_point": info["nuses"],
         },
@@ -433,7 +547,7 @@ def main():
         torch.cuda.synchronize(dev)
         lik_h = lik.cpu().numpy()
         ltot = mdp.log_total(lik_h, win)
-        cpu, parity = cpu_baseline(inp, g_e, g_c, lik_h, ltot, tmax)
+        cpu, parity = cpu_baseline(inp, g_e, g_c, lik_h, ltot, tmax, tmpdir)
         result["cpu_baseline"] = cpu
         result["parity"] = parity
     else:

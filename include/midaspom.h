@@ -156,6 +156,26 @@ int mdp_engine_diag_report(mdp_engine *engine, char *buf, size_t len);
 int mdp_engine_work(const mdp_engine *engine, uint64_t ne, uint64_t nc, double *flop_impl,
                     double *flop_survey, double *bytes_min);
 
+/* Closed-form FP64 work of the factorised algorithm on an ne x nc grid
+ * (DESIGN.md §5), computed from the plan's dimensions alone -- not from any
+ * kernel's emitted code -- so a roofline fraction can be recomputed from the
+ * problem and a kernel duration.  Per c value: Z rows (3 flops per kept
+ * always-zero column, for the engine's current grid), var-column pressures
+ * (1 per row and var column), item factors (1 - pC where B_b = 0, one
+ * multiply per free column), Q sums (len - 1 adds per entry).  Per grid
+ * point: the weight table (2 maxA powers + one product per W[|A|][m] entry
+ * used), every forward use (2 nX + 3: the (nX+1)-term dot product and the
+ * state multiply-add), the prior sum (2 np_last - 1).  Transitions that
+ * recur are counted at every use (the hipRTC kernel caches some: it executes
+ * less).  flop = nc * per-c + ne * nc * per-point.  The per-c terms are zero
+ * on the generic path (MDP_JIT=0), which has no direct plan. */
+typedef struct mdp_work {
+    double z_c, pc_c, item_c, q_c;        /* per c value */
+    double weight_pt, use_pt, final_pt;   /* per grid point */
+    double flop;                          /* the grid's total */
+} mdp_work;
+int mdp_engine_work_fact(const mdp_engine *engine, uint64_t ne, uint64_t nc, mdp_work *work);
+
 /* Engine facts: number of devices, distinct transition pairs, forward
  * "uses" (one per consecutive-year state pair), coefficients per c value,
  * max states per year, selected kernel variant. */

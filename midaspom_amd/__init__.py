@@ -213,6 +213,15 @@ class Engine:
         return {"flop_impl": a.value, "flop_survey": b.value, "bytes_min": c.value}
 
 
+    def work_fact(self, ne: int, nc: int) -> dict:
+        """Closed-form FP64 work of the factorised algorithm on an ne x nc
+        grid (``mdp_engine_work_fact``): per-c and per-point
+        terms and the total ``flop``."""
+        w = _lib.Work()
+        check(lib().mdp_engine_work_fact(self._h, ne, nc, ctypes.byref(w)))
+        return {f: getattr(w, f) for f, _ in w._fields_}
+
+
 def grid(s: int, lo: float = 0.0, hi: float = 1.0):
     """(g, win): the reference's parameter grid (:120, :312-319)."""
     g = np.empty(int(s), dtype=np.float64)

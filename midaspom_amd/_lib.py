@@ -61,6 +61,13 @@ class Problem(ctypes.Structure):
     ]
 
 
+class Work(ctypes.Structure):
+    """Mirror of ``mdp_work`` (closed-form factorised FP64 work)."""
+
+    _fields_ = [(f, ctypes.c_double) for f in
+                ("z_c", "pc_c", "item_c", "q_c", "weight_pt", "use_pt", "final_pt", "flop")]
+
+
 class EngineInfo(ctypes.Structure):
     """Mirror of ``mdp_engine_info``."""
 
@@ -98,6 +105,7 @@ SIGNATURES = [
     ("mdp_engine_kernel_name", ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_int]),
     ("mdp_engine_work", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_dbl_p, c_dbl_p, c_dbl_p]),
+    ("mdp_engine_work_fact", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(Work)]),
     ("mdp_engine_get_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(EngineInfo)]),
     ("mdp_engine_diag_report", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
     ("mdp_last_error", ctypes.c_char_p, []),

@@ -2284,4 +2284,49 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     return MDP_OK;
 }
 
+
+int mdp_engine_work_fact(const mdp_engine *eng, uint64_t ne, uint64_t nc, mdp_work *w)
+{
+    if (!eng || !w) return mdp_set_error(MDP_EINVAL, "null argument");
+    *w = mdp_work{};
+    // per c value (the direct plan's tables; zero on the generic path, which
+    // has none): Z rows, var-column pressures, item factors, Q sums
+    const double cmax = eng->devs.empty() ? -1.0 : eng->devs[0].zs_cmax;
+    for (uint32_t js = 0; js < eng->nj; ++js) {
+        uint32_t kept = 0;
+        for (uint32_t k = 0; k < eng->n; ++k)
+            if (!eng->isvar[k] && !(cmax >= 0.0 && cmax * eng->Sj[(size_t)js * eng->n + k] <= 0x1p-55)) ++kept;
+        w->z_c += 3.0 * kept;        // fma(-c, s, 1) and one multiply per kept column
+        w->pc_c += (double)eng->nvar;  // pC = c S[j][b] per var column
+    }
+    const uint32_t vmask = eng->nvar >= 32 ? ~0u : (1u << eng->nvar) - 1u;
+    for (uint32_t i = 0; i < eng->nitems; ++i) {
+        const uint32_t j = eng->cj_bits[eng->itemRow[i]], B = eng->itemB[i];
+        const uint32_t free = (uint32_t)__builtin_popcount(~j & vmask);
+        // 1 - pC where B_b = 0, one multiply per free column (the last one by Z)
+        w->item_c += (double)__builtin_popcount(~B & ~j & vmask) + (double)free;
+    }
+    for (size_t q = 0; q + 1 < eng->qstart.size(); ++q) {
+        const uint32_t len = eng->qstart[q + 1] - eng->qstart[q];
+        if (len > 1) w->q_c += (double)(len - 1);
+    }
+    // per grid point: the weight table, every use's (nX+1)-term dot product
+    // and its multiply-add into the state vector, the final prior sum
+    std::vector<int> wmax(kMaxDeg + 1, -1);
+    const std::vector<uint32_t> &ud = eng->udesc_d.empty() ? eng->udesc : eng->udesc_d;
+    for (uint32_t d : ud) {
+        const uint32_t nX = (d >> kOffBits) & 31u, nA = d >> 27;
+        wmax[nA] = std::max(wmax[nA], (int)nX);
+        w->use_pt += 2.0 * nX + 3.0;
+    }
+    w->weight_pt = 2.0 * eng->maxA;
+    for (int a = 0; a <= kMaxDeg; ++a)
+        if (wmax[a] >= 0) w->weight_pt += (double)(wmax[a] + 1);
+    w->final_pt = 2.0 * eng->np[eng->tmax - 1] - 1.0;
+    const double per_c = w->z_c + w->pc_c + w->item_c + w->q_c;
+    const double per_pt = w->weight_pt + w->use_pt + w->final_pt;
+    w->flop = (double)nc * per_c + (double)ne * (double)nc * per_pt;
+    return MDP_OK;
+}
+
 }  // extern "C"
