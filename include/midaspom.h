@@ -204,7 +204,8 @@ typedef struct mdp_scenario mdp_scenario;
 /* Engine for the likelihood of the FIRST survey row `row` (n patches, values
  * -1/0/1; dieoff.c:185-232) under the die-off (kind 0) or habitat-loss
  * (kind 1) scenario, on HIP device `device`.  m, p, d as for mdp_model_load
- * (-m, -p, -d).  n <= 8 (the Pc table of 3^n entries lives in LDS). */
+ * (-m, -p, -d).  n <= 16: n <= 8 runs the LDS-resident kernel (factorised
+ * Pc tables in LDS), larger n a kernel whose state vectors live in HBM. */
 int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, double d, int kind, int device,
                         mdp_scenario **out);
 void mdp_scenario_destroy(mdp_scenario *scenario);

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -39,7 +40,10 @@ constexpr int kScnBlock = 1024;       // 16 waves: four per SIMD
 constexpr bool kPingPong = kScnBlock <= 768;  // register double-buffering (needs > 128 VGPRs)
 constexpr int kE = 32;                 // e values per workgroup (lanes mod 32)
 constexpr int kWaves = kScnBlock / 64;
-constexpr uint32_t kMaxN = 8;          // 2 x 2^8 x 32 state values + factor tables in LDS
+constexpr uint32_t kMaxN = 8;          // k_scn: 2 x 2^8 x 32 state values + factor tables in LDS
+constexpr uint32_t kBigMaxN = 16;      // k_scn_big: state vectors in HBM
+constexpr int kBigBlock = 256;
+constexpr size_t kBigScratch = 1ull << 30;  // k_scn_big state-vector scratch per launch (bytes)
 
 #define SCN_TRY(expr)                                                                        \
     do {                                                                                     \
@@ -407,6 +411,111 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
     }
 }
 
+// Any n (the reference builds 2^n states for whatever the first row holds,
+// dieoff.c:238, loss.c:222): one lane per grid point, its two state vectors
+// in an HBM scratch laid out [state][lane] (coalesced).  Per year, for every
+// row j (wave-uniform loop, so S[j][k] are scalar loads), the colonisation
+// sum over the supersets b of j,
+//     (Pc y)[j] = sum_{s <= F} prod_{k in F} (s_k ? pC_jk : 1 - pC_jk) y[j | s],
+// F = the patches not in j, is contracted as a binary tree over the free
+// patches (lowest state bit innermost) while the supersets stream past in
+// ascending order: leaf i completes its trailing-one levels, then parks its
+// node as the left child of the next level -- 2^(f+1) flops and 2^f loads
+// for a row with f free patches, 2 3^n per year in all.  Then extinction, the
+// tensor product over patches, as n in-place pair passes.  Same operator
+// order as k_scn (colonisation, then extinction); sums reordered.
+__global__ __launch_bounds__(kBigBlock) void k_scn_big(ScnArgs a, const double *__restrict__ S,
+                                                       const double *__restrict__ y0src,
+                                                       const double *__restrict__ ev, const double *__restrict__ cv,
+                                                       const double *__restrict__ Kv, const double *__restrict__ srcv,
+                                                       size_t p0, uint32_t npl, double *__restrict__ Y,
+                                                       double *__restrict__ out)
+{
+    typedef const __attribute__((address_space(4))) double cdouble;
+    // the contraction's parked left children, per lane: a level index is
+    // wave-uniform but dynamic, so LDS rather than (scratch-spilled) registers
+    __shared__ double accs[kBigMaxN][kBigBlock];
+    double *acc = &accs[0][threadIdx.x];
+    const uint32_t q = blockIdx.x * kBigBlock + threadIdx.x;
+    const bool live = q < npl;
+    const size_t pt = p0 + (live ? q : 0u);
+    const uint32_t n = a.n, NS = 1u << n;
+    // mode 0: pt = ic ne + ie (v per (c, e)); mode 1: the output order
+    uint32_t ie, ic, iK = 0, id = 0;
+    if (a.mode) {
+        id = (uint32_t)(pt % a.nd);
+        iK = (uint32_t)((pt / a.nd) % a.nK);
+        ic = (uint32_t)((pt / ((size_t)a.nd * a.nK)) % a.nc);
+        ie = (uint32_t)(pt / ((size_t)a.nd * a.nK * a.nc));
+    } else {
+        ic = (uint32_t)(pt / a.ne);
+        ie = (uint32_t)(pt % a.ne);
+    }
+    const double c = cv[ic], K = a.mode ? Kv[iK] : 1.0;
+    const double *src = a.mode && a.loss ? srcv + (size_t)id * n : nullptr;
+    const double Kpc = a.mode && !a.loss ? K : 1.0;
+    double E = a.mode && !a.loss ? ev[ie] / K : ev[ie];  // dieoff.c:56-57 E = e/K; loss.c:57 E = e
+    E = E > 1.0 ? 1.0 : E;
+    const double E1 = 1.0 - E;
+    const size_t st = (size_t)gridDim.x * kBigBlock;
+    double *ya = Y + q, *yb = ya + (size_t)NS * st;
+    for (uint32_t s = 0; s < NS; ++s)
+        ya[s * st] = a.mode ? y0src[((size_t)ic * NS + s) * a.ne + ie] : y0src[s];
+    cdouble *Sc = (cdouble *)S;
+    for (int t = 0; t < a.years; ++t) {
+        for (uint32_t j = 0; j < NS; ++j) {
+            const uint32_t F = ~j & (NS - 1), f = __popc(F);
+            // level L = the L-th lowest free state bit, patch n - 1 - bit
+            double w0[kBigMaxN], w1[kBigMaxN];
+            {
+                uint32_t fb = F;
+#pragma unroll
+                for (uint32_t L = 0; L < kBigMaxN; ++L) {
+                    if (!fb) continue;
+                    const uint32_t k = n - 1 - (uint32_t)__builtin_ctz(fb);
+                    fb &= fb - 1;
+                    const double sv = Sc[(size_t)j * n + k];
+                    double p = src ? c * (sv + src[k] * K) : c * sv * Kpc;  // dieoff.c:78, loss.c:98
+                    p = p > 1.0 ? 1.0 : p;
+                    w1[L] = p;
+                    w0[L] = 1.0 - p;
+                }
+            }
+            double res = 0.0;
+            uint32_t sub = 0;
+            for (uint32_t i = 0;; ++i) {
+                double cur = ya[(size_t)(j | sub) * st];
+                uint32_t L = 0;
+                for (; (i >> L) & 1u; ++L) cur = fma(w1[L], cur, acc[L * kBigBlock]);
+                if (L == f) {
+                    res = cur;
+                    break;
+                }
+                acc[L * kBigBlock] = w0[L] * cur;
+                sub = (sub - F) & F;
+            }
+            yb[(size_t)j * st] = res;
+        }
+        // extinction, ascending patch: y[s | m] = E y[s] + (1 - E) y[s | m]
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t m = 1u << (n - 1 - k);
+            for (uint32_t s = 0; s < NS; ++s)
+                if (s & m) yb[(size_t)s * st] = E * yb[(size_t)(s ^ m) * st] + E1 * yb[(size_t)s * st];
+        }
+        double *tmp = ya;
+        ya = yb;
+        yb = tmp;
+    }
+    if (!live) return;
+    if (!a.mode) {
+        for (uint32_t s = 0; s < NS; ++s) out[((size_t)ic * NS + s) * a.ne + ie] = ya[(size_t)s * st];
+        return;
+    }
+    double L = 0.0;
+    for (uint32_t s = 0; s < NS; ++s) L += ya[(size_t)s * st];
+    out[pt] = L;
+}
+
 // instantiation for n patches: NL = min(3, n) lo patches, NH = n - NL
 typedef void (*ScnKernel)(ScnArgs, const double *, const double *, const double *, const double *, const double *,
                           const double *, const uint32_t *, const uint32_t *, double *);
@@ -453,13 +562,17 @@ struct mdp_scenario {
     uint32_t ne = 0, nc = 0, nK = 0, nd = 0;
     double *de = nullptr, *dc = nullptr, *dK = nullptr, *dsr = nullptr, *dV = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // k_scn_big (n > 8, or MDP_SCN_BIG=1): state-vector scratch, points per launch
+    bool big = false;
+    double *dY = nullptr;
+    uint32_t big_pts = 0;
 };
 
 namespace {
 
 void scn_free_grid(mdp_scenario *sc)
 {
-    for (double **p : {&sc->de, &sc->dc, &sc->dK, &sc->dsr, &sc->dV}) {
+    for (double **p : {&sc->de, &sc->dc, &sc->dK, &sc->dsr, &sc->dV, &sc->dY}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
@@ -476,6 +589,22 @@ size_t scn_lds(const mdp_scenario *sc)
 // v = P^tdis w (which = 1), L = 1^T PK^ts v (which = 2) or both (3) on stream st
 int scn_launch(mdp_scenario *sc, double *dout, hipStream_t st, int which)
 {
+    if (sc->big) {
+        for (int mode = 0; mode < 2; ++mode) {
+            if (!(which & (1 << mode))) continue;
+            ScnArgs a{sc->n, sc->ns, sc->ne, sc->nc, sc->nK, sc->nd, mode ? sc->ts : sc->tdis, sc->kind, mode, 0, 0};
+            const double *y0 = mode ? sc->dV : sc->dw;
+            double *o = mode ? dout : sc->dV;
+            const size_t tot = mode ? (size_t)sc->ne * sc->nc * sc->nK * sc->nd : (size_t)sc->nc * sc->ne;
+            for (size_t p0 = 0; p0 < tot; p0 += sc->big_pts) {
+                const uint32_t npl = (uint32_t)std::min<size_t>(sc->big_pts, tot - p0);
+                hipLaunchKernelGGL(k_scn_big, dim3(sc->big_pts / kBigBlock), dim3(kBigBlock), 0, st, a, sc->dS, y0,
+                                   sc->de, sc->dc, sc->dK, sc->dsr, p0, npl, sc->dY, o);
+            }
+            SCN_TRY(hipGetLastError());
+        }
+        return MDP_OK;
+    }
     const uint32_t nchunk = (sc->ne + kE - 1) / kE;
     ScnKernel fn = scn_kernel(sc->n);
     const size_t lds = scn_lds(sc);
@@ -517,9 +646,9 @@ int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, doubl
 {
     if (!row || !out || n == 0) return mdp_set_error(MDP_EINVAL, "null argument");
     *out = nullptr;
-    if (n > kMaxN)
-        return mdp_set_error(MDP_EUNSUPPORTED, "%u patches: the scenario engine holds 3^n Pc entries in LDS (n <= %u)",
-                             n, kMaxN);
+    if (n > kBigMaxN)
+        return mdp_set_error(MDP_EUNSUPPORTED, "%u patches: the scenario engine takes n <= %u (2^n states)", n,
+                             kBigMaxN);
     for (uint32_t j = 0; j < n; ++j)
         if (row[j] < -1 || row[j] > 1) return mdp_set_error(MDP_EINVAL, "observation %d not in {-1,0,1}", row[j]);
     int ndev = 0;
@@ -533,6 +662,9 @@ int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, doubl
     sc->m = m;
     sc->d = d;
     sc->device = device;
+    // n > 8: the LDS-resident k_scn does not fit; MDP_SCN_BIG=1 forces k_scn_big (tests)
+    const char *bv = getenv("MDP_SCN_BIG");
+    sc->big = n > kMaxN || (bv && atoi(bv) != 0);
     const uint32_t ns = sc->ns;
     // dispersal M (dieoff.c:238-248) and colonisation sums S[j][k] =
     // sum over l != k, ascending, of M[l][k] * j_l (dieoff.c:72-77)
@@ -576,7 +708,7 @@ int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, doubl
     // 2^NL lo rows each) and the hi-row schedule: rows dealt to the waves by
     // longest-processing-time-first (row jh costs its 2^(f-1) superset
     // pairs, f = NH - |jh|, plus one for its loads and epilogue)
-    {
+    if (!sc->big) {
         const uint32_t nl = scn_nl(n), nh = n - nl, nhi = 1u << nh;
         sc->boff.assign(nhi, 0);
         uint32_t off = 0;
@@ -616,9 +748,11 @@ int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, doubl
         mdp_scenario_destroy(sc);
         return rc ? rc : mdp_set_error(MDP_EHIP, "stream creation failed");
     }
-    const size_t lds = scn_lds(sc);
-    if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute((const void *)scn_kernel(n), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (!sc->big) {
+        const size_t lds = scn_lds(sc);
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute((const void *)scn_kernel(n), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
     *out = sc;
     return MDP_OK;
 }
@@ -668,6 +802,16 @@ int mdp_scenario_set_grid(mdp_scenario *sc, int ts, int tdis, const double *e, u
         hipMalloc((void **)&sc->dV, (size_t)nc * ns * ne * sizeof(double)) != hipSuccess) {
         scn_free_grid(sc);
         return mdp_set_error(MDP_ENOMEM, "device allocation failed");
+    }
+    if (sc->big) {  // points per k_scn_big launch: two state vectors each within kBigScratch
+        const size_t tot = std::max((size_t)ne * nc * nK * nd, (size_t)nc * ne);
+        size_t pts = kBigScratch / (2 * (size_t)ns * sizeof(double));
+        pts = std::max<size_t>(kBigBlock, std::min(pts, tot + kBigBlock - 1) / kBigBlock * kBigBlock);
+        sc->big_pts = (uint32_t)std::min<size_t>(pts, (size_t)65535 * kBigBlock);
+        if (hipMalloc((void **)&sc->dY, 2 * (size_t)ns * sc->big_pts * sizeof(double)) != hipSuccess) {
+            scn_free_grid(sc);
+            return mdp_set_error(MDP_ENOMEM, "device allocation failed (state scratch)");
+        }
     }
     if (hipMemcpy(sc->de, e, ne * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(sc->dc, c, nc * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||

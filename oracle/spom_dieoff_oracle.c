@@ -24,19 +24,72 @@
  *                             :322-351  (loss.c:360-386)
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
-/* c = a*b, row-major n x n, the reference's cblas_dgemm(RowMajor,NoTrans,NoTrans) */
+/* c = a*b, row-major n x n, the reference's cblas_dgemm(RowMajor,NoTrans,NoTrans):
+ * every c[i][j] is the k-ascending sum s += a[i][k]*b[k][j].  For n > 8
+ * patches (2^n >= 512 states) b is transposed first, the rows are split over
+ * threads and each dot product runs as four interleaved partial sums -- a
+ * reordering of the same sum, as any optimised BLAS the reference links
+ * makes (naive and OpenBLAS reference outputs differ by <= 1e-13, SURVEY
+ * Appendix C); n <= 8 keeps the exact k-ascending order. */
+struct dg_job {
+    const double *a, *bt;
+    double *c;
+    int n, i0, i1;
+};
+
+static void *dg_rows(void *arg)
+{
+    const struct dg_job *J = arg;
+    const int n = J->n;
+    for (int i = J->i0; i < J->i1; ++i)
+        for (int j = 0; j < n; ++j) {
+            const double *ar = J->a + (size_t)i * n, *br = J->bt + (size_t)j * n;
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;  /* n is a multiple of 4 here */
+            for (int k = 0; k < n; k += 4) {
+                s0 += ar[k] * br[k];
+                s1 += ar[k + 1] * br[k + 1];
+                s2 += ar[k + 2] * br[k + 2];
+                s3 += ar[k + 3] * br[k + 3];
+            }
+            J->c[(size_t)i * n + j] = (s0 + s1) + (s2 + s3);
+        }
+    return NULL;
+}
+
 static void dgemm(const double *a, const double *b, double *c, int n)
 {
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j) {
-            double s = 0.0;
-            for (int k = 0; k < n; ++k) s += a[i * n + k] * b[k * n + j];
-            c[i * n + j] = s;
-        }
+    if (n <= 256) {
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+                double s = 0.0;
+                for (int k = 0; k < n; ++k) s += a[i * n + k] * b[k * n + j];
+                c[i * n + j] = s;
+            }
+        return;
+    }
+    double *bt = malloc(sizeof(double) * (size_t)n * n);
+    for (int k = 0; k < n; ++k)
+        for (int j = 0; j < n; ++j) bt[(size_t)j * n + k] = b[(size_t)k * n + j];
+    long nt = sysconf(_SC_NPROCESSORS_ONLN);
+    const char *ev = getenv("OMP_NUM_THREADS");
+    if (ev && atoi(ev) > 0) nt = atoi(ev);
+    if (nt > 16) nt = 16;
+    if (nt < 1) nt = 1;
+    pthread_t th[16];
+    struct dg_job jobs[16];
+    for (int t = 0; t < nt; ++t) {
+        jobs[t] = (struct dg_job){a, bt, c, n, (int)((long)n * t / nt), (int)((long)n * (t + 1) / nt)};
+        if (t) pthread_create(&th[t], NULL, dg_rows, &jobs[t]);
+    }
+    dg_rows(&jobs[0]);
+    for (int t = 1; t < nt; ++t) pthread_join(th[t], NULL);
+    free(bt);
 }
 
 /* z = x^k, dieoff.c:17-49 (x is overwritten, as in the reference) */

@@ -8,6 +8,7 @@ output is ~1e-20)."""
 from __future__ import annotations
 
 import subprocess
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -89,8 +90,9 @@ def test_random_rows(seed):
 
 
 def test_too_many_patches_fails_loudly():
+    # 2^17 states per grid point: past the engine's n <= 16
     with pytest.raises(mdp.MidaspomError, match="UNSUPPORTED"):
-        mdp.Scenario(np.zeros(9, dtype=np.int32), "dieoff")
+        mdp.Scenario(np.zeros(17, dtype=np.int32), "dieoff")
 
 
 def test_dieoff_cli_output_layout(golden, anchors, tmp_path):
@@ -183,3 +185,62 @@ def test_config4_full_workload(golden):
         refs = list(ex.map(ref, jobs))
     got = np.concatenate([lik[ie, ic, iK] for ie, ic, iK in jobs])
     close(got, np.concatenate(refs))
+
+
+# ---------------------------------------------------------------------------
+# n > 8 patches: k_scn_big (state vectors in HBM); dieoff.c:238 and loss.c:222
+# build 2^n states for whatever the first survey row holds
+# ---------------------------------------------------------------------------
+ROW12 = np.array([1, 0, 1, -1, 0, 1, 1, 0, -1, 1, 0, 1], dtype=np.int32)
+
+
+@pytest.mark.parametrize("kind", ["dieoff", "loss"])
+@pytest.mark.parametrize("row", [ROW12[:3], ROW12[:6], mdp.first_row(Path(__file__).parent / "golden" / "occupancies.txt")],
+                         ids=["n3", "n6", "n8"])
+def test_big_kernel_matches_lds_kernel(monkeypatch, kind, row):
+    """The general kernel forced onto n <= 8 agrees with the LDS kernel."""
+    e, c = np.array([0.05, 0.4, 0.9, 1.3]), np.array([0.1, 0.7, 2.0])
+    K, d = mdp.kgrid(4), mdp.dgrid(2)
+    out = []
+    for big in ("0", "1"):
+        monkeypatch.setenv("MDP_SCN_BIG", big)
+        with mdp.Scenario(row, kind, m=400, d=100) as sc:
+            out.append(sc.lik(e, c, K, d, ts=6, tdis=4))
+    close(out[1], out[0], rtol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["dieoff", "loss"])
+@pytest.mark.parametrize("n", [9, 10])
+def test_scenario_more_than_8_patches_vs_oracle(kind, n):
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+    row = ROW12[:n]
+    e, c = np.array([0.1, 0.45, 0.8]), np.array([0.15, 0.6])
+    K, d = np.array([0.3, 1.0, 7.5]), np.array([250.0, 900.0])
+    with mdp.Scenario(row, kind, m=400, d=100) as sc:
+        got = sc.lik(e, c, K, d, ts=20, tdis=10)
+    assert np.isfinite(got).all() and (got >= 0).all()
+    jobs = [(ie, ic) for ie in range(e.size) for ic in range(c.size)]
+
+    def ref(job):
+        ie, ic = job
+        if kind == "dieoff":
+            return oracle.dieoff_lik(row, K, e[ie], c[ic], ts=20, tdis=10, m=400.0, d=100.0)
+        return oracle.loss_lik(row, K, d, e[ie], c[ic], ts=20, tdis=10, m=400.0, d=100.0)
+
+    with ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1)) as ex:
+        refs = list(ex.map(ref, jobs))
+    for (ie, ic), r in zip(jobs, refs):
+        close(got[ie, ic], r)
+
+
+def test_scenario_12_patches_vs_oracle():
+    """n = 12 (4096 states) against the oracle's dense 4096^2 form, one K, a
+    one-year event (the oracle's dgemms dominate the test)."""
+    row = ROW12
+    with mdp.Scenario(row, "dieoff", m=400, d=100) as sc:
+        got = sc.lik(np.array([0.3]), np.array([0.4]), np.array([0.5, 3.0]), ts=1, tdis=1)[0, 0]
+        full = sc.lik(np.array([0.3, 0.6]), np.array([0.4]), mdp.kgrid(5), ts=20, tdis=10)
+    ref = oracle.dieoff_lik(row, np.array([0.5]), 0.3, 0.4, ts=1, tdis=1, m=400.0, d=100.0)
+    close(got[:1], ref)
+    assert np.isfinite(full).all() and (full >= 0).all()
