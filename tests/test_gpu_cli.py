@@ -84,3 +84,53 @@ def test_torchrun_cli_two_ranks(golden, tmp_path):
     # per-rank order: nextid comes after the dispersal matrix, before the data dump
     i_disp, i_obs = out.index("Dispersal matrix:"), out.index("Input occupancy data:")
     assert i_disp < out.index("nextid=10") < i_obs
+
+
+SCN_FLAGS = {"dieoff": ["-a", "10", "-e", "0.3", "-c", "0.4", "-m", "400", "-d", "100", "-s", "21"],
+             "loss": ["-a", "10", "-e", "0.3", "-c", "0.4", "-m", "400", "-d", "100", "-s", "13", "-v", "5"]}
+
+
+def _scn_strip(text):
+    return [ln for ln in text.splitlines() if "It took" not in ln]
+
+
+@pytest.mark.parametrize("kind", ["dieoff", "loss"])
+def test_python_scenario_cli_matches_compiled(golden, tmp_path, kind):
+    """`python -m midaspom_amd.scenario` = the compiled midaspom_dieoff /
+    midaspom_loss: same stdout lines, same file bytes."""
+    (tmp_path / "py").mkdir()
+    (tmp_path / "c").mkdir()
+    inp = str(golden / "occupancies.txt")
+    exe = _lib.DIEOFF_CLI_PATH if kind == "dieoff" else _lib.LOSS_CLI_PATH
+    rp = subprocess.run([sys.executable, "-m", "midaspom_amd.scenario", kind, *SCN_FLAGS[kind], "-i", inp,
+                         "-o", "lh.txt"], capture_output=True, text=True, timeout=180, env=_env(), cwd=tmp_path / "py")
+    assert rp.returncode == 0, rp.stderr
+    rc = subprocess.run([str(exe), *SCN_FLAGS[kind], "-i", inp, "-o", "lh.txt"], capture_output=True, text=True,
+                        timeout=180, cwd=tmp_path / "c")
+    assert rc.returncode == 0, rc.stderr
+    assert (tmp_path / "py" / "lh.txt").read_bytes() == (tmp_path / "c" / "lh.txt").read_bytes()
+    assert _scn_strip(rp.stdout) == _scn_strip(rc.stdout)
+
+
+@pytest.mark.parametrize("kind", ["dieoff", "loss"])
+def test_torchrun_scenario_two_ranks(golden, tmp_path, kind):
+    """The MIDASPOM_{dieoff,loss}_MPI.out shape: K slabs over 2 ranks, one
+    gather; the file equals the single-process one byte for byte."""
+    inp = str(golden / "occupancies.txt")
+    single, multi = tmp_path / "single.txt", tmp_path / "multi.txt"
+    r1 = subprocess.run([sys.executable, "-m", "midaspom_amd.scenario", kind, *SCN_FLAGS[kind], "-i", inp,
+                         "-o", str(single)], capture_output=True, text=True, timeout=180, env=_env(), cwd=ROOT)
+    assert r1.returncode == 0, r1.stderr
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "midaspom_amd.scenario", kind, "--backend", "gloo", *SCN_FLAGS[kind], "-i", inp, "-o", str(multi)]
+    r2 = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    assert multi.read_bytes() == single.read_bytes()
+    out = r2.stdout
+    assert out.count("beta MPI version") == 2
+    for r in (1, 2):
+        assert f"Starting parallel likelihood computation process {r}/2\n" in out
+        assert f"end likelihood computation process {r}/2\n" in out
+    assert "Sending data (proc 1)... " in out and "Gathering data from 1 proc... " in out
+    assert out.count("Migration matrix:") == 1 and out.count("Writing on file") == 1
