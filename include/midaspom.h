@@ -159,8 +159,9 @@ int mdp_engine_work(const mdp_engine *engine, uint64_t ne, uint64_t nc, double *
 /* Closed-form FP64 work of the factorised algorithm on an ne x nc grid
  * (DESIGN.md §5), computed from the plan's dimensions alone -- not from any
  * kernel's emitted code -- so a roofline fraction can be recomputed from the
- * problem and a kernel duration.  Per c value: Z rows (3 flops per kept
- * always-zero column, for the engine's current grid), var-column pressures
+ * problem and a kernel duration.  Per c value: Z rows (3 flops per explicit
+ * always-zero column and 2*8 + 2 for the series over the small ones, for the
+ * engine's current grid), var-column pressures
  * (1 per row and var column), item factors (1 - pC where B_b = 0, one
  * multiply per free column), Q sums (len - 1 adds per entry).  Per grid
  * point: the weight table (2 maxA powers + one product per W[|A|][m] entry

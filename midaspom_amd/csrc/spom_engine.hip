@@ -217,12 +217,25 @@ __global__ __launch_bounds__(kBlock) void k_zpv(
 // carries kZC c values that share every read.  Same multiplication order as
 // the fused forward kernel (four chains over k mod 8), so both variants give
 // identical bits.
+// Product of a Z row's small-column factors: exp(-c (P1 + c (P2/2 + ... +
+// c P8/8))), Horner from the top (upload_qrows_tables; the fused kernel
+// evaluates the same expression)
+constexpr int kZTermsDev = 8;
+__device__ __forceinline__ double zseries(const double (&p)[kZTermsDev], double c)
+{
+    double q = p[kZTermsDev - 1];
+#pragma unroll
+    for (int i = kZTermsDev - 2; i >= 0; --i) q = fma(q, c, p[i]);
+    return exp(-(q * c));
+}
+
 constexpr uint32_t kZRows = kBlock / 64;  // rows per workgroup
 constexpr uint32_t kZStage = 4;           // staging loads in flight per thread
 constexpr uint32_t kZC = 2;               // c values per lane
 __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cvals, uint32_t nc,
                                                   uint32_t nrows, uint32_t kmax,
-                                                  const double *__restrict__ zsT, double *__restrict__ Zg)
+                                                  const double *__restrict__ zsT, const double *__restrict__ zc,
+                                                  double *__restrict__ Zg)
 {
     extern __shared__ __attribute__((aligned(16))) double zl[];  // [kZRows][kmax]
     const uint32_t r0 = blockIdx.y * kZRows, nr = min(kZRows, nrows - r0);
@@ -243,13 +256,17 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
     __syncthreads();
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
     if (w >= nr) return;
+    // the row's small columns: exp(-c (P1 + c (P2/2 + ...))) (upload_qrows_tables)
+    double zcoef[kZTermsDev];
+#pragma unroll
+    for (int i = 0; i < kZTermsDev; ++i) zcoef[i] = zc[(size_t)(r0 + w) * kZTermsDev + i];
     uint32_t ic[kZC];
-    double c[kZC], za[kZC], zb[kZC], zc[kZC], zd[kZC];
+    double c[kZC], za[kZC], zb[kZC], zc_[kZC], zd[kZC];
 #pragma unroll
     for (uint32_t x = 0; x < kZC; ++x) {
         ic[x] = blockIdx.x * (64 * kZC) + x * 64 + (threadIdx.x & 63);
         c[x] = ic[x] < nc ? cvals[ic[x]] : 0.0;
-        za[x] = zb[x] = zc[x] = zd[x] = 1.0;
+        za[x] = zb[x] = zc_[x] = zd[x] = 1.0;
     }
     const double *z = zl + w * kmax;
     auto chunk = [&](const double *sk) {
@@ -257,7 +274,7 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
         for (uint32_t x = 0; x < kZC; ++x) {
             za[x] *= fma(-c[x], sk[0], 1.0) * fma(-c[x], sk[4], 1.0);
             zb[x] *= fma(-c[x], sk[1], 1.0) * fma(-c[x], sk[5], 1.0);
-            zc[x] *= fma(-c[x], sk[2], 1.0) * fma(-c[x], sk[6], 1.0);
+            zc_[x] *= fma(-c[x], sk[2], 1.0) * fma(-c[x], sk[6], 1.0);
             zd[x] *= fma(-c[x], sk[3], 1.0) * fma(-c[x], sk[7], 1.0);
         }
     };
@@ -277,8 +294,9 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
     }
 #pragma unroll
     for (uint32_t x = 0; x < kZC; ++x) {
-        double zz = (za[x] * zb[x]) * (zc[x] * zd[x]);
+        double zz = (za[x] * zb[x]) * (zc_[x] * zd[x]);
         if (kmax && !(fma(-c[x], z[0], 1.0) > 0.0)) zz = 0.0;
+        zz *= zseries(zcoef, c[x]);
         if (ic[x] < nc) Zg[(size_t)(r0 + w) * nc + ic[x]] = zz;
     }
 }
@@ -303,7 +321,7 @@ constexpr uint32_t kQrowsMaxC = 4;
 template <int NV, bool EXACT>  // EXACT: nvar == NV (no padded factor slots)
 __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     const double *__restrict__ cvals, uint32_t nc, uint32_t cb, uint32_t nvar, uint32_t nrows,
-    const double *__restrict__ Zg, const double *__restrict__ sv,
+    uint32_t kmax, const double *__restrict__ zsT, const double *__restrict__ zc, const double *__restrict__ sv,
     uint32_t nitems, const uint2 *__restrict__ items, uint32_t ncoef, const uint32_t *__restrict__ qstart,
     uint32_t nqi, const uint32_t *__restrict__ qitem, double *__restrict__ Q, uint32_t ldQ,
     unsigned long long *__restrict__ stamps)
@@ -346,12 +364,57 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
             }
         }
     }
-    // 1. Z per (c, row), computed by k_zrows; per (c, row, var column b) the
+    // 1. Z per (c, row): the row's explicit columns (zsT[row][k], loads of
+    // 16 values in flight) in k_zrows' four chains and order, the clamp test,
+    // then the small columns' series -- the bits k_zrows and the fused kernel
+    // produce; per (c, row, var column b) the
     // pressure pC = min(1, c S[j][b]), 1.0 for the columns of j (sv holds
     // -1 there) and past nvar
     for (uint32_t w = threadIdx.x; w < (nrows << lcb); w += kQrowsBlock) {
         const uint32_t cl = w & (cb - 1), r = w >> lcb;
-        if (cl < ncb) Zl[cl * nrows + r] = Zg[(size_t)r * nc + c0 + cl];
+        double c = cv[0];
+#pragma unroll
+        for (uint32_t i = 1; i < kQrowsMaxC; ++i) c = cl == i ? cv[i] : c;
+        const double2 *zr = (const double2 *)(zsT + (size_t)r * kmax);
+        double za = 1.0, zb = 1.0, zcc = 1.0, zd = 1.0;
+        auto chunk = [&](const double *sk) {
+            za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
+            zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);
+            zcc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);
+            zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
+        };
+        double first = 0.0;
+        uint32_t k = 0;
+        for (; k + 16 <= kmax; k += 16) {
+            double sk[16];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const double2 t2 = zr[k / 2 + u];
+                sk[2 * u] = t2.x;
+                sk[2 * u + 1] = t2.y;
+            }
+            if (k == 0) first = sk[0];
+            chunk(sk);
+            chunk(sk + 8);
+        }
+        if (k < kmax) {  // kmax is a multiple of 8
+            double sk[8];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double2 t2 = zr[k / 2 + u];
+                sk[2 * u] = t2.x;
+                sk[2 * u + 1] = t2.y;
+            }
+            if (k == 0) first = sk[0];
+            chunk(sk);
+        }
+        double zz = (za * zb) * (zcc * zd);
+        if (kmax && !(fma(-c, first, 1.0) > 0.0)) zz = 0.0;
+        double zq[kZTermsDev];
+#pragma unroll
+        for (int i = 0; i < kZTermsDev; ++i) zq[i] = zc[(size_t)r * kZTermsDev + i];
+        zz *= zseries(zq, c);
+        if (cl < ncb) Zl[cl * nrows + r] = zz;
     }
     for (uint32_t w = threadIdx.x; w < (nrows << lcb); w += kQrowsBlock) {  // a row's NV loads in flight
         const uint32_t cl = w / nrows, r = w - cl * nrows;
@@ -1041,6 +1104,8 @@ struct DevCtx {
     // direct path: k_zrows / k_qrows tables (zs, row-major [row][k], depends
     // on the grid's c range)
     double *zs = nullptr, *sv = nullptr, *Qrow = nullptr, *Zg = nullptr;
+    double *zc = nullptr;   // Z-row series coefficients [row][kZTerms]
+    size_t cap_zc = 0;
     uint2 *items = nullptr;  // per item {B | row << 24, j | (row >> 8) << 24}
     uint32_t *itemB = nullptr, *qstart = nullptr, *qitem = nullptr;
     size_t cap_zs = 0, cap_qrow = 0, cap_zg = 0;
@@ -1380,28 +1445,58 @@ size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
            (size_t)eng->nitems * sizeof(uint2) + ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);
 }
 
-// zs for a grid whose |c| <= cmax: a column's factor max(0, fma(-c, s, 1)) is
-// exactly 1.0 when |c s| <= 2^-55, so it is dropped.  The kept values of each
-// hidden-state row (largest first: the clamp test reads it) are stored
-// transposed, zs[k][row] with kmax = the longest row rounded up to 8 and zero
-// padding (factor 1.0), so lanes over rows read consecutive addresses.
+// Z rows for a grid whose |c| <= cmax.  Z_j(c) = prod over the always-zero
+// columns k of max(0, 1 - c S[j][k]) splits by the size of |c| S:
+//  * |c| S <= 2^-55: the factor is exactly 1.0 -- dropped;
+//  * 2^-55 < |c| S <= kZTau ("small"): never clamped, and their product is
+//    exp(sum log(1 - c S)) = exp(-sum_i c^i P_i / i) with the power sums
+//    P_i = sum_small S^i.  The series stops after kZTerms terms: the rest is
+//    below sum_small (c S)^(kZTerms+1) / (kZTerms+1) <= 256 * 2^-63 / 9
+//    < 2^-58 relative per 256 small columns (exp: ~1 ulp), so Z keeps
+//    double precision while a row costs kZTerms FMAs and one exp instead of
+//    an FMA and a multiply per column (config 3: 248 -> <= 24 columns a row);
+//  * the rest ("large", |c| S > kZTau or not finite) stay explicit factors,
+//    the largest first (the clamp test reads it).
+// zs[k][row] / zsT[row][k] hold the large columns (kmax = the longest row
+// rounded up to 8, zero padding = factor 1.0); zc[row][kZTerms] the series
+// coefficients P_i / i (zero for a row without small columns: exp(0) = 1).
+constexpr double kZTau = 0x1p-7;
+constexpr int kZTerms = kZTermsDev;
+
+void z_split(const mdp_engine *eng, uint32_t js, double cmax, std::vector<double> &large, double *coef)
+{
+    const uint32_t n = eng->n;
+    large.clear();
+    size_t imax = 0;
+    double pw[kZTerms] = {};
+    for (uint32_t k = 0; k < n; ++k) {
+        if (eng->isvar[k]) continue;
+        const double sv = eng->Sj[(size_t)js * n + k];
+        const double x = cmax * sv;
+        if (x <= 0x1p-55) continue;  // false for NaN / inf: kept
+        if (x <= kZTau) {
+            double t = sv;
+            for (int i = 0; i < kZTerms; ++i, t *= sv) pw[i] += t;
+            continue;
+        }
+        if (!large.empty() && sv > large[imax]) imax = large.size();
+        large.push_back(sv);
+    }
+    if (!large.empty()) std::swap(large[0], large[imax]);
+    if (coef)
+        for (int i = 0; i < kZTerms; ++i) coef[i] = pw[i] / (double)(i + 1);
+}
+
 int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
 {
     const uint32_t n = eng->n, nj = eng->nj;
+    (void)n;
     std::vector<std::vector<double>> rows(nj);
+    std::vector<double> zc((size_t)nj * kZTerms + 1, 0.0);
     size_t kmax = 0;
     for (uint32_t js = 0; js < nj; ++js) {
-        std::vector<double> &r = rows[js];
-        size_t imax = 0;
-        for (uint32_t k = 0; k < n; ++k) {
-            if (eng->isvar[k]) continue;
-            const double sv = eng->Sj[(size_t)js * n + k];
-            if (cmax * sv <= 0x1p-55) continue;  // false for NaN / inf: kept
-            if (!r.empty() && sv > r[imax]) imax = r.size();
-            r.push_back(sv);
-        }
-        if (!r.empty()) std::swap(r[0], r[imax]);
-        kmax = std::max(kmax, r.size());
+        z_split(eng, js, cmax, rows[js], &zc[(size_t)js * kZTerms]);
+        kmax = std::max(kmax, rows[js].size());
     }
     kmax = (kmax + 7) & ~(size_t)7;
     std::vector<double> zs(kmax * nj + 1, 0.0);  // [k][row]: the fused kernel's image
@@ -1413,6 +1508,8 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     int rc;
     if ((rc = dev_reserve(&d.zs, &d.cap_zs, zsT.size()))) return rc;
     HIP_TRY(hipMemcpy(d.zs, zsT.data(), zsT.size() * sizeof(double), hipMemcpyHostToDevice));
+    if ((rc = dev_reserve(&d.zc, &d.cap_zc, zc.size()))) return rc;
+    HIP_TRY(hipMemcpy(d.zc, zc.data(), zc.size() * sizeof(double), hipMemcpyHostToDevice));
     d.zs_cmax = cmax;
     d.zs_len = (uint32_t)(kmax * nj);
     d.zs_kmax = (uint32_t)kmax;
@@ -1432,6 +1529,7 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
         it[i] = make_uint2(eng->itemB[i] | ((r & 0xffu) << 24), eng->cj_bits[r] | ((r >> 8) << 24));
     }
     memcpy(img.data() + pl.off_qs, eng->qstart.data(), eng->qstart.size() * sizeof(uint32_t));
+    memcpy(img.data() + pl.off_zc, zc.data(), (size_t)nj * kZTerms * sizeof(double));
     if (!eng->qitem.empty())
         memcpy(img.data() + pl.off_qi, eng->qitem.data(), eng->qitem.size() * sizeof(uint32_t));
     for (size_t k = 0; k < kmax; ++k)  // zs pairs (k, k+1) of a row adjacent: one ds_read_b128
@@ -1582,7 +1680,7 @@ void free_device(DevCtx &d)
     void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog,
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
                     d.zs, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
-                    d.Pg, d.V, d.np_d, d.udesc_w,
+                    d.Pg, d.V, d.np_d, d.udesc_w, d.zc,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -1634,7 +1732,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         // one e block per c column and a small per-c problem: the forward
         // kernel computes its column's Q itself (one launch)
         const uint32_t gy = (ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
-        d.fused = fused_lds(eng, d.ct_len) <= kFusedLdsMax &&
+        d.fused = fused_lds(eng, d.ct_len) <= kFusedLdsMax && d.zs_kmax <= eng->jit_plan.kzmax &&
                   (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
         if ((rc = jit_load(eng, d, d.fused))) return rc;
         // c values per k_qrows workgroup: enough workgroups for every CU, within the LDS
@@ -1807,7 +1905,9 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, uint
 bool slot_active(const mdp_engine *eng, const DevCtx &d, int k)
 {
     if (eng->wide) return k == 2 || eng->nitems;
-    if (eng->jit) return k == 2 || (k < 2 && eng->nitems && !d.fused);
+    // the direct path computes its Z rows inside k_qrows (slot 0 idle); the
+    // wide path keeps k_zrows for its item kernel
+    if (eng->jit) return k == 2 || (k == 1 && eng->nitems && !d.fused);
     return k != 1 || eng->nuses;
 }
 
@@ -1820,7 +1920,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
         const uint32_t kmax = d.zs_kmax;
         const dim3 grid((d.nc + 64 * kZC - 1) / (64 * kZC), (eng->nj + kZRows - 1) / kZRows);
         MDP_LAUNCH(k_zrows, grid, dim3(kBlock), (size_t)kZRows * kmax * sizeof(double), s, d.c, d.nc, eng->nj,
-                   kmax, d.zs, d.Zg);
+                   kmax, d.zs, d.zc, d.Zg);
         HIP_TRY(hipGetLastError());
         return MDP_OK;
     }
@@ -1829,7 +1929,8 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
         const dim3 grid((d.nc + cb - 1) / cb);
         const size_t lds = qrows_lds(eng, cb);
 #define MDP_QROWS(NV, EX)                                                                              \
-    MDP_LAUNCH((k_qrows<NV, EX>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj, d.Zg,    \
+    MDP_LAUNCH((k_qrows<NV, EX>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj,          \
+               d.zs_kmax, d.zs, d.zc,                                                                  \
                d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart, (uint32_t)eng->qitem.size(),        \
                d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1])
         if (eng->nvar == 8) MDP_QROWS(8, true);
@@ -2005,7 +2106,17 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             plan.nitems = eng->nitems;
             plan.ncoef = eng->ncoef_d;
             plan.nqi = (uint32_t)eng->qitem.size();
-            plan.kzmax = ((eng->n - eng->nvar) + 7u) & ~7u;
+            {   // zs rows compiled into the fused kernel: the longest row of
+                // explicit columns at |c| <= 1 (the default grid); a grid
+                // with more (|c| > 1) runs k_zrows + k_qrows instead
+                size_t kz = 0;
+                std::vector<double> large;
+                for (uint32_t js = 0; js < eng->nj; ++js) {
+                    z_split(eng, js, 1.0, large, nullptr);
+                    kz = std::max(kz, large.size());
+                }
+                plan.kzmax = (uint32_t)std::max<size_t>(8, (kz + 7) & ~(size_t)7);
+            }
             plan.qmaxlen = 0;
             for (size_t q = 0; q + 1 < eng->qstart.size(); ++q)
                 plan.qmaxlen = std::max(plan.qmaxlen, eng->qstart[q + 1] - eng->qstart[q]);
@@ -2013,8 +2124,9 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             plan.off_it = even((size_t)eng->nj * eng->nvar);
             plan.off_qs = even(plan.off_it + eng->nitems);
             plan.off_qi = even(plan.off_qs + (eng->ncoef_d + 2) / 2);
-            plan.off_zs = even(plan.off_qi + (eng->qitem.size() + 1) / 2);
-            const size_t kmax_max = ((size_t)(eng->n - eng->nvar) + 7) & ~(size_t)7;
+            plan.off_zc = even(plan.off_qi + (eng->qitem.size() + 1) / 2);
+            plan.off_zs = even(plan.off_zc + (size_t)eng->nj * kZTerms);
+            const size_t kmax_max = plan.kzmax;
             plan.ct_max = (uint32_t)std::min<size_t>(((plan.off_zs + kmax_max * eng->nj) + 127) & ~(size_t)127,
                                                      kFusedLdsMax / sizeof(double));
             {   // zero-padded zs image when the largest one fits the fused kernel's LDS
@@ -2241,7 +2353,8 @@ const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
     if (!eng || k < 0 || k >= 3) return "";
     if (eng->wide) return k < 2 && !eng->nitems ? "" : kKernelNames[2][k];
-    if (eng->jit && k < 2 && (eng->devs.empty() || eng->devs[0].fused)) return "";  // fused: one kernel
+    // direct path: Z rows inside k_qrows (slot 0 idle); fused: one kernel
+    if (eng->jit && (k == 0 || (k == 1 && (eng->devs.empty() || eng->devs[0].fused)))) return "";
     return kKernelNames[eng->jit ? 1 : 0][k];
 }
 
@@ -2291,12 +2404,15 @@ int mdp_engine_work_fact(const mdp_engine *eng, uint64_t ne, uint64_t nc, mdp_wo
     *w = mdp_work{};
     // per c value (the direct plan's tables; zero on the generic path, which
     // has none): Z rows, var-column pressures, item factors, Q sums
-    const double cmax = eng->devs.empty() ? -1.0 : eng->devs[0].zs_cmax;
+    double cmax = eng->devs.empty() ? 1.0 : eng->devs[0].zs_cmax;
+    if (!(cmax >= 0.0)) cmax = 1.0;  // no grid yet: the default [0, 1]
+    std::vector<double> large;
+    double coef[kZTerms];
     for (uint32_t js = 0; js < eng->nj; ++js) {
-        uint32_t kept = 0;
-        for (uint32_t k = 0; k < eng->n; ++k)
-            if (!eng->isvar[k] && !(cmax >= 0.0 && cmax * eng->Sj[(size_t)js * eng->n + k] <= 0x1p-55)) ++kept;
-        w->z_c += 3.0 * kept;        // fma(-c, s, 1) and one multiply per kept column
+        z_split(eng, js, cmax, large, coef);
+        // fma(-c, s, 1) and one multiply per explicit column; the small
+        // columns' series: kZTerms FMAs, a multiply, the exp (counted 1)
+        w->z_c += 3.0 * (double)large.size() + (coef[0] != 0.0 ? 2.0 * kZTerms + 2.0 : 0.0);
         w->pc_c += (double)eng->nvar;  // pC = c S[j][b] per var column
     }
     const uint32_t vmask = eng->nvar >= 32 ? ~0u : (1u << eng->nvar) - 1u;

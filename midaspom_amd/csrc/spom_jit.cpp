@@ -122,7 +122,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     if (pl.fused)
         o << "#define NJ " << pl.nj << "\n#define NVAR " << pl.nvar << "\n#define NITEMS " << pl.nitems
           << "\n#define NCOEF " << pl.ncoef << "\n#define NQI " << (pl.nqi ? pl.nqi : 1) << "\n#define OFF_IT "
-          << pl.off_it << "\n#define OFF_QS " << pl.off_qs << "\n#define OFF_QI " << pl.off_qi << "\n#define OFF_ZS "
+          << pl.off_it << "\n#define OFF_QS " << pl.off_qs << "\n#define OFF_QI " << pl.off_qi << "\n#define OFF_ZC "
+          << pl.off_zc << "\n#define OFF_ZS "
           << pl.off_zs << "\n#define KZ " << std::max<uint32_t>(8u, pl.kzmax) << "\n#define ZPAD " << (pl.zpad ? 1 : 0)
           << "\n#define QML "
           << std::max<uint32_t>(1u, pl.qmaxlen) << "\n#define QUN " << std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)
@@ -218,6 +219,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    const u32 *Qsl = (const u32 *)(ct + OFF_QS);\n"
              "    const u32 *Qil = (const u32 *)(ct + OFF_QI);\n"
              "    const double *zl = ct + OFF_ZS;\n"
+             "    const double *zcl = ct + OFF_ZC;\n"
              "    double cc[FC];\n"
              "#pragma unroll\n"
              "    for (int f = 0; f < FC; ++f) cc[f] = ic0 + f < nc ? cvals[ic0 + f] : 0.0;\n"
@@ -325,6 +327,21 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "            }\n"
              "            double z = (za * zb) * (zc * zd);\n"
              "            if (kmax && !(fma(-c, sk[0], 1.0) > 0.0)) z = 0.0;\n"
+             // the row's small columns: exp(-c (P1 + c (P2/2 + ...))), the
+             // expression k_zrows evaluates (spom_engine.hip zseries)
+             "            {\n"
+             "                const double2 *zq = (const double2 *)(zcl + r * 8);\n"
+             "                const double2 p01 = zq[0], p23 = zq[1], p45 = zq[2], p67 = zq[3];\n"
+             "                double q = p67.y;\n"
+             "                q = fma(q, c, p67.x);\n"
+             "                q = fma(q, c, p45.y);\n"
+             "                q = fma(q, c, p45.x);\n"
+             "                q = fma(q, c, p23.y);\n"
+             "                q = fma(q, c, p23.x);\n"
+             "                q = fma(q, c, p01.y);\n"
+             "                q = fma(q, c, p01.x);\n"
+             "                z *= exp(-(q * c));\n"
+             "            }\n"
              "            Zl[col * NJ + r] = z;\n"
              "        }\n"
              "    }\n"

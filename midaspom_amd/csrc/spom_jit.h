@@ -16,9 +16,10 @@ struct MdpJitPlan {
     int fused_cols = 2;  // c columns per fused workgroup (KBLOCK threads each)
     uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
-    // items, qstart, qitem, then zs[kmax][nj]
-    uint32_t off_it = 0, off_qs = 0, off_qi = 0, off_zs = 0;
-    uint32_t kzmax = 0;    // bound on the zs rows of any grid: n - nvar rounded up to 8
+    // items, qstart, qitem, the Z-row series coefficients [nj][8], then
+    // zs[kmax][nj] (the explicit "large" columns)
+    uint32_t off_it = 0, off_qs = 0, off_qi = 0, off_zc = 0, off_zs = 0;
+    uint32_t kzmax = 0;    // zs rows compiled in (grids with |c| <= 1; larger ones use k_qrows)
     bool zpad = false;     // the fused image always holds kzmax zs rows (zero past kmax)
     uint32_t qmaxlen = 0;  // most items of one Q entry
     uint32_t ct_max = 0;  // largest column-table image (doubles), for the register staging
