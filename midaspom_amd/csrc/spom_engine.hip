@@ -301,26 +301,29 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
     }
 }
 
-// Transition coefficients of the direct path, one workgroup per kQrowsMaxC
-// (or fewer) consecutive c values, every hidden state j some transition needs
-// ("rows", r) and every (j, b) item:
-//  1. threads over (c, r): Z_r(c) = prod over the always-zero columns k of
-//     1 - min(1, c S[j][k]) -- the row's pruned S values streamed from L2 as
-//     16-byte loads; the clamp to 0 is tested once against the row maximum
-//     (zs[0]); rows are padded to even length with zeros (factor 1.0);
-//  2. threads over (c, item): Pc[j][b] = Z_r prod_{var b' not in j}
-//     (B_b' ? pC : 1 - pC), pC = min(1, c S[j][b']) -- into LDS;
-//  3. threads over (c, q): Q[c][q] = sum of the q-th entry's items (CSR, in
-//     ascending j: fixed order) -- written as coalesced rows for the forward
+// Transition coefficients of the direct path, one workgroup per CB (1, 2 or
+// 4) consecutive c values, every hidden state j some transition needs
+// ("rows", r) and every (j, b) item.  Per-c values sit interleaved in LDS
+// ([r][CB], [item][CB]) so the CB values of one row or item are one 16- or
+// 32-byte access and lanes over rows / items touch consecutive addresses:
+//  1. threads over (r, c): Z_r(c) = the row's explicit columns (zsT[row][k],
+//     16 loads in flight) in k_zrows' four chains and order, the clamp test
+//     against the row maximum (stored first), the small columns' series;
+//  2. threads over items, all CB c values each: Pc[j][b] = Z_r prod_{var b'
+//     not in j} (B_b' ? pC : 1 - pC), pC = min(1, c S[j][b']) from the row's
+//     staged var-column S (-1 marks the columns of j: pC = 1.0 there);
+//  3. threads over Q entries, all CB c values each: the entry's items summed
+//     in CSR (ascending j) order -- written as coalesced rows for the forward
 //     kernel.
-// Nothing but Q leaves the workgroup.  Columns whose factor rounds to exactly
-// 1.0 for every c of the grid are left out of zs, so the products equal the
-// full ones.
+// Nothing but Q leaves the workgroup.  (Round 1 kept the pressures in a
+// [c][row][NV] array whose 64-byte row stride put a wave's reads on a quarter
+// of the LDS banks, and ran threads over (c, item): SQ_LDS_BANK_CONFLICT was
+// 3x SQ_ACTIVE_INST_LDS.)
 constexpr int kQrowsBlock = 1024;
 constexpr uint32_t kQrowsMaxC = 4;
-template <int NV, bool EXACT>  // EXACT: nvar == NV (no padded factor slots)
+template <int NV, bool EXACT, int CB>  // EXACT: nvar == NV (no padded factor slots)
 __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
-    const double *__restrict__ cvals, uint32_t nc, uint32_t cb, uint32_t nvar, uint32_t nrows,
+    const double *__restrict__ cvals, uint32_t nc, uint32_t nvar, uint32_t nrows,
     uint32_t kmax, const double *__restrict__ zsT, const double *__restrict__ zc, const double *__restrict__ sv,
     uint32_t nitems, const uint2 *__restrict__ items, uint32_t ncoef, const uint32_t *__restrict__ qstart,
     uint32_t nqi, const uint32_t *__restrict__ qitem, double *__restrict__ Q, uint32_t ldQ,
@@ -329,31 +332,35 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     extern __shared__ __attribute__((aligned(16))) double lds[];
     MDP_RSTAMP(stamps, 6);
     MDP_STAMP(stamps, 0);
-    const uint32_t c0 = blockIdx.x * cb, ncb = min(cb, nc - c0);
-    double *Zl = lds;                                  // [cb][nrows]
-    double *Pr = Zl + (size_t)cb * nrows;              // [cb][nrows][NV] row colonisation pressures
-    double *Pl = Pr + (size_t)cb * nrows * NV;         // [cb][nitems]
-    uint2 *It = (uint2 *)(Pl + (size_t)cb * nitems);   // [nitems] {B, j}, row in the top bytes
+    const uint32_t c0 = blockIdx.x * CB, ncb = min((uint32_t)CB, nc - c0);
+    double *Zl = lds;                                  // [nrows][CB]
+    double *Svl = Zl + (size_t)nrows * CB;             // [nrows][NV] var-column S, -1 past nvar
+    double *Pl = Svl + (size_t)nrows * NV;             // [nitems][CB]
+    uint2 *It = (uint2 *)(Pl + (size_t)nitems * CB);   // [nitems] {B, j}, row in the top bytes
     uint32_t *Qs = (uint32_t *)(It + nitems);          // [ncoef + 1]
     uint32_t *Qi = Qs + ncoef + 1;                     // [nqi]
-    const uint32_t lcb = cb == 4 ? 2u : cb == 2 ? 1u : 0u;  // cb is 1, 2 or 4
-    double cv[kQrowsMaxC];  // this workgroup's c values, loaded once
+    double cv[CB];  // this workgroup's c values (0 past the grid: harmless)
 #pragma unroll
-    for (uint32_t i = 0; i < kQrowsMaxC; ++i) cv[i] = i < ncb ? cvals[c0 + i] : 0.0;
-    // items and the Q CSR: every thread's loads of all three tables in flight
+    for (int i = 0; i < CB; ++i) cv[i] = (uint32_t)i < ncb ? cvals[c0 + i] : 0.0;
+    // items, the Q CSR and the var-column S: every thread's loads in flight
     // before its stores (one global round trip instead of one per pass)
     {
         constexpr uint32_t kSt = 4;
-        const uint32_t nmax = max(max(nitems, ncoef + 1), nqi);
+        const uint32_t nsv = nrows * NV;
+        const uint32_t nmax = max(max(max(nitems, ncoef + 1), nqi), nsv);
         for (uint32_t i0 = threadIdx.x; i0 < nmax; i0 += kSt * kQrowsBlock) {
             uint2 ti[kSt];
             uint32_t ts[kSt], tq[kSt];
+            double tv[kSt];
 #pragma unroll
             for (uint32_t u = 0; u < kSt; ++u) {
                 const uint32_t i = i0 + u * kQrowsBlock;
                 ti[u] = i < nitems ? items[i] : make_uint2(0u, 0u);
                 ts[u] = i <= ncoef ? qstart[i] : 0u;
                 tq[u] = i < nqi ? qitem[i] : 0u;
+                const uint32_t r = i / NV, b = i % NV;
+                const double v = i < nsv && (EXACT || b < nvar) ? sv[(size_t)r * nvar + b] : 0.0;
+                tv[u] = v < 0.0 ? 0.0 : v;  // -1 marks a column of j: its factor is 1.0 via (s, n)
             }
 #pragma unroll
             for (uint32_t u = 0; u < kSt; ++u) {
@@ -361,20 +368,16 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
                 if (i < nitems) It[i] = ti[u];
                 if (i <= ncoef) Qs[i] = ts[u];
                 if (i < nqi) Qi[i] = tq[u];
+                if (i < nsv) Svl[i] = tv[u];
             }
         }
     }
-    // 1. Z per (c, row): the row's explicit columns (zsT[row][k], loads of
-    // 16 values in flight) in k_zrows' four chains and order, the clamp test,
-    // then the small columns' series -- the bits k_zrows and the fused kernel
-    // produce; per (c, row, var column b) the
-    // pressure pC = min(1, c S[j][b]), 1.0 for the columns of j (sv holds
-    // -1 there) and past nvar
-    for (uint32_t w = threadIdx.x; w < (nrows << lcb); w += kQrowsBlock) {
-        const uint32_t cl = w & (cb - 1), r = w >> lcb;
+    // 1. Z per (row, c)
+    for (uint32_t w = threadIdx.x; w < nrows * CB; w += kQrowsBlock) {
+        const uint32_t cl = w % CB, r = w / CB;
         double c = cv[0];
 #pragma unroll
-        for (uint32_t i = 1; i < kQrowsMaxC; ++i) c = cl == i ? cv[i] : c;
+        for (int i = 1; i < CB; ++i) c = cl == (uint32_t)i ? cv[i] : c;
         const double2 *zr = (const double2 *)(zsT + (size_t)r * kmax);
         double za = 1.0, zb = 1.0, zcc = 1.0, zd = 1.0;
         auto chunk = [&](const double *sk) {
@@ -414,83 +417,84 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
 #pragma unroll
         for (int i = 0; i < kZTermsDev; ++i) zq[i] = zc[(size_t)r * kZTermsDev + i];
         zz *= zseries(zq, c);
-        if (cl < ncb) Zl[cl * nrows + r] = zz;
-    }
-    for (uint32_t w = threadIdx.x; w < (nrows << lcb); w += kQrowsBlock) {  // a row's NV loads in flight
-        const uint32_t cl = w / nrows, r = w - cl * nrows;
-        double c = cv[0];
-#pragma unroll
-        for (uint32_t i = 1; i < kQrowsMaxC; ++i) c = cl == i ? cv[i] : c;
-        double sb[NV];
-#pragma unroll
-        for (int b = 0; b < NV; ++b) sb[b] = EXACT || (uint32_t)b < nvar ? sv[(size_t)r * nvar + b] : -1.0;
-        double2 *pr = (double2 *)(Pr + (size_t)w * NV);
-#pragma unroll
-        for (int b = 0; b < NV; b += 2) {
-            double p2[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                double pcv = c * sb[b + u];
-                pcv = pcv > 1.0 ? 1.0 : pcv;
-                p2[u] = sb[b + u] < 0.0 ? 1.0 : pcv;
-            }
-            pr[b / 2] = make_double2(p2[0], p2[1]);
-        }
+        Zl[w] = zz;
     }
     __syncthreads();
     MDP_STAMP(stamps, 1);
-    // 2. Pc per (c, item): Z times the product F of the var-column factors
-    // f_b = B_b ? pC_b : 1 - pC_b = fma(s_b, pC_b, n_b), (s_b, n_b) = (1, 0) or
-    // (-1, 1) built from the bit (j <= B, so j's columns give pC = 1.0), in
-    // the pairwise tree over NV slots -- the fused kernel's tree over nvar.
-    for (uint32_t w = threadIdx.x; w < (nitems << lcb); w += kQrowsBlock) {
-        const uint32_t cl = w & (cb - 1), it = w >> lcb;
+    // 2. Pc per item, its CB c values: Z times the product F of the
+    // var-column factors f_b = B_b ? pC_b : 1 - pC_b = fma(s_b, pC_b, n_b),
+    // (s_b, n_b) = (1, 0) or (-1, 1) from the bit (j <= B, so j's columns give
+    // pC = 1.0), in the pairwise tree over NV slots -- the fused kernel's
+    // tree over nvar (padded slots are 1.0)
+    for (uint32_t it = threadIdx.x; it < nitems; it += kQrowsBlock) {
         const uint2 t = It[it];
-        const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), nB = ~t.x;
-        const double z = Zl[cl * nrows + r];
-        const double2 *pr = (const double2 *)(Pr + ((size_t)cl * nrows + r) * NV);
-        double f[NV];
-#pragma unroll
-        for (int b = 0; b < NV / 2; ++b) {
-            const double2 p2 = pr[b];
-            f[2 * b] = p2.x;
-            f[2 * b + 1] = p2.y;
-        }
+        const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), nB = ~t.x, J = t.y & 0xffffffu;
+        // per slot (s_b, n_b): (1, 0) where B_b, (-1, 1) where not, (0, 1) for
+        // the columns of j and the padded slots -- so f_b = fma(s_b, min(1,
+        // c S), n_b) is p, 1 - p or exactly 1.0 with no selects; the values
+        // (hence the bits) are the fused kernel's
+        double sg[NV], nb[NV];
 #pragma unroll
         for (int b = 0; b < NV; ++b) {
-            // bit of B for slot b; slots past nvar read as set (pC = 1.0 there)
-            const uint32_t nbit = EXACT ? (nB >> (NV - 1 - b)) & 1u
-                                        : ((uint32_t)b < nvar ? (nB >> (nvar - 1 - (uint32_t)b)) & 1u : 0u);
-            const double sg = __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
-            const double nb = __hiloint2double((int)(nbit * 0x3ff00000u), 0);
-            f[b] = fma(sg, f[b], nb);
+            const uint32_t bit = EXACT ? (uint32_t)(NV - 1 - b) : nvar - 1 - (uint32_t)b;  // wraps past nvar
+            const bool one = (!EXACT && (uint32_t)b >= nvar) || ((J >> bit) & 1u);
+            const uint32_t nbit = one ? 0u : (nB >> bit) & 1u;
+            sg[b] = one ? 0.0 : __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
+            nb[b] = one ? 1.0 : __hiloint2double((int)(nbit * 0x3ff00000u), 0);
+        }
+        double sb[NV];
+        {
+            const double2 *s2 = (const double2 *)(Svl + (size_t)r * NV);
+#pragma unroll
+            for (int b = 0; b < NV / 2; ++b) {
+                const double2 v = s2[b];
+                sb[2 * b] = v.x;
+                sb[2 * b + 1] = v.y;
+            }
+        }
+        double zr[CB], pc[CB];
+#pragma unroll
+        for (int i = 0; i < CB; ++i) zr[i] = Zl[(size_t)r * CB + i];
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+            double f[NV];
+#pragma unroll
+            for (int b = 0; b < NV; ++b) f[b] = fma(sg[b], fmin(1.0, cv[i] * sb[b]), nb[b]);
+#pragma unroll
+            for (int sh = 1; sh < NV; sh *= 2)
+#pragma unroll
+                for (int b = 0; b + sh < NV; b += 2 * sh) f[b] *= f[b + sh];
+            pc[i] = zr[i] * f[0];
         }
 #pragma unroll
-        for (int sh = 1; sh < NV; sh *= 2)
-#pragma unroll
-            for (int b = 0; b + sh < NV; b += 2 * sh) f[b] *= f[b + sh];
-        Pl[cl * nitems + it] = z * f[0];
+        for (int i = 0; i < CB; ++i) Pl[(size_t)it * CB + i] = pc[i];
     }
     __syncthreads();
     MDP_STAMP(stamps, 2);
-    // 3. Q rows: the entry's items in CSR order, eight loads in flight.
-    // (Loading each thread's CSR bounds and first indices from global memory
-    // at kernel start measured slower: 14.0 -> 17.1 us on config 3.)
-    for (uint32_t w = threadIdx.x; w < ncb * ldQ; w += kQrowsBlock) {
-        const uint32_t cl = w / ldQ, q = w - cl * ldQ;
-        double a = 0.0;
+    // 3. Q rows: per entry its items in CSR order (four in flight), CB sums
+    for (uint32_t q = threadIdx.x; q < ldQ; q += kQrowsBlock) {
+        double a[CB];
+#pragma unroll
+        for (int i = 0; i < CB; ++i) a[i] = 0.0;
         if (q < ncoef) {
-            const double *pl = Pl + (size_t)cl * nitems;
             const uint32_t i0 = Qs[q], i1 = Qs[q + 1];
-            for (uint32_t i = i0; i < i1; i += 8) {
-                double pv[8];
+            for (uint32_t k = i0; k < i1; k += 4) {
+                double pv[4][CB];
 #pragma unroll
-                for (uint32_t u = 0; u < 8; ++u) pv[u] = pl[Qi[i + u < i1 ? i + u : i]];
+                for (uint32_t u = 0; u < 4; ++u) {
+                    const double *pl = Pl + (size_t)Qi[k + u < i1 ? k + u : k] * CB;
 #pragma unroll
-                for (uint32_t u = 0; u < 8; ++u) a = i + u < i1 ? a + pv[u] : a;
+                    for (int i = 0; i < CB; ++i) pv[u][i] = pl[i];
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int i = 0; i < CB; ++i) a[i] = k + u < i1 ? a[i] + pv[u][i] : a[i];
             }
         }
-        Q[(size_t)(c0 + cl) * ldQ + q] = a;
+#pragma unroll
+        for (int i = 0; i < CB; ++i)
+            if ((uint32_t)i < ncb) Q[(size_t)(c0 + i) * ldQ + q] = a[i];
     }
     MDP_STAMP(stamps, 3);
     MDP_RSTAMP(stamps, 7);
@@ -1441,7 +1445,7 @@ constexpr size_t kFusedLdsMax = 64 * 1024;  // fused forward kernel: every table
 size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
 {
     const size_t nv = eng->nvar <= 8 ? 8 : eng->nvar <= 16 ? 16 : 24;  // k_qrows NV
-    return ((size_t)cb * eng->nj + (size_t)cb * eng->nj * nv + (size_t)cb * eng->nitems) * sizeof(double) +
+    return ((size_t)cb * eng->nj + (size_t)eng->nj * nv + (size_t)cb * eng->nitems) * sizeof(double) +
            (size_t)eng->nitems * sizeof(uint2) + ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);
 }
 
@@ -1654,8 +1658,11 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
         }
         const size_t lds_max = qrows_lds(eng, kQrowsMaxC);
         if (lds_max > 64 * 1024)
-            for (const void *fn : {(const void *)k_qrows<8, true>, (const void *)k_qrows<8, false>,
-                                   (const void *)k_qrows<16, false>, (const void *)k_qrows<24, false>})
+            for (const void *fn : {(const void *)k_qrows<8, true, 1>, (const void *)k_qrows<8, false, 1>,
+                                   (const void *)k_qrows<16, false, 1>, (const void *)k_qrows<24, false, 1>,
+                                   (const void *)k_qrows<8, true, 2>, (const void *)k_qrows<8, false, 2>,
+                                   (const void *)k_qrows<16, false, 2>, (const void *)k_qrows<8, true, 4>,
+                                   (const void *)k_qrows<8, false, 4>})
                 HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)std::min(lds_max, kQrowsLdsMax)));
         if ((rc = jit_load(eng, d, eng->fused_mode == 1))) return rc;
@@ -1737,6 +1744,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         if ((rc = jit_load(eng, d, d.fused))) return rc;
         // c values per k_qrows workgroup: enough workgroups for every CU, within the LDS
         uint32_t cb = nc >= 1024 ? 4u : nc >= 512 ? 2u : 1u;  // power of two
+        cb = std::min(cb, eng->nvar <= 8 ? 4u : eng->nvar <= 16 ? 2u : 1u);  // registers (k_qrows)
         while (cb > 1 && qrows_lds(eng, cb) > kQrowsLdsMax) cb >>= 1;
         d.qrows_cb = cb;
     } else if ((rc = dev_reserve(&d.ZPV, &d.cap_zpv, (size_t)nc * (eng->nvar + 1) * eng->nstates)) ||
@@ -1928,16 +1936,26 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
         const uint32_t cb = d.qrows_cb;
         const dim3 grid((d.nc + cb - 1) / cb);
         const size_t lds = qrows_lds(eng, cb);
-#define MDP_QROWS(NV, EX)                                                                              \
-    MDP_LAUNCH((k_qrows<NV, EX>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, cb, eng->nvar, eng->nj,          \
-               d.zs_kmax, d.zs, d.zc,                                                                  \
-               d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart, (uint32_t)eng->qitem.size(),        \
-               d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1])
-        if (eng->nvar == 8) MDP_QROWS(8, true);
-        else if (eng->nvar < 8) MDP_QROWS(8, false);
-        else if (eng->nvar <= 16) MDP_QROWS(16, false);
-        else MDP_QROWS(24, false);
-#undef MDP_QROWS
+#define MDP_QROWS_CB(NV, EX, CB)                                                                        \
+    MDP_LAUNCH((k_qrows<NV, EX, CB>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, eng->nvar, eng->nj,         \
+               d.zs_kmax, d.zs, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
+               (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1])
+        // c values per workgroup: <= qrows_maxcb(nvar) (register budget at 1024 threads)
+        if (eng->nvar == 8) {
+            if (cb == 4) MDP_QROWS_CB(8, true, 4);
+            else if (cb == 2) MDP_QROWS_CB(8, true, 2);
+            else MDP_QROWS_CB(8, true, 1);
+        } else if (eng->nvar < 8) {
+            if (cb == 4) MDP_QROWS_CB(8, false, 4);
+            else if (cb == 2) MDP_QROWS_CB(8, false, 2);
+            else MDP_QROWS_CB(8, false, 1);
+        } else if (eng->nvar <= 16) {
+            if (cb == 2) MDP_QROWS_CB(16, false, 2);
+            else MDP_QROWS_CB(16, false, 1);
+        } else {
+            MDP_QROWS_CB(24, false, 1);
+        }
+#undef MDP_QROWS_CB
         HIP_TRY(hipGetLastError());
         return MDP_OK;
     }
