@@ -1732,9 +1732,8 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     } else if (eng->jit) {
         double cmax = 0.0;
         for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
-        if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ)) ||
-            (rc = dev_reserve(&d.Zg, &d.cap_zg, (size_t)nc * eng->nj + 1)))
-            return rc;
+        // (no Zg: k_qrows and the fused kernel form their Z rows themselves)
+        if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ))) return rc;
         if (!(d.zs_cmax == cmax) && (rc = upload_qrows_tables(eng, d, cmax))) return rc;
         // one e block per c column and a small per-c problem: the forward
         // kernel computes its column's Q itself (one launch)
