@@ -334,8 +334,11 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     MDP_STAMP(stamps, 0);
     const uint32_t c0 = blockIdx.x * CB, ncb = min((uint32_t)CB, nc - c0);
     double *Zl = lds;                                  // [nrows][CB]
-    double *Svl = Zl + (size_t)nrows * CB;             // [nrows][NV] var-column S, -1 past nvar
-    double *Pl = Svl + (size_t)nrows * NV;             // [nitems][CB]
+    // per row, c and var column the pressure min(1, c S[j][b]): rows padded
+    // by one double2 so rows read by one wave fall on different banks
+    constexpr uint32_t PRS = CB * NV + 2;
+    double *Prl = Zl + (((size_t)nrows * CB + 1) & ~(size_t)1);  // [nrows][PRS], 16-byte aligned
+    double *Pl = Prl + (size_t)nrows * PRS;            // [nitems][CB]
     uint2 *It = (uint2 *)(Pl + (size_t)nitems * CB);   // [nitems] {B, j}, row in the top bytes
     uint32_t *Qs = (uint32_t *)(It + nitems);          // [ncoef + 1]
     uint32_t *Qi = Qs + ncoef + 1;                     // [nqi]
@@ -346,21 +349,16 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // before its stores (one global round trip instead of one per pass)
     {
         constexpr uint32_t kSt = 4;
-        const uint32_t nsv = nrows * NV;
-        const uint32_t nmax = max(max(max(nitems, ncoef + 1), nqi), nsv);
+        const uint32_t nmax = max(max(nitems, ncoef + 1), nqi);
         for (uint32_t i0 = threadIdx.x; i0 < nmax; i0 += kSt * kQrowsBlock) {
             uint2 ti[kSt];
             uint32_t ts[kSt], tq[kSt];
-            double tv[kSt];
 #pragma unroll
             for (uint32_t u = 0; u < kSt; ++u) {
                 const uint32_t i = i0 + u * kQrowsBlock;
                 ti[u] = i < nitems ? items[i] : make_uint2(0u, 0u);
                 ts[u] = i <= ncoef ? qstart[i] : 0u;
                 tq[u] = i < nqi ? qitem[i] : 0u;
-                const uint32_t r = i / NV, b = i % NV;
-                const double v = i < nsv && (EXACT || b < nvar) ? sv[(size_t)r * nvar + b] : 0.0;
-                tv[u] = v < 0.0 ? 0.0 : v;  // -1 marks a column of j: its factor is 1.0 via (s, n)
             }
 #pragma unroll
             for (uint32_t u = 0; u < kSt; ++u) {
@@ -368,7 +366,6 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
                 if (i < nitems) It[i] = ti[u];
                 if (i <= ncoef) Qs[i] = ts[u];
                 if (i < nqi) Qi[i] = tq[u];
-                if (i < nsv) Svl[i] = tv[u];
             }
         }
     }
@@ -418,6 +415,16 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         for (int i = 0; i < kZTermsDev; ++i) zq[i] = zc[(size_t)r * kZTermsDev + i];
         zz *= zseries(zq, c);
         Zl[w] = zz;
+        // the row's pressures for this c: min(1, c S) (the columns of j, where
+        // sv holds -1, and padded slots get a factor of exactly 1.0 from
+        // (s, n) = (0, 1) in phase 2 whatever is stored here)
+        double pr[NV];
+#pragma unroll
+        for (int b = 0; b < NV; ++b)
+            pr[b] = (EXACT || (uint32_t)b < nvar) ? fmin(1.0, c * sv[(size_t)r * nvar + b]) : 0.0;
+        double2 *pd = (double2 *)(Prl + (size_t)r * PRS + cl * NV);
+#pragma unroll
+        for (int b = 0; b < NV / 2; ++b) pd[b] = make_double2(pr[2 * b], pr[2 * b + 1]);
     }
     __syncthreads();
     MDP_STAMP(stamps, 1);
@@ -442,24 +449,19 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
             sg[b] = one ? 0.0 : __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
             nb[b] = one ? 1.0 : __hiloint2double((int)(nbit * 0x3ff00000u), 0);
         }
-        double sb[NV];
-        {
-            const double2 *s2 = (const double2 *)(Svl + (size_t)r * NV);
-#pragma unroll
-            for (int b = 0; b < NV / 2; ++b) {
-                const double2 v = s2[b];
-                sb[2 * b] = v.x;
-                sb[2 * b + 1] = v.y;
-            }
-        }
         double zr[CB], pc[CB];
 #pragma unroll
         for (int i = 0; i < CB; ++i) zr[i] = Zl[(size_t)r * CB + i];
 #pragma unroll
         for (int i = 0; i < CB; ++i) {
             double f[NV];
+            const double2 *ps = (const double2 *)(Prl + (size_t)r * PRS + i * NV);
 #pragma unroll
-            for (int b = 0; b < NV; ++b) f[b] = fma(sg[b], fmin(1.0, cv[i] * sb[b]), nb[b]);
+            for (int b = 0; b < NV / 2; ++b) {
+                const double2 p2 = ps[b];
+                f[2 * b] = fma(sg[2 * b], p2.x, nb[2 * b]);
+                f[2 * b + 1] = fma(sg[2 * b + 1], p2.y, nb[2 * b + 1]);
+            }
 #pragma unroll
             for (int sh = 1; sh < NV; sh *= 2)
 #pragma unroll
@@ -1445,7 +1447,8 @@ constexpr size_t kFusedLdsMax = 64 * 1024;  // fused forward kernel: every table
 size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
 {
     const size_t nv = eng->nvar <= 8 ? 8 : eng->nvar <= 16 ? 16 : 24;  // k_qrows NV
-    return ((size_t)cb * eng->nj + (size_t)eng->nj * nv + (size_t)cb * eng->nitems) * sizeof(double) +
+    return ((((size_t)cb * eng->nj + 1) & ~(size_t)1) + (size_t)eng->nj * (cb * nv + 2) + (size_t)cb * eng->nitems) *
+               sizeof(double) +
            (size_t)eng->nitems * sizeof(uint2) + ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);
 }
 

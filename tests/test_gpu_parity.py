@@ -424,3 +424,31 @@ def test_grid_dropping_columns_then_full_grid(monkeypatch, fused):
             ref = ref_model.loglik_grid(e, c)
             assert np.isfinite(ref).sum() >= 20  # not only impossible points
             assert_loglik_close(eng.loglik_grid(e, c), ref)
+
+
+@pytest.mark.parametrize("fname", ["config2_64x50.txt", "config3_256x200.txt", "occupancies.txt"])
+def test_work_fact_per_point_terms_from_the_model(golden, fname):
+    """mdp_engine_work_fact's per-point terms restated from the enumerated
+    model alone: every use (k -> l between consecutive years)
+    costs 2 |A&B| + 3, the weight table 2 maxA + one product per W[|A|][m]
+    used, the prior sum 2 np_last - 1; flop = nc per-c + ne nc per-point."""
+    model = mdp.Model.load(golden / fname)
+    ids, ss = model.year_ids, model.short_state
+    use, mmax = 0.0, {}
+    for t in range(1, model.tmax):
+        for b in ids[t]:
+            for a in ids[t - 1]:
+                A, B = int(ss[a]), int(ss[b])
+                nX, nA = bin(A & B).count("1"), bin(A).count("1")
+                use += 2 * nX + 3
+                mmax[nA] = max(mmax.get(nA, -1), nX)
+    maxA = max(mmax) if mmax else 0
+    weight = 2 * maxA + sum(m + 1 for m in mmax.values())
+    final = 2 * len(ids[-1]) - 1
+    g, _ = mdp.grid(8)
+    with mdp.Engine(model) as eng:
+        eng.set_grid(g, g)
+        w = eng.work_fact(8, 8)
+    assert (w["use_pt"], w["weight_pt"], w["final_pt"]) == (use, weight, final)
+    per_c = w["z_c"] + w["pc_c"] + w["item_c"] + w["q_c"]
+    assert w["flop"] == 8 * per_c + 64 * (use + weight + final)
