@@ -452,3 +452,17 @@ def test_work_fact_per_point_terms_from_the_model(golden, fname):
     assert (w["use_pt"], w["weight_pt"], w["final_pt"]) == (use, weight, final)
     per_c = w["z_c"] + w["pc_c"] + w["item_c"] + w["q_c"]
     assert w["flop"] == 8 * per_c + 64 * (use + weight + final)
+
+
+def test_wide_single_year():
+    """One year with 6 unvisited patches (64 states), no transition: the wide
+    path's L = prior0 * 64 (Q3 semantics, main_MIDASPOM.c:368-392)."""
+    obs = np.array([[1, -1, -1, 1, -1, -1, -1, -1, 0, 1]])
+    model = mdp.Model.from_obs(obs, p=0.3)
+    g, _ = mdp.grid(4)
+    with mdp.Engine(model) as eng:
+        assert eng.info()["variant"] >= 20000
+        got = eng.loglik_grid(g, g)
+    ref = oracle.OracleModel.from_obs(obs, 400.0, 0.3, 100.0).loglik_grid(g, g)
+    assert_loglik_close(got, ref)
+    assert np.allclose(got, np.log(float(model.prior[0]) * 64))

@@ -244,3 +244,20 @@ def test_scenario_12_patches_vs_oracle():
     ref = oracle.dieoff_lik(row, np.array([0.5]), 0.3, 0.4, ts=1, tdis=1, m=400.0, d=100.0)
     close(got[:1], ref)
     assert np.isfinite(full).all() and (full >= 0).all()
+
+
+def test_scenario_13_patches_split_invariance():
+    """n = 13 (8192 states, beyond any oracle run here): at K_D = 1 the
+    die-off operator before the event equals the one after it, so
+    L(ts = a, tdis = b) = L(ts = a + b, tdis = 0) for every split -- a
+    property of the reference's formulation (dieoff.c:304-351) that holds
+    at any n."""
+    row = np.array([1, 0, 1, -1, 0, 1, 1, 0, -1, 1, 0, 1, 1], dtype=np.int32)
+    e, c, K = np.array([0.2, 0.55]), np.array([0.35]), np.array([1.0])
+    with mdp.Scenario(row, "dieoff", m=400, d=100) as sc:
+        a = sc.lik(e, c, K, ts=4, tdis=2)
+        b = sc.lik(e, c, K, ts=6, tdis=0)
+        d = sc.lik(e, c, K, ts=1, tdis=5)
+    assert np.isfinite(a).all() and (a > 0).all()
+    close(a, b, rtol=1e-12)
+    close(d, b, rtol=1e-12)
