@@ -286,6 +286,10 @@ const char *mdp_last_error(void);
 
 int mdp_abi_version(void);
 
+/* Number of visible HIP devices (0 when none); the CLIs use it to deal work
+ * over GPUs. */
+int mdp_device_count(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,7 +27,7 @@ from ._lib import MidaspomError, check, lib
 __all__ = [
     "Model", "Engine", "grid", "log_total", "write_posterior", "posterior",
     "run_file", "MidaspomError", "Scenario", "kgrid", "dgrid", "first_row",
-    "Future", "read_survey", "read_posterior",
+    "Future", "read_survey", "read_posterior", "device_count",
 ]
 
 
@@ -220,6 +220,11 @@ class Engine:
         w = _lib.Work()
         check(lib().mdp_engine_work_fact(self._h, ne, nc, ctypes.byref(w)))
         return {f: getattr(w, f) for f, _ in w._fields_}
+
+
+def device_count() -> int:
+    """Visible HIP devices, from the library (mdp_device_count)."""
+    return int(lib().mdp_device_count())
 
 
 def grid(s: int, lo: float = 0.0, hi: float = 1.0):

@@ -110,6 +110,7 @@ SIGNATURES = [
     ("mdp_engine_diag_report", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
     ("mdp_last_error", ctypes.c_char_p, []),
     ("mdp_abi_version", ctypes.c_int, []),
+    ("mdp_device_count", ctypes.c_int, []),
     ("mdp_kgrid", ctypes.c_double, [ctypes.c_uint32, ctypes.c_double, ctypes.c_double, c_dbl_p]),
     ("mdp_dgrid", ctypes.c_double, [ctypes.c_uint32, ctypes.c_double, ctypes.c_double, c_dbl_p]),
     ("mdp_scenario_create", ctypes.c_int,

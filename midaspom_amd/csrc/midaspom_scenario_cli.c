@@ -10,11 +10,16 @@
  * runs on the GPU through mdp_scenario_lik (include/midaspom.h).
  *
  * Policy: the reference leaves tdis, eB and cB uninitialised
- * when -a, -e or -c is omitted; here they are required.  -g <id> picks the
- * GPU (default 0).
+ * when -a, -e or -c is omitted; here they are required.
+ *
+ * Extension: -g <N> (or MIDASPOM_GPUS=N) splits the K grid into N contiguous
+ * slabs (remainder to the first, the MIDASPOM_{dieoff,loss}_MPI.out
+ * partition, dieoff_MPI.c:323-330), one host thread and engine per slab, the
+ * slabs dealt round-robin over the visible GPUs; the output is the same file.
  */
 #include <ctype.h>
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <time.h>
@@ -25,6 +30,30 @@
 #ifndef SCN_KIND
 #define SCN_KIND 0
 #endif
+
+struct slab {
+    const int32_t *row;
+    unsigned n, nK, nd;
+    double mdisp, d, eB, cB;
+    float prioroc;
+    int ts, tdis, dev;
+    const double *K, *dv;
+    double *L;
+    int rc;
+    char err[256];
+};
+
+static void *run_slab(void *arg)
+{
+    struct slab *sl = arg;
+    mdp_scenario *sc = NULL;
+    sl->rc = mdp_scenario_create(sl->row, sl->n, sl->mdisp, sl->prioroc, sl->d, SCN_KIND, sl->dev, &sc);
+    if (sl->rc == MDP_OK && sl->nK)
+        sl->rc = mdp_scenario_lik(sc, sl->ts, sl->tdis, &sl->eB, 1, &sl->cB, 1, sl->K, sl->nK, sl->dv, sl->nd, sl->L);
+    if (sl->rc != MDP_OK) snprintf(sl->err, sizeof sl->err, "%s", mdp_last_error());
+    mdp_scenario_destroy(sc);
+    return NULL;
+}
 
 int main(int argc, char **argv)
 {
@@ -39,7 +68,8 @@ int main(int argc, char **argv)
     const char *opts = "b:a:e:c:m:p:d:i:o:s:v:l:u:L:U:g:";
     const char *fout = "lh_loss.txt";
 #endif
-    int ts = 20, tdis = 0, have_a = 0, have_e = 0, have_c = 0, dev = 0;
+    int ts = 20, tdis = 0, have_a = 0, have_e = 0, have_c = 0, ngpu = 1;
+    if (getenv("MIDASPOM_GPUS")) ngpu = atoi(getenv("MIDASPOM_GPUS"));
     unsigned nstep = 151, nstepd = 20;
     double eB = 0, cB = 0, Kmin = 0.1, Kmax = 100.0, mdisp = 400.0, d = 200, dmin = 200, dmax = 4000;
     float prioroc = 0.5f;
@@ -63,7 +93,7 @@ int main(int argc, char **argv)
         case 'u': Kmax = atof(optarg); break;
         case 'L': dmin = atof(optarg); break;
         case 'U': dmax = atof(optarg); break;
-        case 'g': dev = atoi(optarg); break;
+        case 'g': ngpu = atoi(optarg); break;
         case '?':
             if (optopt == 'c')
                 fprintf(stderr, "Option -%c requires an argument.\n", optopt);
@@ -152,17 +182,32 @@ int main(int argc, char **argv)
     time_t start, end;
     time(&start);
     printf("Starting likelihood computation\n");
-    mdp_scenario *sc = NULL;
     const unsigned nd = SCN_KIND == 1 ? nstepd : 1u;
     double *L = malloc((size_t)nstep * nd * sizeof(double));
-    int rc = mdp_scenario_create(row, n, mdisp, prioroc, d, SCN_KIND, dev, &sc);
-    if (rc == MDP_OK) rc = mdp_scenario_lik(sc, ts, tdis, &eB, 1, &cB, 1, K, nstep, dv, nd, L);
-    if (rc != MDP_OK) {
-        fprintf(stderr, "midaspom: %s\n", mdp_last_error());
-        mdp_scenario_destroy(sc);
-        return 1;
+    if (ngpu < 1) ngpu = 1;
+    if ((unsigned)ngpu > nstep) ngpu = (int)(nstep ? nstep : 1);
+    struct slab *sl = calloc((size_t)ngpu, sizeof *sl);
+    pthread_t *th = calloc((size_t)ngpu, sizeof *th);
+    const unsigned avg = nstep / (unsigned)ngpu, rem = nstep % (unsigned)ngpu;
+    for (int r = 0; r < ngpu; ++r) {
+        const unsigned k0 = r == 0 ? 0 : (unsigned)r * avg + rem, k1 = (unsigned)(r + 1) * avg + rem;
+        sl[r] = (struct slab){row, n, k1 - k0, nd, mdisp, d, eB, cB, prioroc, ts, tdis, r, K + k0, dv,
+                              L + (size_t)k0 * nd, 0, ""};
     }
-    mdp_scenario_destroy(sc);
+    {   /* slabs dealt round-robin over the visible devices */
+        const int ndev = mdp_device_count() > 0 ? mdp_device_count() : 1;
+        for (int r = 0; r < ngpu; ++r) sl[r].dev = r % ndev;
+    }
+    for (int r = 1; r < ngpu; ++r) pthread_create(&th[r], NULL, run_slab, &sl[r]);
+    run_slab(&sl[0]);
+    for (int r = 1; r < ngpu; ++r) pthread_join(th[r], NULL);
+    for (int r = 0; r < ngpu; ++r)
+        if (sl[r].rc != MDP_OK) {
+            fprintf(stderr, "midaspom: %s\n", sl[r].err);
+            return 1;
+        }
+    free(sl);
+    free(th);
     printf("end likelihood computation\n");
     printf("Writing on file %s... ", fout);
     FILE *fe = fopen(fout, "wb");

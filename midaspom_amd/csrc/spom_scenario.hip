@@ -641,6 +641,12 @@ double mdp_dgrid(uint32_t s, double lo, double hi, double *dv)
     return s ? dv[0] : 0.0;
 }
 
+int mdp_device_count(void)
+{
+    int ndev = 0;
+    return hipGetDeviceCount(&ndev) == hipSuccess ? ndev : 0;
+}
+
 int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, double d, int kind, int device,
                         mdp_scenario **out)
 {

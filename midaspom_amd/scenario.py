@@ -53,7 +53,8 @@ def parse_args(kind, argv):
         ap.add_argument("-v", type=int, default=20, help="source-distance grid steps")
         ap.add_argument("-L", type=float, default=200.0, help="source distance lower bound")
         ap.add_argument("-U", type=float, default=4000.0, help="source distance upper bound")
-    ap.add_argument("-g", type=int, default=0, help="GPU (single process)")
+    ap.add_argument("-g", type=int, default=None,
+                    help="GPUs (single process): K slabs, one thread per slab (default MIDASPOM_GPUS or 1)")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl)")
     return ap.parse_args(argv)
 
@@ -78,6 +79,41 @@ def _states(row, p):
                 pr[k] = np.float32(pr[k] * np.float32(np.float32(b) * np.float32(p) +
                                                        np.float32(1 - b) * np.float32(1 - np.float32(p))))
     return ps, pr
+
+
+def _lik_slabs(mdp, mdist, row, kind, a, K, dv, nd):
+    """Single-process -g N: the K grid in N contiguous slabs (the MPI
+    partition), one thread and scenario engine per slab, the slabs dealt
+    round-robin over the visible GPUs (midaspom_scenario_cli.c run_slab).
+    The engine calls release the GIL (ctypes), so the slabs run together."""
+    import os
+    import threading
+
+    ngpu = a.g if a.g is not None else int(os.environ.get("MIDASPOM_GPUS", "1"))
+    ngpu = max(1, min(ngpu, a.s)) if a.s else 1
+    ndev = max(1, mdp.device_count())
+    lik = np.zeros((a.s, nd))
+    errs = []
+
+    def run(r):
+        r0, r1 = mdist.row_slab(r, ngpu, a.s)
+        try:
+            if r1 > r0:
+                with mdp.Scenario(row, kind, m=a.m, p=a.p, d=a.d, device=r % ndev) as sc:
+                    lik[r0:r1] = sc.lik(a.e, a.c, K[r0:r1], dv if kind == "loss" else None,
+                                        ts=a.b, tdis=a.a)[0, 0].reshape(r1 - r0, nd)
+        except Exception as exc:  # re-raised on the main thread
+            errs.append(exc)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(1, ngpu)]
+    for t in th:
+        t.start()
+    run(0)
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return lik
 
 
 def main(argv=None) -> int:
@@ -135,8 +171,7 @@ def main(argv=None) -> int:
     start = int(time.time())
     if not mpi:
         out("Starting likelihood computation\n")
-        with mdp.Scenario(row, kind, m=a.m, p=a.p, d=a.d, device=a.g) as sc:
-            lik = sc.lik(a.e, a.c, K, dv if kind == "loss" else None, ts=a.b, tdis=a.a)[0, 0]
+        lik = _lik_slabs(mdp, mdist, row, kind, a, K, dv, nd)
         out("end likelihood computation\n")
     else:
         import torch

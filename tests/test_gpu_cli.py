@@ -133,3 +133,22 @@ def test_torchrun_scenario_two_ranks(golden, tmp_path, kind):
         assert f"end likelihood computation process {r}/2\n" in out
     assert "Sending data (proc 1)... " in out and "Gathering data from 1 proc... " in out
     assert out.count("Migration matrix:") == 1 and out.count("Writing on file") == 1
+
+
+@pytest.mark.parametrize("kind", ["dieoff", "loss"])
+def test_scenario_cli_multi_gpu_slabs(golden, tmp_path, kind):
+    """-g N: the K grid in N slabs, one host thread + engine each (dealt
+    round-robin over the visible GPUs, so N = 3 runs three engines on a
+    one-GPU box concurrently); file bytes equal the -g 1 run, for the
+    compiled CLI and the Python one.  N > s clamps to s slabs."""
+    inp = str(golden / "occupancies.txt")
+    exe = _lib.DIEOFF_CLI_PATH if kind == "dieoff" else _lib.LOSS_CLI_PATH
+    outs = {}
+    for tag, cmd in {"c1": [str(exe), "-g", "1"], "c3": [str(exe), "-g", "3"],
+                     "c99": [str(exe), "-g", "99"],
+                     "py3": [sys.executable, "-m", "midaspom_amd.scenario", kind, "-g", "3"]}.items():
+        r = subprocess.run([*cmd, *SCN_FLAGS[kind], "-i", inp, "-o", str(tmp_path / f"{tag}.txt")],
+                           capture_output=True, text=True, timeout=180, env=_env(), cwd=ROOT)
+        assert r.returncode == 0, (tag, r.stderr[-2000:])
+        outs[tag] = (tmp_path / f"{tag}.txt").read_bytes()
+    assert outs["c3"] == outs["c1"] and outs["c99"] == outs["c1"] and outs["py3"] == outs["c1"]
