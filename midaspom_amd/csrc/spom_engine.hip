@@ -2155,11 +2155,14 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             }
             if (jit_check && ndev == 0) {
                 const int r0 = jit_build(eng, false), r1 = r0 ? r0 : jit_build(eng, true);
+                uint32_t ipr = 0;  // most items of one row
+                for (uint32_t js = 0; js + 1 < eng->cj_item0.size(); ++js)
+                    ipr = std::max(ipr, eng->cj_item0[js + 1] - eng->cj_item0[js]);
                 if (!r1)
                     mdp_set_error(MDP_ENODEV,
-                                  "no HIP device available (forward kernels compiled; nj %u nitems %u ldQ %zu "
-                                  "qitems %u kzmax %u fused LDS %zu)",
-                                  plan.nj, plan.nitems, (size_t)plan.ldQ, plan.nqi, plan.kzmax,
+                                  "no HIP device available (forward kernels compiled; nj %u nitems %u "
+                                  "items/row %u ldQ %zu qitems %u qmaxlen %u kzmax %u fused LDS %zu)",
+                                  plan.nj, plan.nitems, ipr, (size_t)plan.ldQ, plan.nqi, plan.qmaxlen, plan.kzmax,
                                   fused_lds(eng, ((plan.off_zs + (size_t)plan.kzmax * eng->nj) + 127) & ~(size_t)127));
                 delete eng;
                 return r1 ? r1 : MDP_ENODEV;
