@@ -196,23 +196,29 @@ def bench_future(args, world, rank, dev):
         t = _coll_tensor(torch.tensor([dt], dtype=torch.float64, device=dev), args)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    # The kernel is bound by integer VALU issue (Philox4x32-10: 4 calls per
-    # replicate-year), not by FP64: its roofline is vector-instruction issue,
-    # 256 CUs x 4 SIMDs x one wave64 VALU instruction per 2 cycles at 2.4 GHz
-    # (MI355X_MICROARCH.md), against the VALU instructions per launch counted
-    # by rocprofv3 (SQ_INSTS_VALU, profiles/pmc_valu_cfg5.json) for the
-    # same replicate count.  The FP64 work the model itself needs (n^2
-    # colonisation-sum adds + n source adds + n products c*s1 per
-    # replicate-year, simpij future.c:64-110) is reported beside it.
+    # The kernel is bound by VALU issue (Philox4x32-10: 4 calls per
+    # replicate-year, 19 v_mad_u64_u32 each), not by FP64.  Its roofline is
+    # SIMD issue cycles: the VALU instructions per launch counted by
+    # rocprofv3 per class (profiles/pmc_valu_cfg5.json) priced at their
+    # measured issue cost (v_mad_u64_u32 8 cycles, FP64 4, 32-bit 2:
+    # scripts/ubench/int_rates.hip, scripts/pmc_valu.py), against 256 CUs x
+    # 4 SIMDs x 2.4 GHz.  The plain instruction count against one wave64
+    # instruction per 2 cycles (what round 1 reported) and the FP64 work the
+    # model itself needs (n^2 colonisation-sum adds + n source adds + n
+    # products c*s1 per replicate-year, simpij future.c:64-110) are reported
+    # beside it.
     n = row.size
     flop_per_ry = n * n + 2 * n + n
-    valu_issue_peak = 256 * 4 * 2.4e9 / 2 / 1e9  # G wave-instructions/s
-    achieved, valu_src = None, None
+    issue_peak = 256 * 4 * 2.4e9 / 1e9  # G SIMD issue cycles/s
+    valu_issue_peak = issue_peak / 2  # G wave-instructions/s at 2 cycles each
+    achieved = insts = None
+    valu_src = None
     vf = ROOT / "profiles" / "pmc_valu_cfg5.json"
     if vf.exists():
         pv = json.loads(vf.read_text())
-        if pv.get("replicates") == r1 - r0 and pv.get("years") == tfut:
-            achieved = pv["valu_insts_per_launch"] / (kms * 1e-3) / 1e9
+        if pv.get("replicates") == r1 - r0 and pv.get("years") == tfut and "issue_cycles_per_launch" in pv:
+            achieved = pv["issue_cycles_per_launch"] / (kms * 1e-3) / 1e9
+            insts = pv["valu_insts_per_launch"] / (kms * 1e-3) / 1e9
             valu_src = str(vf.relative_to(ROOT))
     result = {
         "metric": "replicate-year simulations/sec (MIDASPOM_future ensemble)",
@@ -226,10 +232,13 @@ def bench_future(args, world, rank, dev):
                    "patches": int(n), "replicates": nsim, "years": tfut,
                    "parallelism": f"replicate ranges x{world}" + (", RCCL reduce" if world > 1 else "")},
         "kernel_ms": {"k_future": kms},
-        "roofline": {"kernel": "k_future", "bound": "valu-issue", "compute_unit": "VALU issue (Philox integer work)",
-                     "achieved": achieved, "peak": valu_issue_peak, "unit": "G VALU wave-instructions/s",
-                     "frac": achieved / valu_issue_peak if achieved else None, "traffic": None,
+        "roofline": {"kernel": "k_future", "bound": "valu-issue",
+                     "compute_unit": "VALU issue cycles (Philox integer work), instructions priced by class",
+                     "achieved": achieved, "peak": issue_peak, "unit": "G SIMD issue cycles/s",
+                     "frac": achieved / issue_peak if achieved else None, "traffic": None,
                      "valu_source": valu_src,
+                     "valu_insts_rate": insts, "valu_insts_peak": valu_issue_peak,
+                     "valu_insts_frac": insts / valu_issue_peak if insts else None,
                      "fp64_tflops": flop_per_ry * (r1 - r0) * tfut / (kms * 1e-3) / 1e12,
                      "flop_per_replicate_year": flop_per_ry},
         "cpu_baseline": None,
