@@ -1826,7 +1826,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
                         (void *)&ctab, (void *)&ctl,    (void *)&kmax};
         const uint64_t gy = (d.ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
         const uint32_t fc = d.fused ? (uint32_t)eng->jit_plan.fused_cols : 1u;
-        const uint64_t nb = d.fused ? (d.nc + fc - 1) / fc : gy * d.nc;
+        const uint64_t nb = gy * ((d.nc + fc - 1) / fc);  // e blocks x column groups
         if (nb * kBlock * fc > 0xffffffffull)
             return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
         const uint32_t dyn = d.fused ? (d.ct_len + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch

@@ -147,7 +147,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                  : "    const u32 lb = blockIdx.x + 0 * full;\n") <<
          // FC columns per workgroup (fused variant): KBLOCK threads each
          "    const u32 half = threadIdx.x / KBLOCK, tid = threadIdx.x % KBLOCK;\n"
-         "    const u32 ic0 = FC == 1 ? lb % nc : lb * FC, by = FC == 1 ? lb / nc : 0u;\n"
+         // (column group, e block): FC columns x KBLOCK*EPL e values per workgroup
+         "    const u32 ncb = (nc + FC - 1) / FC, ic0 = lb % ncb * FC, by = lb / ncb;\n"
          "    const u32 ic = ic0 + half;\n"
          "    const double *Qh = Ql + half * LDQ;\n"
          // this lane's e values: issued first, their latency hides under the prologue

@@ -333,18 +333,22 @@ def test_direct_and_generic_paths_agree(golden, monkeypatch, fname, s):
     assert_loglik_close(a, b, atol=1e-11)
 
 
-@pytest.mark.parametrize("fname,s", [("config2_64x50.txt", 200), ("config3_256x200.txt", 64)])
-def test_fused_and_qrows_identical(golden, monkeypatch, fname, s):
+@pytest.mark.parametrize("fname,ne,nc", [("config2_64x50.txt", 200, 200), ("config3_256x200.txt", 64, 64),
+                                          ("config2_64x50.txt", 1100, 37), ("config3_256x200.txt", 700, 33)])
+def test_fused_and_qrows_identical(golden, monkeypatch, fname, ne, nc):
     """The fused forward kernel runs k_qrows' arithmetic for its column: the
-    two direct variants agree bit for bit."""
+    two direct variants agree bit for bit (also with several e blocks per
+    column for the Q-row variant; config 3's tables do not fit the fused
+    kernel's LDS, so there both runs take k_qrows)."""
     model = mdp.Model.load(golden / fname)
-    g, _ = mdp.grid(s)
-    out = []
-    for mode in ("1", "0"):
+    e, _ = mdp.grid(ne)
+    c, _ = mdp.grid(nc)
+    out = {}
+    for mode in ("0", "1"):
         monkeypatch.setenv("MDP_FUSED", mode)
         with mdp.Engine(model) as eng:
-            out.append(eng.loglik_grid(g, g))
-    assert np.array_equal(out[0], out[1])
+            out[mode] = eng.loglik_grid(e, c)
+    assert np.array_equal(out["1"], out["0"])
 
 
 def test_explicit_device_list(golden):
