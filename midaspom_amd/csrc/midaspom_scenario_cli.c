@@ -198,9 +198,14 @@ int main(int argc, char **argv)
         const int ndev = mdp_device_count() > 0 ? mdp_device_count() : 1;
         for (int r = 0; r < ngpu; ++r) sl[r].dev = r % ndev;
     }
-    for (int r = 1; r < ngpu; ++r) pthread_create(&th[r], NULL, run_slab, &sl[r]);
+    char *started = calloc((size_t)ngpu, 1);
+    for (int r = 1; r < ngpu; ++r) started[r] = pthread_create(&th[r], NULL, run_slab, &sl[r]) == 0;
     run_slab(&sl[0]);
-    for (int r = 1; r < ngpu; ++r) pthread_join(th[r], NULL);
+    for (int r = 1; r < ngpu; ++r) {
+        if (started[r]) pthread_join(th[r], NULL);
+        else run_slab(&sl[r]);  // no thread: this slab runs here, after the others
+    }
+    free(started);
     for (int r = 0; r < ngpu; ++r)
         if (sl[r].rc != MDP_OK) {
             fprintf(stderr, "midaspom: %s\n", sl[r].err);
