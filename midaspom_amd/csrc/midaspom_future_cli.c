@@ -7,7 +7,12 @@
  * replicate loop runs on the GPU through mdp_future_simulate.
  *
  * Extensions (the reference has no other way to set them):
- *   -g <id>    GPU (default 0)
+ *   -g <N>     GPUs (or MIDASPOM_GPUS=N): the replicates in N contiguous
+ *              ranges (remainder to the first, the MIDASPOM_future_MPI.out
+ *              partition, future_MPI.c:376-383), one host thread and engine
+ *              per range, the ranges dealt round-robin over the visible GPUs;
+ *              replicate r draws from the stream addressed by (seed, r), so
+ *              the counts do not depend on N
  *   -r <seed>  generator seed; default time(NULL) like srand(time(NULL))
  *              (:345), or $MIDASPOM_SEED.  The draws are Philox streams, not
  *              glibc rand(): runs are reproducible per seed and agree with
@@ -15,6 +20,7 @@
  */
 #include <ctype.h>
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <time.h>
@@ -22,11 +28,36 @@
 
 #include "midaspom.h"
 
+struct range {
+    const int32_t *pend;
+    const double *post;
+    uint32_t n, necstep, tfut;
+    double mdisp, d, KD, KS, dS;
+    int dev;
+    unsigned long long seed;
+    uint64_t rep0, nrep;
+    uint64_t *cnt;  /* [tfut] */
+    int rc;
+    char err[256];
+};
+
+static void *run_range(void *arg)
+{
+    struct range *r = arg;
+    mdp_future *f = NULL;
+    r->rc = mdp_future_create(r->pend, r->n, r->post, r->necstep, r->mdisp, r->d, r->KD, r->KS, r->dS, r->dev, &f);
+    if (r->rc == MDP_OK && r->nrep) r->rc = mdp_future_simulate(f, r->seed, r->rep0, r->nrep, r->tfut, r->cnt);
+    if (r->rc != MDP_OK) snprintf(r->err, sizeof r->err, "%s", mdp_last_error());
+    mdp_future_destroy(f);
+    return NULL;
+}
+
 int main(int argc, char **argv)
 {
     printf("------MIDASPOM, beta MPI version -------\n-> N. Alcala, E. M. Cole, N. A. Rosenberg  <-\n");
     time_t start, end;
-    int tfut = 50, nsimul = 10000, dev = 0;
+    int tfut = 50, nsimul = 10000, ngpu = 1;
+    if (getenv("MIDASPOM_GPUS")) ngpu = atoi(getenv("MIDASPOM_GPUS"));
     double KS = 0, dS = 200, KD = 1, mdisp = 400.0, d = 200;
     float prioroc = 0.5f;
     const char *finame = "posterior.txt", *fname = "input.txt", *fout = "pext_future.txt";
@@ -47,7 +78,7 @@ int main(int argc, char **argv)
         case 'S': KS = atof(optarg); break;
         case 's': dS = atof(optarg); break;
         case 'D': KD = atof(optarg); break;
-        case 'g': dev = atoi(optarg); break;
+        case 'g': ngpu = atoi(optarg); break;
         case 'r': seed = strtoull(optarg, NULL, 0); break;
         case '?':
             if (optopt == 'c')
@@ -119,19 +150,37 @@ int main(int argc, char **argv)
     int *lik = calloc(tfut > 0 ? (size_t)tfut : 1, sizeof(int));
     time(&start);
     printf("Starting likelihood computation\n");
-    mdp_future *f = NULL;
-    int rc = mdp_future_create(pend, n, post, necstep, mdisp, d, KD, KS, dS, dev, &f);
-    if (rc == MDP_OK && tfut > 0 && nsimul > 0) {
-        uint64_t *cnt = calloc((size_t)tfut, sizeof(uint64_t));
-        rc = mdp_future_simulate(f, seed, 0, (uint64_t)nsimul, (uint32_t)tfut, cnt);
-        for (int t = 0; t < tfut; ++t) lik[t] = (int)cnt[t];
-        free(cnt);
+    int rc = MDP_OK;
+    if (tfut > 0 && nsimul > 0) {
+        if (ngpu < 1) ngpu = 1;
+        if (ngpu > nsimul) ngpu = nsimul;
+        const int ndev = mdp_device_count() > 0 ? mdp_device_count() : 1;
+        struct range *rg = calloc((size_t)ngpu, sizeof *rg);
+        pthread_t *th = calloc((size_t)ngpu, sizeof *th);
+        char *started = calloc((size_t)ngpu, 1);
+        const uint64_t avg = (uint64_t)nsimul / (uint64_t)ngpu, rem = (uint64_t)nsimul % (uint64_t)ngpu;
+        for (int r = 0; r < ngpu; ++r) {
+            const uint64_t r0 = r == 0 ? 0 : (uint64_t)r * avg + rem, r1 = (uint64_t)(r + 1) * avg + rem;
+            rg[r] = (struct range){pend, post, n, necstep, (uint32_t)tfut, mdisp, d, KD, KS, dS, r % ndev, seed,
+                                   r0, r1 - r0, calloc((size_t)tfut, sizeof(uint64_t)), 0, ""};
+        }
+        for (int r = 1; r < ngpu; ++r) started[r] = pthread_create(&th[r], NULL, run_range, &rg[r]) == 0;
+        run_range(&rg[0]);
+        for (int r = 1; r < ngpu; ++r) {
+            if (started[r]) pthread_join(th[r], NULL);
+            else run_range(&rg[r]);  // no thread: this range runs here, after the others
+        }
+        for (int r = 0; r < ngpu; ++r) {
+            if (rg[r].rc != MDP_OK && rc == MDP_OK) {
+                rc = rg[r].rc;
+                fprintf(stderr, "GPU future simulation failed: %s\n", rg[r].err);
+            }
+            for (int t = 0; t < tfut; ++t) lik[t] += (int)rg[r].cnt[t];
+            free(rg[r].cnt);
+        }
+        free(rg), free(th), free(started);
     }
-    mdp_future_destroy(f);
-    if (rc != MDP_OK) {
-        fprintf(stderr, "GPU future simulation failed: %s\n", mdp_last_error());
-        return 1;
-    }
+    if (rc != MDP_OK) return 1;
     printf("end likelihood computation\n");
     printf("Writing on file %s... ", fout);
     FILE *fe = fopen(fout, "wb");

@@ -152,3 +152,76 @@ def test_scenario_cli_multi_gpu_slabs(golden, tmp_path, kind):
         assert r.returncode == 0, (tag, r.stderr[-2000:])
         outs[tag] = (tmp_path / f"{tag}.txt").read_bytes()
     assert outs["c3"] == outs["c1"] and outs["c99"] == outs["c1"] and outs["py3"] == outs["c1"]
+
+
+# ---------------------------------------------------------------------------
+# MIDASPOM_future: python -m midaspom_amd.future vs the compiled drop-in, the
+# torchrun form of MIDASPOM_future_MPI.out, and -g N replicate ranges
+# ---------------------------------------------------------------------------
+FUT_FLAGS = ["-a", "20", "-m", "400", "-d", "100", "-S", "1", "-s", "200", "-n", "30001", "-r", "123"]
+
+
+@pytest.fixture(scope="module")
+def fut_post(tmp_path_factory, golden):
+    import oracle  # the posterior the future program reads (CPU oracle, s = 101)
+
+    p = tmp_path_factory.mktemp("fut") / "posterior.txt"
+    oracle.run(golden / "occupancies.txt", p, m=400, d=100, s=101)
+    return str(p)
+
+
+def test_python_future_cli_matches_compiled(golden, tmp_path, fut_post):
+    """Same stdout lines and file bytes (fixed seed) as the compiled
+    midaspom_future."""
+    (tmp_path / "py").mkdir()
+    (tmp_path / "c").mkdir()
+    inp = str(golden / "occupancies.txt")
+    rp = subprocess.run([sys.executable, "-m", "midaspom_amd.future", *FUT_FLAGS, "-i", inp, "-q", fut_post,
+                         "-o", "pext.txt"], capture_output=True, text=True, timeout=180, env=_env(),
+                        cwd=tmp_path / "py")
+    assert rp.returncode == 0, rp.stderr
+    rc = subprocess.run([str(_lib.FUTURE_CLI_PATH), *FUT_FLAGS, "-i", inp, "-q", fut_post, "-o", "pext.txt"],
+                        capture_output=True, text=True, timeout=180, cwd=tmp_path / "c")
+    assert rc.returncode == 0, rc.stderr
+    assert (tmp_path / "py" / "pext.txt").read_bytes() == (tmp_path / "c" / "pext.txt").read_bytes()
+    assert _scn_strip(rp.stdout) == _scn_strip(rc.stdout)
+    vals = [int(x) for x in (tmp_path / "c" / "pext.txt").read_text().split("\t")[:-1]]
+    assert len(vals) == 20 and all(0 <= v <= 30001 for v in vals)
+
+
+def test_torchrun_future_two_ranks(golden, tmp_path, fut_post):
+    """The MIDASPOM_future_MPI.out shape: replicate ranges over 2 ranks, one
+    sum-reduce; the file equals the single-process one byte for byte."""
+    inp = str(golden / "occupancies.txt")
+    single, multi = tmp_path / "single.txt", tmp_path / "multi.txt"
+    r1 = subprocess.run([sys.executable, "-m", "midaspom_amd.future", *FUT_FLAGS, "-i", inp, "-q", fut_post,
+                         "-o", str(single)], capture_output=True, text=True, timeout=180, env=_env(), cwd=ROOT)
+    assert r1.returncode == 0, r1.stderr
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "midaspom_amd.future", "--backend", "gloo", *FUT_FLAGS, "-i", inp, "-q", fut_post,
+           "-o", str(multi)]
+    r2 = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    assert multi.read_bytes() == single.read_bytes()
+    out = r2.stdout
+    assert out.count("beta MPI version") == 1 and out.count("npstates = ") == 2
+    for r in (1, 2):
+        assert f"Starting parallel likelihood computation process {r}/2\n" in out
+        assert f"end likelihood computation process {r}/2\n" in out
+    assert "Sending data (proc 1)... " in out and "Gathering data from 1 proc... " in out
+    assert out.count("Migration matrix:") == 1 and out.count("Writing on file") == 1
+
+
+def test_future_cli_multi_gpu_ranges(golden, tmp_path, fut_post):
+    """-g N: replicate ranges, one thread + engine each; the counts do not
+    depend on N (addressed draws), for the compiled CLI and the Python one."""
+    inp = str(golden / "occupancies.txt")
+    outs = {}
+    for tag, cmd in {"c1": [str(_lib.FUTURE_CLI_PATH), "-g", "1"], "c3": [str(_lib.FUTURE_CLI_PATH), "-g", "3"],
+                     "py4": [sys.executable, "-m", "midaspom_amd.future", "-g", "4"]}.items():
+        r = subprocess.run([*cmd, *FUT_FLAGS, "-i", inp, "-q", fut_post, "-o", str(tmp_path / f"{tag}.txt")],
+                           capture_output=True, text=True, timeout=180, env=_env(), cwd=ROOT)
+        assert r.returncode == 0, (tag, r.stderr[-2000:])
+        outs[tag] = (tmp_path / f"{tag}.txt").read_bytes()
+    assert outs["c3"] == outs["c1"] and outs["py4"] == outs["c1"]
