@@ -40,3 +40,28 @@ def test_problem_dump_mpi_nextid_position():
     lines.clear()
     cli._print_problem(model, lambda t, all_ranks=False: lines.append((t, all_ranks)), mpi=False)
     assert not any(t.startswith("nextid=") for t, _ in lines)
+
+
+def test_future_completions_and_priors():
+    """`python -m midaspom_amd.future` prints the last survey's completions
+    the way the drop-in does (future.c:286-332): the first missing patch is
+    the most significant bit, pr is float arithmetic times a double."""
+    from midaspom_amd import future
+
+    np_, comps = future._completions(np.array([1, -1, 0, -1]), 0.3)
+    assert np_ == 4
+    assert [v for v, _ in comps] == [[1, 0, 0, 0], [1, 0, 0, 1], [1, 1, 0, 0], [1, 1, 0, 1]]
+    f07 = float(np.float32(0.7))  # (float)(1 - bit) * (1 - prioroc) with prioroc = 0.3f
+    f03 = float(np.float32(0.3))
+    assert [p for _, p in comps] == [f07 * f07, f07 * f03, f03 * f07, f03 * f03]
+    assert future._completions(np.array([0, 1]), 0.5) == (1, [([0, 1], 1.0)])
+
+
+def test_future_args_defaults():
+    """The code defaults of main_MIDASPOM_future.c:123-133 (-D 1, not the
+    manual's 0)."""
+    from midaspom_amd import future
+
+    a = future.parse_args([])
+    assert (a.n, a.a, a.m, a.p, a.d, a.S, a.s, a.D) == (10000, 50, 400.0, 0.5, 200.0, 0.0, 200.0, 1.0)
+    assert (a.q, a.i, a.o) == ("posterior.txt", "input.txt", "pext_future.txt")
