@@ -14,6 +14,7 @@ when Ltot == 0 (:527).
 from __future__ import annotations
 
 import argparse
+import os
 import sys
 import time
 
@@ -29,6 +30,9 @@ def parse_args(argv):
     ap.add_argument("-s", type=int, default=101, help="grid steps")
     ap.add_argument("-l", type=float, default=0.0, help="lower bound")
     ap.add_argument("-u", type=float, default=1.0, help="upper bound")
+    ap.add_argument("-g", type=int, default=None,
+                    help="GPUs of this process (single process; default MIDASPOM_GPUS or the current device), "
+                         "as the compiled midaspom's -g")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl)")
     return ap.parse_args(argv)
 
@@ -90,7 +94,8 @@ def main(argv=None) -> int:
 
     if world == 1:
         out("Starting parallel likelihood computation\n")
-        with mdp.Engine(model) as eng:
+        ngpu = a.g if a.g is not None else int(os.environ.get("MIDASPOM_GPUS", "0"))
+        with mdp.Engine(model, n_devices=max(0, ngpu)) as eng:  # 0: the current device
             lik = eng.loglik_grid(g, g)
         for ie in range(a.s):  # ((float)ie+1)*100.0/nstep, exact in double (:394)
             out(f"{(ie + 1) * 100.0 / a.s:.2f}% done\n")

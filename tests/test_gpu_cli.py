@@ -46,7 +46,7 @@ def test_python_cli_matches_compiled_cli(golden, tmp_path):
     (tmp_path / "py").mkdir()
     (tmp_path / "c").mkdir()
     inp = str(golden / "occupancies.txt")
-    rp = subprocess.run([sys.executable, "-m", "midaspom_amd", *FLAGS, "-i", inp, "-o", "post.txt"],
+    rp = subprocess.run([sys.executable, "-m", "midaspom_amd", *FLAGS, "-g", "1", "-i", inp, "-o", "post.txt"],
                         capture_output=True, text=True, timeout=180, env=_env(), cwd=tmp_path / "py")
     assert rp.returncode == 0, rp.stderr
     rc = subprocess.run([str(_lib.CLI_PATH), *FLAGS, "-i", inp, "-o", "post.txt"],
