@@ -59,3 +59,21 @@ def test_cli_unknown_option():
     assert r.returncode == 1
     assert "Unknown option `-z'." in r.stderr
     assert r.stdout.startswith("------ MIDASPOM, beta version ------\n")
+
+
+def test_scenario_and_future_cli_argument_errors(tmp_path):
+    """The other drop-ins' argument handling (no GPU needed): unknown option
+    -> the getopt message and exit 1; dieoff / loss without -a -e -c -> exit 1
+    (quirk Q11); a missing input file -> exit 1 with its name."""
+    for exe in (_lib.DIEOFF_CLI_PATH, _lib.LOSS_CLI_PATH, _lib.FUTURE_CLI_PATH):
+        r = subprocess.run([str(exe), "-z"], capture_output=True, text=True)
+        assert r.returncode == 1 and "Unknown option `-z'." in r.stderr, exe
+        assert "beta" in r.stdout.splitlines()[0]
+    for exe in (_lib.DIEOFF_CLI_PATH, _lib.LOSS_CLI_PATH):
+        r = subprocess.run([str(exe), "-e", "0.3", "-c", "0.4"], capture_output=True, text=True)
+        assert r.returncode == 1 and "-a" in r.stderr
+        r = subprocess.run([str(exe), "-a", "1", "-e", "0.3", "-c", "0.4", "-i", str(tmp_path / "none.txt")],
+                           capture_output=True, text=True)
+        assert r.returncode == 1 and "none.txt" in r.stderr
+    r = subprocess.run([str(_lib.FUTURE_CLI_PATH), "-i", str(tmp_path / "none.txt")], capture_output=True, text=True)
+    assert r.returncode == 1
