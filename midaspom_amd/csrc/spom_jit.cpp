@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <sstream>
 #include <algorithm>
@@ -77,7 +78,8 @@ void write_file(const std::string &dir, const std::string &path, const std::vect
     std::string parent = dir.substr(0, dir.find_last_of('/'));
     mkdir(parent.c_str(), 0755);
     mkdir(dir.c_str(), 0755);
-    std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+    static std::atomic<unsigned> seq{0};  // threads of one process write distinct temporaries
+    std::string tmp = path + ".tmp" + std::to_string((long)getpid()) + "." + std::to_string(seq++);
     FILE *f = fopen(tmp.c_str(), "wb");
     if (!f) return;
     const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
