@@ -10,6 +10,7 @@ Tolerances (written here, per BASELINE north_star / SURVEY.md §8(c)):
 """
 from __future__ import annotations
 
+import os
 import subprocess
 
 import numpy as np
@@ -147,7 +148,36 @@ def engine_path(request, monkeypatch):
     return request.param
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MDP_FUZZ_LARGE", "24"))))  # more: a longer fuzz
+def test_random_problems_large_grids(seed, monkeypatch):
+    """Random problems on grids the small fuzz never reaches: several e
+    blocks per column (ne > 512), odd and large nc (k_qrows with 1, 2 or 4 c
+    values per workgroup), |c| > 1 for some.  The fused and Q-row variants
+    must agree bit for bit on the whole grid, and both with the oracle at a
+    sample of points."""
+    rng = np.random.default_rng(5000 + seed)
+    n = int(rng.integers(2, 40))
+    nvar = int(rng.integers(1, min(n, 9) + 1))
+    T = int(rng.integers(2, 30))
+    obs = synth.random_obs(rng, n, T, nvar, pmiss=float(rng.choice([0.0, 0.1, 0.3])),
+                           max_missing=int(rng.integers(0, 4)), p1=float(rng.uniform(0.2, 0.8)))
+    m, d, p = float(rng.choice([100, 400])), float(rng.choice([50, 100, 200])), 0.5
+    ne, nc = int(rng.integers(300, 1400)), int(rng.integers(1, 1300))
+    e, _ = mdp.grid(ne, 0.0, float(rng.choice([1.0, 1.2])))
+    c, _ = mdp.grid(nc, 0.0, float(rng.choice([1.0, 1.5])))
+    model = mdp.Model.from_obs(obs, m=m, p=p, d=d)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MDP_FUSED", mode)
+        out[mode] = gpu_grid(model, e, c)
+    assert np.array_equal(out["1"], out["0"], equal_nan=True)
+    ie = np.unique(np.r_[0, ne - 1, rng.integers(0, ne, 6)])
+    ic = np.unique(np.r_[0, nc - 1, rng.integers(0, nc, 6)])
+    ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e[ie], c[ic])
+    assert_loglik_close(out["0"][np.ix_(ie, ic)], ref)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MDP_FUZZ_SMALL", "24"))))  # more: a longer fuzz
 def test_random_problems(seed, engine_path):
     rng = np.random.default_rng(1000 + seed)
     n = int(rng.integers(2, 48))
