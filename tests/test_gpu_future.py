@@ -6,6 +6,7 @@ falls past the last cell, missing-data initial states, source / K_D
 scenarios, NaN posteriors, 8..64 patches and any replicate split."""
 from __future__ import annotations
 
+import os
 import subprocess
 
 import numpy as np
@@ -139,3 +140,26 @@ def test_future_cli_layout(golden, tmp_path):
     ref = oracle.future_counts(row, oracle.read_posterior(post), tfut=10, nrep=10000, seed=123, m=400, d=100,
                                KS=1, dS=200)
     assert vals == [int(x) for x in ref]
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MDP_FUZZ_FUT", "8"))))  # more: a longer fuzz
+def test_random_futures(seed):
+    """Random last surveys (1-64 patches, missing data), random posteriors
+    (2-101 steps, sparse or flat, some exact zeros), rates K_D / K_S / d_S,
+    horizons and replicate offsets: the GPU counts equal the oracle's under
+    the same addressed Philox stream, count for count."""
+    rng = np.random.default_rng(9000 + seed)
+    n = int(rng.choice([1, 3, 8, 12, 20, 40, 64]))
+    row = rng.choice([-1, 0, 1], size=n, p=[0.15, 0.45, 0.4]).astype(np.int32)
+    if rng.random() < 0.3:
+        row[rng.integers(0, n)] = 1  # never all empty at the start
+    s = int(rng.choice([2, 5, 21, 101]))
+    post = rng.random((s, s)) ** float(rng.choice([1.0, 8.0]))
+    post[rng.random((s, s)) < 0.3] = 0.0
+    kw = dict(m=float(rng.choice([100.0, 400.0])), d=float(rng.choice([50.0, 200.0])),
+              KD=float(rng.choice([0.0, 0.5, 1.0, 3.0])), KS=float(rng.choice([0.0, 0.5, 2.0])),
+              dS=float(rng.choice([50.0, 200.0, 1000.0])))
+    nrep, tfut = int(rng.integers(1, 5000)), int(rng.integers(1, 60))
+    got, ref = _both(row, post, nrep, tfut, seed=int(rng.integers(0, 2 ** 40)),
+                     rep0=int(rng.integers(0, 10 ** 6)), **kw)
+    assert np.array_equal(got, ref), (seed, got, ref)

@@ -7,6 +7,7 @@ L > 1e-14, absolute 1e-20 below (the %.20lf print floor of the reference's
 output is ~1e-20)."""
 from __future__ import annotations
 
+import os
 import subprocess
 from pathlib import Path
 
@@ -66,13 +67,21 @@ def test_examples_input_grid_vs_oracle(golden, kind):
             close(got[ie, ic], ref)
 
 
-@pytest.mark.parametrize("seed", range(6))
-def test_random_rows(seed):
+@pytest.mark.parametrize("kernel", ["lds", "big"])
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MDP_FUZZ_SCN", "8"))))  # more: a longer fuzz
+def test_random_rows(seed, kernel, monkeypatch):
+    """Random first rows (n <= 8, missing patches), rates, K / source grids,
+    ts and tdis (0 included) and e counts across the 32-value e chunks, on
+    the LDS kernel and on k_scn_big (MDP_SCN_BIG=1), against the oracle."""
+    if kernel == "big":
+        monkeypatch.setenv("MDP_SCN_BIG", "1")
+    else:
+        monkeypatch.delenv("MDP_SCN_BIG", raising=False)
     rng = np.random.default_rng(500 + seed)
     n = int(rng.integers(1, 9))
     row = rng.choice([-1, 0, 1], size=n, p=[0.2, 0.4, 0.4]).astype(np.int32)
     kind = "loss" if seed % 2 else "dieoff"
-    e = rng.uniform(0.0, 1.2, 3)
+    e = rng.uniform(0.0, 1.2, int(rng.choice([1, 3, 33, 70])))
     c = rng.uniform(0.0, 1.5, 2)
     K = mdp.kgrid(4, 0.2, 30.0)
     d = np.array([150.0, 900.0])
@@ -80,7 +89,7 @@ def test_random_rows(seed):
     m, dd, p = float(rng.choice([100, 400])), float(rng.choice([50, 200])), float(rng.choice([0.5, 0.3]))
     with mdp.Scenario(row, kind, m=m, p=p, d=dd) as sc:
         got = sc.lik(e, c, K, d, ts=ts, tdis=tdis)
-    for ie in range(e.size):
+    for ie in sorted({0, e.size - 1, int(rng.integers(0, e.size))}):
         for ic in range(c.size):
             if kind == "dieoff":
                 ref = oracle.dieoff_lik(row, K, e[ie], c[ic], ts=ts, tdis=tdis, m=m, p=p, d=dd)
