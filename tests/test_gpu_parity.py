@@ -235,6 +235,30 @@ def test_wide_years_vs_oracle(missing):
     assert_loglik_close(got, ref)
 
 
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MDP_FUZZ_WIDE", "6"))))  # more: a longer fuzz
+def test_random_wide_problems(seed, monkeypatch):
+    """Random problems with 5-7 missing patches in random years (32-128
+    states) and random dispersal / grid bounds, on the wide path (whole
+    launches and one c value per launch) against the oracle."""
+    rng = np.random.default_rng(7000 + seed)
+    n, T = int(rng.integers(8, 16)), int(rng.integers(2, 7))
+    years = rng.choice(T, size=int(rng.integers(1, 3)), replace=False)
+    missing = {int(y): int(rng.integers(5, 8)) for y in years}
+    obs = _wide_obs(rng, n, T, missing)
+    m, d, p = float(rng.choice([100, 400])), float(rng.choice([50, 100, 200])), float(rng.choice([0.5, 0.3]))
+    model = mdp.Model.from_obs(obs, m=m, p=p, d=d)
+    e, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.2])))
+    c, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.5])))
+    ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c, threads=16)
+    for cb in (None, "1"):
+        if cb:
+            monkeypatch.setenv("MDP_WIDE_CB", cb)
+        with mdp.Engine(model) as eng:
+            assert eng.info()["variant"] >= 20000
+            got = eng.loglik_grid(e, c)
+        assert_loglik_close(got, ref)
+
+
 def test_wide_survey_series_sampled(tmp_path):
     """A survey-like series (the Appendix C generator, config-2 shape, 45 %
     of the variable patches unvisited in each year: 2-64 states per year,
