@@ -44,6 +44,8 @@ constexpr uint32_t kMaxN = 8;          // k_scn: 2 x 2^8 x 32 state values + fac
 constexpr uint32_t kBigMaxN = 16;      // k_scn_big: state vectors in HBM
 constexpr int kBigBlock = 256;
 constexpr size_t kBigScratch = 1ull << 30;  // k_scn_big state-vector scratch per launch (bytes)
+constexpr int kRowBlock = 256;              // k_scn_row: one grid point per workgroup
+constexpr uint32_t kRowMaxN = 12;           // k_scn_row: 2 x 2^n states + 3 n x 256 per-lane values in LDS
 
 #define SCN_TRY(expr)                                                                        \
     do {                                                                                     \
@@ -516,6 +518,116 @@ __global__ __launch_bounds__(kBigBlock) void k_scn_big(ScnArgs a, const double *
     out[pt] = L;
 }
 
+// 8 < n <= 12 (the reference's dieoff / loss on larger first rows,
+// dieoff.c:238, loss.c:222, typically one (e, c) and a K grid): one workgroup
+// per grid point, its two state vectors in LDS, the 256 threads over the rows
+// j.  A row is k_scn_big's contraction -- the supersets of j stream past in
+// ascending order and are reduced as a binary tree over the free patches,
+// lowest state bit innermost -- with the level factors and parked left
+// children in per-thread LDS columns (the level index differs between lanes).
+// Rows are dealt round-robin in order of decreasing free-patch count (jord),
+// so every thread starts with one of the heavy rows.  Extinction: n in-place
+// pair passes, threads over the pairs, a barrier per pass.  Same operator
+// order and sums as k_scn_big.
+__global__ __launch_bounds__(kRowBlock) void k_scn_row(ScnArgs a, const double *__restrict__ S,
+                                                       const double *__restrict__ y0src,
+                                                       const double *__restrict__ ev, const double *__restrict__ cv,
+                                                       const double *__restrict__ Kv, const double *__restrict__ srcv,
+                                                       const uint32_t *__restrict__ jord, size_t p0,
+                                                       double *__restrict__ out)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const uint32_t n = a.n, NS = 1u << n, tid = threadIdx.x;
+    double *ya = lds, *yb = lds + NS;
+    double *accs = lds + 2 * NS;                 // [n][kRowBlock] parked left children
+    double *w0s = accs + (size_t)n * kRowBlock;  // [n][kRowBlock] 1 - pC per level
+    double *w1s = w0s + (size_t)n * kRowBlock;   // [n][kRowBlock] pC per level
+    const size_t pt = p0 + blockIdx.x;
+    // mode 0: pt = ic ne + ie (v per (c, e)); mode 1: the output order
+    uint32_t ie, ic, iK = 0, id = 0;
+    if (a.mode) {
+        id = (uint32_t)(pt % a.nd);
+        iK = (uint32_t)((pt / a.nd) % a.nK);
+        ic = (uint32_t)((pt / ((size_t)a.nd * a.nK)) % a.nc);
+        ie = (uint32_t)(pt / ((size_t)a.nd * a.nK * a.nc));
+    } else {
+        ic = (uint32_t)(pt / a.ne);
+        ie = (uint32_t)(pt % a.ne);
+    }
+    const double c = cv[ic], K = a.mode ? Kv[iK] : 1.0;
+    const double *src = a.mode && a.loss ? srcv + (size_t)id * n : nullptr;
+    const double Kpc = a.mode && !a.loss ? K : 1.0;
+    double E = a.mode && !a.loss ? ev[ie] / K : ev[ie];  // dieoff.c:56-57 E = e/K; loss.c:57 E = e
+    E = E > 1.0 ? 1.0 : E;
+    const double E1 = 1.0 - E;
+    for (uint32_t st = tid; st < NS; st += kRowBlock)
+        ya[st] = a.mode ? y0src[((size_t)ic * NS + st) * a.ne + ie] : y0src[st];
+    __syncthreads();
+    double *acc = accs + tid, *w0 = w0s + tid, *w1 = w1s + tid;
+    for (int t = 0; t < a.years; ++t) {
+        for (uint32_t r = tid; r < NS; r += kRowBlock) {
+            const uint32_t j = jord[r];
+            const uint32_t F = ~j & (NS - 1), f = __popc(F);
+            {   // level L = the L-th lowest free state bit, patch n - 1 - bit
+                uint32_t fb = F;
+                for (uint32_t L = 0; L < f; ++L) {
+                    const uint32_t k = n - 1 - (uint32_t)__builtin_ctz(fb);
+                    fb &= fb - 1;
+                    const double sv = S[(size_t)j * n + k];
+                    double p = src ? c * (sv + src[k] * K) : c * sv * Kpc;  // dieoff.c:78, loss.c:98
+                    p = p > 1.0 ? 1.0 : p;
+                    w1[L * kRowBlock] = p;
+                    w0[L * kRowBlock] = 1.0 - p;
+                }
+            }
+            double res = 0.0;
+            uint32_t sub = 0;
+            for (uint32_t i = 0;; ++i) {
+                double cur = ya[j | sub];
+                uint32_t L = 0;
+                for (; (i >> L) & 1u; ++L) cur = fma(w1[L * kRowBlock], cur, acc[L * kRowBlock]);
+                if (L == f) {
+                    res = cur;
+                    break;
+                }
+                acc[L * kRowBlock] = w0[L * kRowBlock] * cur;
+                sub = (sub - F) & F;
+            }
+            yb[j] = res;
+        }
+        __syncthreads();
+        // extinction, ascending patch: y[s | m] = E y[s] + (1 - E) y[s | m]
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t m = 1u << (n - 1 - k);
+            for (uint32_t q = tid; q < NS / 2; q += kRowBlock) {
+                const uint32_t s1 = ((q & ~(m - 1)) << 1) | m | (q & (m - 1));  // q-th state with bit m set
+                yb[s1] = E * yb[s1 ^ m] + E1 * yb[s1];
+            }
+            __syncthreads();
+        }
+        double *tmp = ya;
+        ya = yb;
+        yb = tmp;
+    }
+    if (!a.mode) {
+        for (uint32_t st = tid; st < NS; st += kRowBlock) out[((size_t)ic * NS + st) * a.ne + ie] = ya[st];
+        return;
+    }
+    // L = sum over the states: per thread a strided partial, then thread 0
+    // adds the 256 partials in order
+    double part = 0.0;
+    for (uint32_t st = tid; st < NS; st += kRowBlock) part += ya[st];
+    acc[0] = part;
+    __syncthreads();
+    if (tid == 0) {
+        double L = 0.0;
+        for (int i = 0; i < kRowBlock; ++i) L += accs[i];
+        out[pt] = L;
+    }
+}
+
+size_t row_lds(uint32_t n) { return (2 * ((size_t)1 << n) + 3 * (size_t)n * kRowBlock) * sizeof(double); }
+
 // instantiation for n patches: NL = min(3, n) lo patches, NH = n - NL
 typedef void (*ScnKernel)(ScnArgs, const double *, const double *, const double *, const double *, const double *,
                           const double *, const uint32_t *, const uint32_t *, double *);
@@ -566,6 +678,9 @@ struct mdp_scenario {
     bool big = false;
     double *dY = nullptr;
     uint32_t big_pts = 0;
+    // k_scn_row (8 < n <= 12, or MDP_SCN_ROW=1): rows by decreasing free-patch count
+    bool row = false;
+    uint32_t *djord = nullptr;
 };
 
 namespace {
@@ -589,6 +704,23 @@ size_t scn_lds(const mdp_scenario *sc)
 // v = P^tdis w (which = 1), L = 1^T PK^ts v (which = 2) or both (3) on stream st
 int scn_launch(mdp_scenario *sc, double *dout, hipStream_t st, int which)
 {
+    if (sc->row) {
+        for (int mode = 0; mode < 2; ++mode) {
+            if (!(which & (1 << mode))) continue;
+            ScnArgs a{sc->n, sc->ns, sc->ne, sc->nc, sc->nK, sc->nd, mode ? sc->ts : sc->tdis, sc->kind, mode, 0, 0};
+            const double *y0 = mode ? sc->dV : sc->dw;
+            double *o = mode ? dout : sc->dV;
+            const size_t tot = mode ? (size_t)sc->ne * sc->nc * sc->nK * sc->nd : (size_t)sc->nc * sc->ne;
+            constexpr size_t kPer = (size_t)1 << 22;  // points per launch (grid of < 2^32 threads)
+            for (size_t p0 = 0; p0 < tot; p0 += kPer) {  // one workgroup per point
+                const uint32_t nb = (uint32_t)std::min(kPer, tot - p0);
+                hipLaunchKernelGGL(k_scn_row, dim3(nb), dim3(kRowBlock), row_lds(sc->n), st, a, sc->dS, y0, sc->de,
+                                   sc->dc, sc->dK, sc->dsr, sc->djord, p0, o);
+            }
+            SCN_TRY(hipGetLastError());
+        }
+        return MDP_OK;
+    }
     if (sc->big) {
         for (int mode = 0; mode < 2; ++mode) {
             if (!(which & (1 << mode))) continue;
@@ -669,8 +801,12 @@ int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, doubl
     sc->d = d;
     sc->device = device;
     // n > 8: the LDS-resident k_scn does not fit; MDP_SCN_BIG=1 forces k_scn_big (tests)
-    const char *bv = getenv("MDP_SCN_BIG");
-    sc->big = n > kMaxN || (bv && atoi(bv) != 0);
+    // 8 < n <= 12: k_scn_row (MDP_SCN_ROW=1 forces it for any n <= 12); n > 12:
+    // k_scn_big (MDP_SCN_BIG=1 forces it for any n)
+    const char *bv = getenv("MDP_SCN_BIG"), *rv = getenv("MDP_SCN_ROW");
+    const bool force_big = bv && atoi(bv) != 0, force_row = rv && atoi(rv) != 0;
+    sc->row = !force_big && n <= kRowMaxN && (n > kMaxN || force_row);
+    sc->big = !sc->row && (n > kMaxN || force_big);
     const uint32_t ns = sc->ns;
     // dispersal M (dieoff.c:238-248) and colonisation sums S[j][k] =
     // sum over l != k, ascending, of M[l][k] * j_l (dieoff.c:72-77)
@@ -714,7 +850,14 @@ int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, doubl
     // 2^NL lo rows each) and the hi-row schedule: rows dealt to the waves by
     // longest-processing-time-first (row jh costs its 2^(f-1) superset
     // pairs, f = NH - |jh|, plus one for its loads and epilogue)
-    if (!sc->big) {
+    std::vector<uint32_t> jord;
+    if (sc->row) {  // rows by decreasing free-patch count (stable: ascending j within a count)
+        jord.resize(ns);
+        for (uint32_t j = 0; j < ns; ++j) jord[j] = j;
+        std::stable_sort(jord.begin(), jord.end(),
+                         [](uint32_t x, uint32_t y) { return __builtin_popcount(x) < __builtin_popcount(y); });
+    }
+    if (!sc->big && !sc->row) {
         const uint32_t nl = scn_nl(n), nh = n - nl, nhi = 1u << nh;
         sc->boff.assign(nhi, 0);
         uint32_t off = 0;
@@ -750,11 +893,16 @@ int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, doubl
         return mdp_set_error(MDP_EHIP, "hipSetDevice(%d) failed", device);
     }
     if ((rc = dev_up(&sc->dS, sc->S)) || (rc = dev_up(&sc->dw, sc->w)) || (rc = dev_up(&sc->dboff, sc->boff)) ||
-        (rc = dev_up(&sc->djsched, sc->jsched)) || hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking) != hipSuccess) {
+        (rc = dev_up(&sc->djsched, sc->jsched)) || (rc = dev_up(&sc->djord, jord)) ||
+        hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking) != hipSuccess) {
         mdp_scenario_destroy(sc);
         return rc ? rc : mdp_set_error(MDP_EHIP, "stream creation failed");
     }
-    if (!sc->big) {
+    if (sc->row) {
+        if (row_lds(n) > 64 * 1024)
+            (void)hipFuncSetAttribute((const void *)k_scn_row, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)row_lds(n));
+    } else if (!sc->big) {
         const size_t lds = scn_lds(sc);
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute((const void *)scn_kernel(n), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -769,7 +917,7 @@ void mdp_scenario_destroy(mdp_scenario *sc)
     (void)hipSetDevice(sc->device);
     if (sc->stream) (void)hipStreamSynchronize(sc->stream);
     scn_free_grid(sc);
-    for (void *p : {(void *)sc->dS, (void *)sc->dw, (void *)sc->dboff, (void *)sc->djsched})
+    for (void *p : {(void *)sc->dS, (void *)sc->dw, (void *)sc->dboff, (void *)sc->djsched, (void *)sc->djord})
         if (p) (void)hipFree(p);
     if (sc->ev0) (void)hipEventDestroy(sc->ev0);
     if (sc->ev1) (void)hipEventDestroy(sc->ev1);

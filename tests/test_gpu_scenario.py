@@ -67,16 +67,15 @@ def test_examples_input_grid_vs_oracle(golden, kind):
             close(got[ie, ic], ref)
 
 
-@pytest.mark.parametrize("kernel", ["lds", "big"])
+@pytest.mark.parametrize("kernel", ["lds", "big", "row"])
 @pytest.mark.parametrize("seed", range(int(os.environ.get("MDP_FUZZ_SCN", "8"))))  # more: a longer fuzz
 def test_random_rows(seed, kernel, monkeypatch):
     """Random first rows (n <= 8, missing patches), rates, K / source grids,
     ts and tdis (0 included) and e counts across the 32-value e chunks, on
-    the LDS kernel and on k_scn_big (MDP_SCN_BIG=1), against the oracle."""
-    if kernel == "big":
-        monkeypatch.setenv("MDP_SCN_BIG", "1")
-    else:
-        monkeypatch.delenv("MDP_SCN_BIG", raising=False)
+    the LDS kernel, k_scn_big (MDP_SCN_BIG=1) and k_scn_row (MDP_SCN_ROW=1),
+    against the oracle."""
+    monkeypatch.setenv("MDP_SCN_BIG", "1" if kernel == "big" else "0")
+    monkeypatch.setenv("MDP_SCN_ROW", "1" if kernel == "row" else "0")
     rng = np.random.default_rng(500 + seed)
     n = int(rng.integers(1, 9))
     row = rng.choice([-1, 0, 1], size=n, p=[0.2, 0.4, 0.4]).astype(np.int32)
@@ -207,15 +206,38 @@ ROW12 = np.array([1, 0, 1, -1, 0, 1, 1, 0, -1, 1, 0, 1], dtype=np.int32)
 @pytest.mark.parametrize("row", [ROW12[:3], ROW12[:6], mdp.first_row(Path(__file__).parent / "golden" / "occupancies.txt")],
                          ids=["n3", "n6", "n8"])
 def test_big_kernel_matches_lds_kernel(monkeypatch, kind, row):
-    """The general kernel forced onto n <= 8 agrees with the LDS kernel."""
+    """The general kernels forced onto n <= 8 (k_scn_big: MDP_SCN_BIG=1;
+    k_scn_row: MDP_SCN_ROW=1) agree with the LDS kernel."""
     e, c = np.array([0.05, 0.4, 0.9, 1.3]), np.array([0.1, 0.7, 2.0])
     K, d = mdp.kgrid(4), mdp.dgrid(2)
     out = []
-    for big in ("0", "1"):
+    for big, rowk in (("0", "0"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("MDP_SCN_BIG", big)
+        monkeypatch.setenv("MDP_SCN_ROW", rowk)
         with mdp.Scenario(row, kind, m=400, d=100) as sc:
             out.append(sc.lik(e, c, K, d, ts=6, tdis=4))
     close(out[1], out[0], rtol=1e-12)
+    close(out[2], out[0], rtol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["dieoff", "loss"])
+@pytest.mark.parametrize("n", [9, 10, 12])
+def test_row_kernel_matches_big_kernel(monkeypatch, kind, n):
+    """For 8 < n <= 12 the default is k_scn_row (one workgroup per point,
+    threads over rows, states in LDS); it runs k_scn_big's contraction and
+    operator order, so the two agree to rounding of the final sum, on a grid
+    with 1 to 33 e values (ts = 0 and tdis = 0 included)."""
+    rng = np.random.default_rng(n)
+    row = rng.choice([-1, 0, 1], size=n, p=[0.2, 0.4, 0.4]).astype(np.int32)
+    for ne, ts, tdis in ((1, 3, 2), (33, 0, 2), (5, 4, 0)):
+        e, c = rng.uniform(0.0, 1.2, ne), np.array([0.15, 0.8])
+        K, d = mdp.kgrid(3, 0.2, 30.0), mdp.dgrid(2)
+        out = []
+        for big in ("0", "1"):
+            monkeypatch.setenv("MDP_SCN_BIG", big)
+            with mdp.Scenario(row, kind, m=400, d=100) as sc:
+                out.append(sc.lik(e, c, K, d, ts=ts, tdis=tdis))
+        close(out[0], out[1], rtol=1e-12)
 
 
 @pytest.mark.parametrize("kind", ["dieoff", "loss"])
