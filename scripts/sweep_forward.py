@@ -38,7 +38,7 @@ args = ap.parse_args()
 torch.cuda.set_device(0)
 tmp = Path(tempfile.mkdtemp())
 KEYS = ("MDP_JIT", "MDP_EPL", "MDP_JIT_WINDOW", "MDP_FWD", "MDP_DIAG", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED",
-        "MDP_JIT_SMEM", "MDP_FUSED_COLS", "MDP_JIT_WPE", "MDP_JIT_HACK")
+        "MDP_JIT_SMEM", "MDP_FUSED_COLS", "MDP_JIT_WPE", "MDP_JIT_HACK", "MDP_JIT_STORE")
 for cfgid in [int(x) for x in args.configs.split(",")]:
     gen, s = (synth.CONFIG2, 512) if cfgid == 2 else (synth.CONFIG3, 1024)
     f = synth.write(tmp / f"c{cfgid}.txt", **gen)
