@@ -76,8 +76,8 @@ def main(argv=None) -> int:
             all_ranks=True)
     else:
         out("------ MIDASPOM, beta version ------\n-> N. Alcala, E. M. Cole, and N. A. Rosenberg <-\n")
-    if a.s < 2:
-        sys.stderr.write("midaspom: -s must be at least 2\n")
+    if a.s < 1:  # the reference indexes g[s - 1] (main_MIDASPOM.c:319): s = 0 is out of bounds there
+        sys.stderr.write("midaspom: -s must be at least 1\n")
         return 1
     g, win = mdp.grid(a.s, a.l, a.u)
     out(f"Parameters for numerical approximation of the posterior density:\n\tWindow size={win:f}, "

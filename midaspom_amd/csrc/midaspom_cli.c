@@ -60,8 +60,8 @@ int main(int argc, char **argv)
             abort();
         }
     }
-    if (nstep < 2) {
-        fprintf(stderr, "midaspom: -s must be at least 2\n");
+    if (nstep < 1) {  /* the reference indexes g[s - 1] (main_MIDASPOM.c:319): s = 0 is out of bounds there */
+        fprintf(stderr, "midaspom: -s must be at least 1\n");
         return 1;
     }
 

@@ -436,6 +436,39 @@ def test_cli_matches_oracle_file(golden, tmp_path):
     assert_posterior_close(np.loadtxt(out), np.loadtxt(ref_out))
 
 
+@pytest.mark.parametrize("fname,flags", [
+    ("occupancies.txt", ["-s", "1"]),            # one point (1, 1): -inf, Ltot -nan
+    ("occupancies.txt", ["-s", "2"]),            # the grid corners only: all -inf
+    ("occupancies.txt", ["-s", "37", "-p", "0.3", "-l", "0.1", "-u", "0.9", "-m", "200", "-d", "50"]),
+    ("occupancies.txt", ["-s", "23", "-l", "0.2", "-u", "1.4"]),  # e, c past 1 (clamped)
+    ("manual_p3_obs.txt", ["-s", "9", "-m", "400", "-d", "200", "-p", "0.7"]),
+    ("config2_64x50.txt", ["-s", "19", "-l", "0.05", "-u", "0.95", "-p", "0.4"]),
+])
+def test_cli_flags_match_oracle_cli(golden, tmp_path, fname, flags):
+    """Every flag of the drop-in (main_MIDASPOM.c:66-139) against the oracle's
+    own CLI (oracle/orc_main.c) with the same command line, including the
+    one- and two-point grids: same 'Total log-likelihood=' line, same file
+    layout and '-nan' cells, posteriors within the parity bar."""
+    out, ref_out = tmp_path / "post.txt", tmp_path / "ref.txt"
+    r = subprocess.run([str(_lib.CLI_PATH), *flags, "-i", str(golden / fname), "-o", str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    orc = subprocess.run([str(oracle.CLI), *flags, "-i", str(golden / fname),
+                          "-o", str(ref_out)], capture_output=True, text=True, timeout=120)
+    assert orc.returncode == 0, orc.stderr
+    total = [ln for ln in r.stdout.splitlines() if ln.startswith("Total log-likelihood=")]
+    assert total == [ln for ln in orc.stdout.splitlines() if ln.startswith("Total log-likelihood=")]
+    got_txt, ref_txt = out.read_text(), ref_out.read_text()
+    assert [ln.count("\t") for ln in got_txt.split("\n")] == [ln.count("\t") for ln in ref_txt.split("\n")]
+    got_cells = [x for x in got_txt.split()]
+    ref_cells = [x for x in ref_txt.split()]
+    assert [x == "-nan" for x in got_cells] == [x == "-nan" for x in ref_cells]
+    s = int(flags[1])
+    got = np.array([float(x) for x in got_cells]).reshape(s, s)
+    ref = np.array([float(x) for x in ref_cells]).reshape(s, s)
+    assert_posterior_close(got, ref)
+
+
 def test_cli_all_nan_file(tmp_path):
     inp = tmp_path / "q5.txt"
     inp.write_text("0 1 1 1\n0 0 0 0\n0 1 0 1\n")
