@@ -2116,6 +2116,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (const char *cv = getenv("MDP_JIT_SLOTS")) plan.slots = atoi(cv);
             if (const char *wv = getenv("MDP_JIT_WPE")) plan.wpe = atoi(wv);
             if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
+            if (const char *fv2 = getenv("MDP_JIT_EFAST")) plan.efast = atoi(fv2) != 0;
             if (const char *ev = getenv("MDP_EPL")) plan.epl = atoi(ev);
             if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
             // compile the variant a small grid uses now (the other on demand)

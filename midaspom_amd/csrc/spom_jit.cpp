@@ -150,7 +150,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          // FC columns per workgroup (fused variant): KBLOCK threads each
          "    const u32 half = threadIdx.x / KBLOCK, tid = threadIdx.x % KBLOCK;\n"
          // (column group, e block): FC columns x KBLOCK*EPL e values per workgroup
-         "    const u32 ncb = (nc + FC - 1) / FC, ic0 = lb % ncb * FC, by = lb / ncb;\n"
+      << (pl.efast ? "    const u32 gy = (ne + KBLOCK * EPL - 1) / (KBLOCK * EPL), ic0 = lb / gy * FC, by = lb % gy;\n"
+                   : "    const u32 ncb = (nc + FC - 1) / FC, ic0 = lb % ncb * FC, by = lb / ncb;\n") <<
          "    const u32 ic = ic0 + half;\n"
          "    const double *Qh = Ql + half * LDQ;\n"
          // this lane's e values: issued first, their latency hides under the prologue

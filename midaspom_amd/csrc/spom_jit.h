@@ -27,6 +27,7 @@ struct MdpJitPlan {
     int window = 8;               // transitions per scheduling region
     bool diag = false;            // record s_memtime phase stamps (MDP_DIAG)
     bool xcd = true;              // XCD-aware block order
+    bool efast = true;            // e blocks of one column group dispatched back to back (same XCD)
     int slots = 8;                // registers caching transitions that recur (0: none)
     int wpe = 0;                  // minimum waves per SIMD asked of the compiler (0: its default)
     double flops_pt = 0;          // out: FP64 flops per grid point of the generated code
