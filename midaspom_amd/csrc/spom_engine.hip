@@ -327,12 +327,18 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     uint32_t kmax, const double *__restrict__ zsT, const double *__restrict__ zc, const double *__restrict__ sv,
     uint32_t nitems, const uint2 *__restrict__ items, uint32_t ncoef, const uint32_t *__restrict__ qstart,
     uint32_t nqi, const uint32_t *__restrict__ qitem, double *__restrict__ Q, uint32_t ldQ,
-    unsigned long long *__restrict__ stamps)
+    unsigned long long *__restrict__ stamps, uint32_t xcd)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     MDP_RSTAMP(stamps, 6);
     MDP_STAMP(stamps, 0);
-    const uint32_t c0 = blockIdx.x * CB, ncb = min((uint32_t)CB, nc - c0);
+    // XCD-aware: workgroups are dealt round-robin over the 8 XCDs, so XCD x
+    // takes a contiguous eighth of the c range -- the columns the forward
+    // kernel's XCD-aware order gives XCD x -- and the forward reads these Q
+    // rows from its own L2
+    const uint32_t nb = gridDim.x, full = nb & ~7u;
+    const uint32_t lb = xcd && blockIdx.x < full ? (blockIdx.x & 7u) * (full >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const uint32_t c0 = lb * CB, ncb = min((uint32_t)CB, nc - c0);
     double *Zl = lds;                                  // [nrows][CB]
     // per row, c and var column the pressure min(1, c S[j][b]): rows padded
     // by one double2 so rows read by one wave fall on different banks
@@ -1150,6 +1156,7 @@ struct mdp_engine {
     bool diag = false;        // MDP_DIAG: record phase stamps
     bool jit = false;         // forward kernel specialised with hipRTC (spom_jit.cpp)
     bool wide = false;        // wide path (k_witems + k_wq + k_fwd_wide): npmax > 16 or MDP_WIDE=1
+    bool qrows_xcd = true;    // k_qrows deals c ranges XCD-aware (MDP_QROWS_XCD=0: blockIdx order)
     double wide_flops_pt = 0; // its FP64 flops per grid point
     int jit_epl = 1;          // its grid points per lane
     double jit_flops_pt = 0;  // its FP64 flops per grid point (counted by the generator)
@@ -1941,7 +1948,8 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
 #define MDP_QROWS_CB(NV, EX, CB)                                                                        \
     MDP_LAUNCH((k_qrows<NV, EX, CB>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, eng->nvar, eng->nj,         \
                d.zs_kmax, d.zs, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
-               (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1])
+               (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1],                 \
+               (uint32_t)(eng->qrows_xcd ? 1u : 0u))
         // c values per workgroup: <= qrows_maxcb(nvar) (register budget at 1024 threads)
         if (eng->nvar == 8) {
             if (cb == 4) MDP_QROWS_CB(8, true, 4);
@@ -2117,6 +2125,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (const char *wv = getenv("MDP_JIT_WPE")) plan.wpe = atoi(wv);
             if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
             if (const char *fv2 = getenv("MDP_JIT_EFAST")) plan.efast = atoi(fv2) != 0;
+            if (const char *qx = getenv("MDP_QROWS_XCD")) eng->qrows_xcd = atoi(qx) != 0;
             if (const char *ev = getenv("MDP_EPL")) plan.epl = atoi(ev);
             if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
             // compile the variant a small grid uses now (the other on demand)
