@@ -48,6 +48,18 @@ CONFIGS = {
 }
 
 
+def _pmc_traffic(cfg):
+    """HBM bytes per launch of the config's dominant kernel from the committed
+    rocprofv3 PMC passes (scripts/gpu_measure.sh, scripts/pmc_traffic.py):
+    FETCH_SIZE x2 + WRITE_SIZE; null when no profile of this config exists."""
+    tf = ROOT / "profiles" / f"pmc_traffic_cfg{cfg}.json"
+    if not tf.exists():
+        return {"traffic": None}
+    return {"traffic": json.loads(tf.read_text())["hbm_bytes_per_launch"],
+            "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": str(tf.relative_to(ROOT))}
+
+
 def host_info():
     """nproc, the cores this process may use, and the CPU model."""
     model = "unknown"
@@ -235,7 +247,7 @@ def bench_future(args, world, rank, dev):
         "roofline": {"kernel": "k_future", "bound": "valu-issue",
                      "compute_unit": "VALU issue cycles (Philox integer work), instructions priced by class",
                      "achieved": achieved, "peak": issue_peak, "unit": "G SIMD issue cycles/s",
-                     "frac": achieved / issue_peak if achieved else None, "traffic": None,
+                     "frac": achieved / issue_peak if achieved else None, **_pmc_traffic(5),
                      "valu_source": valu_src,
                      "valu_insts_rate": insts, "valu_insts_peak": valu_issue_peak,
                      "valu_insts_frac": insts / valu_issue_peak if insts else None,
@@ -338,7 +350,7 @@ def bench_dieoff(args, world, rank, dev):
         "kernel_ms": kms,
         "roofline": {"kernel": "k_scn_lik", "bound": "fp64-valu", "compute_unit": "FP64 VALU",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "flop_per_point_year": flop_year},
+                     "frac": achieved / FP64_PEAK_TFLOPS, **_pmc_traffic(4), "flop_per_point_year": flop_year},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

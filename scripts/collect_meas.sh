@@ -10,5 +10,5 @@ for c in 2 3 4 5; do
   cp $M/prof_bench_cfg$c.json $D/bench_cfg$c.json
   cp $M/prof_cfg$c/run_kernel_stats.csv $D/rocprof_kernel_stats_cfg$c.csv
 done
-cp $M/pmc_summary_cfg2.txt $M/pmc_summary_cfg3.txt $M/pmc_traffic_cfg2.json $M/pmc_traffic_cfg3.json $M/pmc_valu_cfg5.json $D/
-cp $M/pmc_traffic_cfg2.json $M/pmc_traffic_cfg3.json $M/pmc_valu_cfg5.json profiles/
+cp $M/pmc_summary_cfg2.txt $M/pmc_summary_cfg3.txt $M/pmc_traffic_cfg*.json $M/pmc_valu_cfg5.json $D/
+cp $M/pmc_traffic_cfg*.json $M/pmc_valu_cfg5.json profiles/

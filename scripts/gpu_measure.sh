@@ -26,6 +26,15 @@ for CFG in 2 3; do
   python3 $R/scripts/pmc_summary.py $O/pmc/c${CFG}p1 $O/pmc/c${CFG}p2 > $O/pmc_summary_cfg$CFG.txt || exit 1
   echo "pmc cfg$CFG ok"
 done
+for spec in "4:k_scn<" "5:k_future<"; do
+  CFG=${spec%%:*}; KN=${spec#*:}
+  for p in 7:FETCH_SIZE 8:WRITE_SIZE; do
+    i=${p%%:*}; C=${p#*:}
+    timeout -k 10 200 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $O/pmc/c${CFG}p$i -o run -- python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 2 --warmup 1 > $O/pmc/c${CFG}p$i.json 2> $O/pmc/c${CFG}p$i.err || { echo "pmc $CFG $C failed"; tail $O/pmc/c${CFG}p$i.err; exit 1; }
+  done
+  python3 $R/scripts/pmc_traffic.py $O/pmc $CFG $O/pmc_traffic_cfg$CFG.json "$KN" || exit 1
+  echo "pmc traffic cfg$CFG ok"
+done
 timeout -k 10 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_CVT --kernel-trace --output-format csv -d $O/pmc/c5p1 -o run -- python3 $R/bench.py --config 5 --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc/c5p1.json 2> $O/pmc/c5p1.err || { echo "pmc 5 failed"; exit 1; }
 python3 $R/scripts/pmc_valu.py $O/pmc/c5p1 1000000 50 $O/pmc_valu_cfg5.json || exit 1
 echo "all ok"
