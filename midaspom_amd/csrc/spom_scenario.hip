@@ -161,6 +161,23 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
     const double c = cv[ic], K = a.mode ? Kv[iK] : 1.0;
     const double *src = a.mode && a.loss ? srcv + (size_t)id * N : nullptr;
     const double Kpc = a.mode && !a.loss ? K : 1.0;
+    // initial states: every load of the thread issued first (unconditionally,
+    // to a valid address), so their global round trip overlaps the table
+    // build; stored to y after it
+    constexpr int kIS = (NS * kE + kScnBlock - 1) / kScnBlock;
+    double t0[kIS];
+#pragma unroll
+    for (int u = 0; u < kIS; ++u) {
+        const uint32_t i = tid + u * kScnBlock, x = (i / kE) % NS, le = i % kE;
+        const uint32_t st = ((x % NHI) << NL) | (x / NHI);
+        const bool ok = !a.mode || e0 + le < a.ne;
+        const size_t idx = a.mode ? ((size_t)ic * NS + st) * a.ne + e0 + le : st;
+        const double v = y0src[ok ? idx : 0];
+        t0[u] = ok ? v : 0.0;
+    }
+    // hi-row offsets of the factor table, for the flat build below
+    __shared__ uint32_t boffs[NHI];
+    if (tid < (uint32_t)NHI) boffs[tid] = boff[tid];
     // pC for every (j, k), k not in j: dieoff.c:78 (c S) K, loss.c:98 c (S + src Ks)
     {  // every S (and source) load of the thread in flight before the first store
         constexpr int kPC = (NS * N + kScnBlock - 1) / kScnBlock;
@@ -207,42 +224,34 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
         }
         At[i] = r;
     }
-    // hi factors B_j(bh): patches 0..NH-1, ascending; [jh][rank of bh][jl]
-    for (uint32_t jh = 0; jh < (uint32_t)NHI; ++jh) {
-        const uint32_t fr = ~jh & (NHI - 1), cnt = (1u << __popc(fr)) * NLO;
-        double *dst = Bt + boff[jh];
-        for (uint32_t i = tid; i < cnt; i += kScnBlock) {
-            const uint32_t r = i / NLO, jl = i % NLO, bh = jh | deposit(r, fr), j = (jh << NL) | jl;
-            double v = 1.0;
-            for (int k = 0; k < NH; ++k) {
-                const uint32_t bit = 1u << (NH - 1 - k);
-                if (jh & bit) continue;
-                const double p = pc[j * N + k];
-                v *= (bh & bit) ? p : 1.0 - p;
-            }
-            dst[i] = v;
+    // hi factors B_j(bh): patches 0..NH-1, ascending; [jh][rank of bh][jl].
+    // One flat pass over the table (entry t belongs to the last hi row jh
+    // with boff[jh] <= t: a binary search over the staged offsets).  The
+    // earlier loop over the 2^NH hi rows (a global offset load and a short
+    // partial pass each) plus the initial-state round trip after it made the
+    // per-workgroup fixed cost 32 ms of config 4's 241 ms; now 10.6 ms
+    for (uint32_t t = tid; t < a.btot; t += kScnBlock) {
+        uint32_t jh = 0;
+#pragma unroll
+        for (uint32_t st = NHI / 2; st > 0; st >>= 1)
+            if (boffs[jh + st] <= t) jh += st;
+        const uint32_t i = t - boffs[jh], fr = ~jh & (NHI - 1);
+        const uint32_t r = i / NLO, jl = i % NLO, bh = jh | deposit(r, fr), j = (jh << NL) | jl;
+        double v = 1.0;
+        for (int k = 0; k < NH; ++k) {
+            const uint32_t bit = 1u << (NH - 1 - k);
+            if (jh & bit) continue;
+            const double p = pc[j * N + k];
+            v *= (bh & bit) ? p : 1.0 - p;
         }
+        Bt[t] = v;
     }
     if (tid < (uint32_t)NLO) Bt[a.btot + tid] = 0.0;  // zero block (upper half, no free hi bit)
-    // initial states: every load of the thread issued (unconditionally, to
-    // a valid address) before the first LDS store, one global round trip
-    {
-        constexpr int kIS = (NS * kE + kScnBlock - 1) / kScnBlock;
-        double t0[kIS];
+    // initial states: stored into y once the tables are built (loaded first)
 #pragma unroll
-        for (int u = 0; u < kIS; ++u) {
-            const uint32_t i = tid + u * kScnBlock, x = (i / kE) % NS, le = i % kE;
-            const uint32_t st = ((x % NHI) << NL) | (x / NHI);
-            const bool ok = !a.mode || e0 + le < a.ne;
-            const size_t idx = a.mode ? ((size_t)ic * NS + st) * a.ne + e0 + le : st;
-            const double v = y0src[ok ? idx : 0];
-            t0[u] = ok ? v : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < kIS; ++u) {
-            const uint32_t i = tid + u * kScnBlock, x = i / kE, le = i % kE;
-            if (i < (uint32_t)(NS * kE)) y[(x / NHI) * LS + (x % NHI) * kE + le] = t0[u];
-        }
+    for (int u = 0; u < kIS; ++u) {
+        const uint32_t i = tid + u * kScnBlock, x = i / kE, le = i % kE;
+        if (i < (uint32_t)(NS * kE)) y[(x / NHI) * LS + (x % NHI) * kE + le] = t0[u];
     }
     __syncthreads();
     const uint32_t w = tid / 64, g = (tid >> 5) & 1u, le = tid & 31u;
