@@ -14,6 +14,12 @@ import numpy as np
 # The BASELINE.json workloads as concrete inputs.
 CONFIG2 = dict(n=64, T=50, nvar=8, e=0.3, c=0.1, m=400, d=100, pmiss=0.05, seed=1)
 CONFIG3 = dict(n=256, T=200, nvar=8, e=0.1, c=0.05, m=400, d=100, pmiss=0.03, seed=2)
+# SURVEY.md §8(c) "Q1 reproducer": the config-2 generator with the variable
+# block in the middle (columns 28-35), so always-zero columns lie right of the
+# last variable column -- the input on which the serial reference mis-numbers
+# its states (quirk Q1, main_MIDASPOM.c:244) and the MPI build reports
+# Ltot -153.68039 at -s 17 (main_MIDASPOM_MPI.c:262).
+Q1_MID = dict(CONFIG2, v0=28)
 MD5 = {
     "config2": "6bd6f4bf7e69d794078d9c5718cda157",
     "config3": "5cf6ad09063e720a952fcd4c32b47030",
@@ -21,10 +27,13 @@ MD5 = {
 
 
 def generate(n: int, T: int, nvar: int, e: float, c: float, m: float, d: float,
-             pmiss: float, seed: int) -> str:
-    """Return the occupancy file text (space-separated ints, '\\n' per year)."""
+             pmiss: float, seed: int, v0: int | None = None) -> str:
+    """Return the occupancy file text (space-separated ints, '\\n' per year).
+    ``v0`` moves the variable block to columns [v0, v0 + nvar) (default: the
+    rightmost block of Appendix C)."""
     rng = np.random.default_rng(seed)
-    var = np.arange(n - nvar, n)
+    v0 = n - nvar if v0 is None else v0
+    var = np.arange(v0, v0 + nvar)
     idx = np.arange(n)
     disp = np.exp(-np.abs(idx[:, None] - idx[None, :]) * d / m)
     np.fill_diagonal(disp, 0)

@@ -13,6 +13,9 @@ Provenance of every fixture (all are DATA -- inputs and expected outputs):
                            and loss (p.5) tables for the next rows of §8(f).
   config2_64x50.txt        synth.generate(**synth.CONFIG2)  (md5 6bd6f4bf...)
   config3_256x200.txt      synth.generate(**synth.CONFIG3)  (md5 5cf6ad09...)
+  q1_64x50_mid.txt         synth.generate(**synth.Q1_MID): config 2 with the
+                           variable block at columns 28-35, the SURVEY §8(c)
+                           Q1 reproducer (its MPI-build Ltot is in anchors.json)
 """
 import hashlib
 import shutil
@@ -44,6 +47,7 @@ def main():
     (HERE / "manual_p3_posterior.txt").write_text(MANUAL_P3_POST)
     synth.write(HERE / "config2_64x50.txt", **synth.CONFIG2)
     synth.write(HERE / "config3_256x200.txt", **synth.CONFIG3)
+    synth.write(HERE / "q1_64x50_mid.txt", **synth.Q1_MID)
     assert md5(HERE / "config2_64x50.txt") == synth.MD5["config2"]
     assert md5(HERE / "config3_256x200.txt") == synth.MD5["config3"]
     assert md5(HERE / "occupancies.txt") == "d5306e9bbb6c873b4e38510f70a452c6"

@@ -71,6 +71,8 @@ CASES = [
     ("config3_256x200.txt", dict(m=400, d=100, s=9)),
     ("config3_256x200.txt", dict(m=400, d=100, s=17)),
     ("config3_256x200.txt", dict(m=400, d=100, s=5)),  # Q4: all underflow -> -nan
+    ("q1_64x50_mid.txt", dict(m=400, d=100, s=17)),    # Q1: variable block mid-row
+    ("q1_64x50_mid.txt", dict(m=400, d=100, s=64)),
 ]
 
 
@@ -97,7 +99,7 @@ def test_anchor_ltot_values(golden, anchors):
     """Total log-likelihood lines equal the reference's."""
     from conftest import run_by_name
     for name in ["manual_p3", "default_example_s101", "config1_s50", "config2_s17",
-                 "config2_s17_p03", "config3_s9", "config3_s17", "config3_s32"]:
+                 "config2_s17_p03", "config3_s9", "config3_s17", "config3_s32", "q1_mid_block_s17"]:
         r = run_by_name(anchors, name)
         f = r["flags"]
         lik, lt = mdp.run_file(golden / r["input"], m=f["m"], p=f.get("p", 0.5), d=f["d"], s=f["s"])

@@ -23,7 +23,7 @@ def _same_model(pm: mdp.Model, om: oracle.OracleModel):
 
 
 @pytest.mark.parametrize("fname", ["occupancies.txt", "manual_p3_obs.txt", "config2_64x50.txt",
-                                   "config3_256x200.txt"])
+                                   "config3_256x200.txt", "q1_64x50_mid.txt"])
 @pytest.mark.parametrize("p", [0.5, 0.3])
 def test_model_matches_oracle_files(golden, fname, p):
     pm = mdp.Model.load(golden / fname, m=400, p=p, d=100)

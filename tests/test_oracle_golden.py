@@ -74,6 +74,22 @@ def test_config2_posterior_md5(golden, anchors, tmp_path):
     assert md5(out) == r["md5"]["openblas"]
 
 
+def test_q1_mid_block_mpi_ltot(golden, anchors, tmp_path):
+    """Quirk Q1: with always-zero columns right of the last
+    variable column the serial reference mis-numbers its states and aborts;
+    the MPI build numbers them correctly (main_MIDASPOM_MPI.c:262) and reports
+    Ltot -153.68039 at -s 17.  The oracle follows the MPI semantics and is
+    pinned to that value here (the fixture is the config-2 generator with
+    the block at columns 28-35, synth.Q1_MID)."""
+    assert hashlib.md5(synth.generate(**synth.Q1_MID).encode()).hexdigest() == \
+        anchors["inputs_md5"]["q1_64x50_mid.txt"]
+    r, lik, lt, out = _run(golden, anchors, tmp_path, "q1_mid_block_s17")
+    assert f"{lt:.5f}" == r["ltot"]
+    m = oracle.OracleModel.load(golden / r["input"])
+    # the always-zero columns 36-63 lie right of the variable block
+    assert m.nvar == 8 and m.n == 64
+
+
 def test_q3_prior_semantics(golden, anchors, tmp_path):
     r, lik, lt, out = _run(golden, anchors, tmp_path, "config2_s17_p03")
     assert f"{lt:.5f}" == r["ltot"]
