@@ -512,7 +512,14 @@ def main():
     info = eng.info()
     fwd_ms = kms.get("k_forward", float("nan"))
     fused = "k_qrows" not in kms  # the fused forward kernel does the per-c work too
-    flop_fwd = fact["flop"] if fused else s * s * (fact["weight_pt"] + fact["use_pt"] + fact["final_pt"])
+    # numerator: the algorithmic minimum (mdp_engine_work_fact flop_min): each
+    # distinct transition's dot product once per point, every use's state
+    # update, the weight table, the prior sum (+ the per-c tables when the
+    # fused kernel forms them); a transition that recurs is algorithmic
+    # reuse, not work (the every-use count is reported beside it)
+    per_pt_min = fact["weight_pt"] + fact["use_pt_min"] + fact["final_pt"]
+    flop_fwd = fact["flop_min"] if fused else s * s * per_pt_min
+    flop_every = fact["flop"] if fused else s * s * (fact["weight_pt"] + fact["use_pt"] + fact["final_pt"])
     achieved_tf = flop_fwd / (fwd_ms * 1e-3) / 1e12
     result = {
         "metric": "grid-point x timestep likelihood evals/sec",
@@ -549,8 +556,10 @@ def main():
             # closed-form factorised count from the plan's dimensions
             # (mdp_engine_work_fact): the kernel's share of it
             "flop_per_launch": flop_fwd,
-            "flop_basis": "closed-form factorised count, " + ("per-c + per-point terms (fused kernel)" if fused
-                                                              else "per-point terms (k_qrows does the per-c work)"),
+            "flop_basis": "closed-form factorised minimum, each distinct transition once per point, "
+                          + ("per-c + per-point terms (fused kernel)" if fused
+                             else "per-point terms (k_qrows does the per-c work)"),
+            "flop_per_launch_every_use": flop_every,
             "work_fact": fact,
             "step_tflops_fact": fact["flop"] / (dt / args.steps) / 1e12,
             # the hipRTC generator's count of the code it emitted (transition caching included)

@@ -36,7 +36,7 @@ extern "C" {
 #define MDP_ENODEV (-5)       /* no usable GPU                             */
 #define MDP_EUNSUPPORTED (-6) /* problem outside the engine's limits       */
 
-#define MDP_ABI_VERSION 4
+#define MDP_ABI_VERSION 5
 
 /* ------------------------------------------------------------------ */
 /* Host model: parse + state enumeration (the reference's L2 layer)    */
@@ -166,14 +166,19 @@ int mdp_engine_work(const mdp_engine *engine, uint64_t ne, uint64_t nc, double *
  * multiply per free column), Q sums (len - 1 adds per entry).  Per grid
  * point: the weight table (2 maxA powers + one product per W[|A|][m] entry
  * used), every forward use (2 nX + 3: the (nX+1)-term dot product and the
- * state multiply-add), the prior sum (2 np_last - 1).  Transitions that
- * recur are counted at every use (the hipRTC kernel caches some: it executes
- * less).  flop = nc * per-c + ne * nc * per-point.  The per-c terms are zero
- * on the generic path (MDP_JIT=0), which has no direct plan. */
+ * state multiply-add), the prior sum (2 np_last - 1).  use_pt counts a
+ * transition that recurs at every use; use_pt_min is the algorithmic
+ * minimum: each distinct transition's dot product once per point (2 nX + 1)
+ * plus every use's state update (2) -- the hipRTC kernel caches recurring
+ * transitions and executes between the two.  flop = nc * per-c + ne * nc *
+ * per-point, flop_min the same with use_pt_min.  The per-c terms are zero on
+ * the generic path (MDP_JIT=0), which has no direct plan. */
 typedef struct mdp_work {
     double z_c, pc_c, item_c, q_c;        /* per c value */
     double weight_pt, use_pt, final_pt;   /* per grid point */
     double flop;                          /* the grid's total */
+    double use_pt_min;                    /* per grid point, distinct transitions once */
+    double flop_min;                      /* the grid's total with use_pt_min */
 } mdp_work;
 int mdp_engine_work_fact(const mdp_engine *engine, uint64_t ne, uint64_t nc, mdp_work *work);
 
@@ -189,6 +194,12 @@ typedef struct mdp_engine_info {
     uint32_t variant;
 } mdp_engine_info;
 int mdp_engine_get_info(const mdp_engine *engine, mdp_engine_info *info);
+
+/* The kernel instantiations this engine has launched so far, space-separated
+ * and sorted (e.g. "k_qrows<16,0,2> mdp_fwd_jit<reading,maxA12>"): which
+ * template of each hot-path kernel ran, for tests and profiles.  Writes at
+ * most len bytes (NUL-terminated) and returns the full length. */
+int mdp_engine_launched(const mdp_engine *engine, char *buf, size_t len);
 
 /* ------------------------------------------------------------------ */
 /* Scenario likelihoods: in-situ die-off and habitat loss              */
@@ -257,10 +268,11 @@ int mdp_future_simulate(mdp_future *future, uint64_t seed, uint64_t rep0, uint64
 /* Same into caller-owned device memory d_counts[tfut] (overwritten, not
  * accumulated) on `stream` (NULL = HIP's null stream); asynchronous.  A
  * replicate whose posterior draw needs more look-back than the engine holds
- * raises a device error flag (cleared by each call in stream order);
- * mdp_future_check waits for `stream` and returns MDP_EUNSUPPORTED when it
- * is set -- the counts of those launches are then not valid (the host form
- * mdp_future_simulate does this check itself). */
+ * raises a sticky device error flag; mdp_future_check waits for `stream`,
+ * reads and clears the flag, and returns MDP_EUNSUPPORTED when it was set --
+ * the counts of some launch since the previous check are then not valid, so
+ * one check after several launches covers all of them (the host form
+ * mdp_future_simulate checks its own launch with a separate flag). */
 int mdp_future_simulate_device(mdp_future *future, uint64_t seed, uint64_t rep0, uint64_t nrep, uint32_t tfut,
                                uint64_t *d_counts, void *stream);
 int mdp_future_check(mdp_future *future, void *stream);

@@ -207,6 +207,13 @@ class Engine:
         check(lib().mdp_engine_get_info(self._h, ctypes.byref(inf)))
         return {f: getattr(inf, f) for f, _ in inf._fields_}
 
+    def launched(self) -> set:
+        """The kernel instantiations this engine has launched (e.g.
+        {"k_qrows<16,0,2>", "mdp_fwd_jit<reading,maxA12>"})."""
+        buf = ctypes.create_string_buffer(4096)
+        check(lib().mdp_engine_launched(self._h, buf, len(buf)))
+        return set(buf.value.decode().split())
+
     def work(self, ne: int, nc: int) -> dict:
         a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         check(lib().mdp_engine_work(self._h, ne, nc, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
@@ -445,8 +452,8 @@ class Future:
                                                ctypes.c_void_p(stream)))
 
     def check(self, stream: int = 0) -> None:
-        """Wait for ``stream``; raise if a device launch since the last
-        simulate_device on it overflowed the posterior look-back."""
+        """Wait for ``stream``; raise if any device launch since the previous
+        check overflowed the posterior look-back (the flag is cleared here)."""
         check(lib().mdp_future_check(self._h, ctypes.c_void_p(stream)))
 
     def time_kernel(self, nrep: int, tfut: int, seed: int = 0, reps: int = 10) -> float:

@@ -65,7 +65,8 @@ class Work(ctypes.Structure):
     """Mirror of ``mdp_work`` (closed-form factorised FP64 work)."""
 
     _fields_ = [(f, ctypes.c_double) for f in
-                ("z_c", "pc_c", "item_c", "q_c", "weight_pt", "use_pt", "final_pt", "flop")]
+                ("z_c", "pc_c", "item_c", "q_c", "weight_pt", "use_pt", "final_pt", "flop", "use_pt_min",
+                 "flop_min")]
 
 
 class EngineInfo(ctypes.Structure):
@@ -107,6 +108,7 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_dbl_p, c_dbl_p, c_dbl_p]),
     ("mdp_engine_work_fact", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(Work)]),
     ("mdp_engine_get_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(EngineInfo)]),
+    ("mdp_engine_launched", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
     ("mdp_engine_diag_report", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
     ("mdp_last_error", ctypes.c_char_p, []),
     ("mdp_abi_version", ctypes.c_int, []),

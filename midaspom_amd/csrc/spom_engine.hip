@@ -32,11 +32,13 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <new>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -422,12 +424,15 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         zz *= zseries(zq, c);
         Zl[w] = zz;
         // the row's pressures for this c: min(1, c S) (the columns of j, where
-        // sv holds -1, and padded slots get a factor of exactly 1.0 from
-        // (s, n) = (0, 1) in phase 2 whatever is stored here)
+        // sv holds -1, and padded slots select a factor of exactly 1.0 in
+        // phase 2 whatever is stored here)
         double pr[NV];
 #pragma unroll
-        for (int b = 0; b < NV; ++b)
-            pr[b] = (EXACT || (uint32_t)b < nvar) ? fmin(1.0, c * sv[(size_t)r * nvar + b]) : 0.0;
+        for (int b = 0; b < NV; ++b) {
+            // min(1, c S) as the reference clamps it (:355-357): NaN stays NaN
+            const double t = (EXACT || (uint32_t)b < nvar) ? c * sv[(size_t)r * nvar + b] : 0.0;
+            pr[b] = t > 1.0 ? 1.0 : t;
+        }
         double2 *pd = (double2 *)(Prl + (size_t)r * PRS + cl * NV);
 #pragma unroll
         for (int b = 0; b < NV / 2; ++b) pd[b] = make_double2(pr[2 * b], pr[2 * b + 1]);
@@ -442,18 +447,20 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     for (uint32_t it = threadIdx.x; it < nitems; it += kQrowsBlock) {
         const uint2 t = It[it];
         const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), nB = ~t.x, J = t.y & 0xffffffu;
-        // per slot (s_b, n_b): (1, 0) where B_b, (-1, 1) where not, (0, 1) for
-        // the columns of j and the padded slots -- so f_b = fma(s_b, min(1,
-        // c S), n_b) is p, 1 - p or exactly 1.0 with no selects; the values
-        // (hence the bits) are the fused kernel's
+        // per slot (s_b, n_b): (1, 0) where B_b, (-1, 1) where not, so f_b =
+        // fma(s_b, min(1, c S), n_b) is p or 1 - p; the columns of j and the
+        // padded slots select exactly 1.0 (a product 0 * p would turn an
+        // infinite pressure into NaN) -- the values (hence the bits) are the
+        // fused kernel's
         double sg[NV], nb[NV];
+        bool onef[NV];
 #pragma unroll
         for (int b = 0; b < NV; ++b) {
             const uint32_t bit = EXACT ? (uint32_t)(NV - 1 - b) : nvar - 1 - (uint32_t)b;  // wraps past nvar
-            const bool one = (!EXACT && (uint32_t)b >= nvar) || ((J >> bit) & 1u);
-            const uint32_t nbit = one ? 0u : (nB >> bit) & 1u;
-            sg[b] = one ? 0.0 : __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
-            nb[b] = one ? 1.0 : __hiloint2double((int)(nbit * 0x3ff00000u), 0);
+            onef[b] = (!EXACT && (uint32_t)b >= nvar) || ((J >> bit) & 1u);
+            const uint32_t nbit = (nB >> bit) & 1u;
+            sg[b] = __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
+            nb[b] = __hiloint2double((int)(nbit * 0x3ff00000u), 0);
         }
         double zr[CB], pc[CB];
 #pragma unroll
@@ -465,8 +472,8 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
 #pragma unroll
             for (int b = 0; b < NV / 2; ++b) {
                 const double2 p2 = ps[b];
-                f[2 * b] = fma(sg[2 * b], p2.x, nb[2 * b]);
-                f[2 * b + 1] = fma(sg[2 * b + 1], p2.y, nb[2 * b + 1]);
+                f[2 * b] = onef[2 * b] ? 1.0 : fma(sg[2 * b], p2.x, nb[2 * b]);
+                f[2 * b + 1] = onef[2 * b + 1] ? 1.0 : fma(sg[2 * b + 1], p2.y, nb[2 * b + 1]);
             }
 #pragma unroll
             for (int sh = 1; sh < NV; sh *= 2)
@@ -1096,7 +1103,7 @@ int dev_reserve(T **p, size_t *cap, size_t count)
 constexpr int kNumEv = 6;  // start/stop per kernel: k_zpv, k_coefs, k_forward
 const char *const kKernelNames[3][3] = {{"k_zpv", "k_coefs", "k_forward"},
                                         {"k_zrows", "k_qrows", "k_forward"},
-                                        {"k_zrows", "k_wq", "k_forward"}};
+                                        {"k_zrows", "k_witems+k_wq", "k_fwd_wide"}};
 
 struct DevCtx {
     int device = 0;
@@ -1177,6 +1184,7 @@ struct mdp_engine {
     double prior0 = 1.0;
     std::vector<uint32_t> np, pairA, pairB, pairOff, use_pair, prog, udesc, pairPart0, partP, partK0;
     std::vector<DevCtx> devs;
+    mutable std::set<std::string> launched;  // kernel instantiations launched so far (mdp_engine_launched)
     int profiling = 0;
     double last_ms[3] = {0, 0, 0};  // mean per run over the last collected runs
     int nlast = 0;
@@ -1184,6 +1192,18 @@ struct mdp_engine {
 };
 
 namespace {
+
+// record a launched kernel instantiation ("k_qrows<16,0,2>", ...)
+void note_launch(const mdp_engine *eng, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+void note_launch(const mdp_engine *eng, const char *fmt, ...)
+{
+    char b[96];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(b, sizeof b, fmt, ap);
+    va_end(ap);
+    eng->launched.emplace(b);
+}
 
 constexpr int kDegBuckets[] = {4, 8, 16, 24};
 
@@ -1725,6 +1745,13 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
             (rc = dev_reserve(&d.Zg, &d.cap_zg, (size_t)nc * eng->nj + 1)))
             return rc;
         if (!(d.zs_cmax == cmax) && (rc = upload_qrows_tables(eng, d, cmax))) return rc;
+        // k_zrows stages kZRows rows of explicit columns in dynamic LDS
+        const size_t zl = (size_t)kZRows * d.zs_kmax * sizeof(double);
+        if (zl > kQrowsLdsMax)
+            return mdp_set_error(MDP_EUNSUPPORTED, "%u explicit colonisation columns per row exceed the LDS of k_zrows",
+                                 d.zs_kmax);
+        if (zl > 64 * 1024)
+            HIP_TRY(hipFuncSetAttribute((const void *)k_zrows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)zl));
         // c values per launch: item factors within kWidePgBytes, the two state
         // vectors of every point of a launch within kWideVBytes
         const size_t ne_pad = (size_t)std::max<uint32_t>(1u, (ne + kBlock - 1) / kBlock) * kBlock;
@@ -1785,6 +1812,7 @@ void launch_fwd_epl(const mdp_engine *eng, const DevCtx &d, double *out, uint32_
 {
     dim3 grid(d.nc, (d.ne + kBlock * EPL - 1) / (kBlock * EPL));
     const uint32_t nprog = (uint32_t)eng->prog.size() - 1;
+    note_launch(eng, "%s<%d,%d,%d>", eng->fwd_lds ? "k_forward_lds" : "k_forward", NP, DEG, EPL);
     if (eng->fwd_lds)
         MDP_LAUNCH((k_forward_lds<NP, DEG, EPL>), grid, dim3(kBlock), eng->fwd_lds_bytes, s,
                            d.R, ldR_of(eng), d.prog, nprog, eng->np[0], eng->prior0, d.e, d.ne, out, ld,
@@ -1839,6 +1867,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
         const uint32_t dyn = d.fused ? (d.ct_len + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch
         HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kBlock * fc), 1, 1, kBlock * fc, 1, 1, dyn, s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));
+        note_launch(eng, "mdp_fwd_jit<%s,maxA%u>", d.fused ? "fused" : "reading", eng->maxA);
         return MDP_OK;
     }
     switch (eng->variant / 100) {
@@ -1857,6 +1886,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
 template <bool LDSZ, bool LDSP, int NV>
 void launch_coefs_nv(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
 {
+    note_launch(eng, "k_coefs<%d,%d,%d>", (int)LDSZ, (int)LDSP, NV);
     MDP_LAUNCH((k_coefs<LDSZ, LDSP, NV>), dim3(d.nc), dim3(kBlock), eng->coef_lds, s, d.ZPV,
                        eng->nstates, eng->nvar, d.pairA, d.pairB, d.pairOff, d.pairPart0, eng->npairs,
                        d.partP, d.partK0, (uint32_t)eng->partP.size(), eng->ncoef, d.udesc,
@@ -1895,12 +1925,14 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, uint
             const uint32_t n = std::min(cb, d.nc - c0);
             const dim3 gi((eng->nitems + kBlock - 1) / kBlock, n);
 #define MDP_WITEMS(NV) \
-    hipLaunchKernelGGL((k_witems<NV>), gi, dim3(kBlock), 0, s, d.c, d.nc, c0, eng->nvar, d.Zg, d.sv, eng->nitems, d.items, d.Pg)
+    do { note_launch(eng, "k_witems<%d>", NV); \
+    hipLaunchKernelGGL((k_witems<NV>), gi, dim3(kBlock), 0, s, d.c, d.nc, c0, eng->nvar, d.Zg, d.sv, eng->nitems, d.items, d.Pg); } while (0)
             if (eng->nvar <= 8) MDP_WITEMS(8);
             else if (eng->nvar <= 16) MDP_WITEMS(16);
             else MDP_WITEMS(24);
 #undef MDP_WITEMS
             const dim3 gq((uint32_t)((eng->ldQ + kBlock - 1) / kBlock), n);
+            note_launch(eng, "k_wq");
             hipLaunchKernelGGL(k_wq, gq, dim3(kBlock), 0, s, c0, eng->nitems, d.Pg, eng->ncoef_d, d.qstart, d.qitem,
                                d.Qrow, (uint32_t)eng->ldQ);
         }
@@ -1909,6 +1941,7 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, uint
         for (uint32_t c0 = 0; c0 < d.nc; c0 += cb) {
             const uint32_t n = std::min(cb, d.nc - c0);
             const dim3 g((d.ne + kBlock - 1) / kBlock, n);
+            note_launch(eng, "k_fwd_wide");
             hipLaunchKernelGGL(k_fwd_wide, g, dim3(kBlock), wide_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.udesc_w,
                                d.np_d, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, d.V, eng->npmax, out, ld);
         }
@@ -1936,6 +1969,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
     if ((eng->jit || eng->wide) && k == 0) {  // Z rows
         const uint32_t kmax = d.zs_kmax;
         const dim3 grid((d.nc + 64 * kZC - 1) / (64 * kZC), (eng->nj + kZRows - 1) / kZRows);
+        note_launch(eng, "k_zrows");
         MDP_LAUNCH(k_zrows, grid, dim3(kBlock), (size_t)kZRows * kmax * sizeof(double), s, d.c, d.nc, eng->nj,
                    kmax, d.zs, d.zc, d.Zg);
         HIP_TRY(hipGetLastError());
@@ -1946,10 +1980,12 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
         const dim3 grid((d.nc + cb - 1) / cb);
         const size_t lds = qrows_lds(eng, cb);
 #define MDP_QROWS_CB(NV, EX, CB)                                                                        \
+    do {                                                                                                \
+    note_launch(eng, "k_qrows<%d,%d,%d>", NV, (int)EX, CB);                                              \
     MDP_LAUNCH((k_qrows<NV, EX, CB>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, eng->nvar, eng->nj,         \
                d.zs_kmax, d.zs, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
                (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1],                 \
-               (uint32_t)(eng->qrows_xcd ? 1u : 0u))
+               (uint32_t)(eng->qrows_xcd ? 1u : 0u)); } while (0)
         // c values per workgroup: <= qrows_maxcb(nvar) (register budget at 1024 threads)
         if (eng->nvar == 8) {
             if (cb == 4) MDP_QROWS_CB(8, true, 4);
@@ -1971,6 +2007,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
     }
     if (k == 0) {
         dim3 grid((eng->nstates + kZpvJ - 1) / kZpvJ, (d.nc + kZpvCT - 1) / kZpvCT);
+        note_launch(eng, "k_zpv");
         MDP_LAUNCH(k_zpv, grid, dim3(kBlock), 0, s, d.S, eng->nstates, eng->n - eng->nvar, eng->nvar, d.c,
                    d.nc, d.ZPV, d.stamps[0]);
         HIP_TRY(hipGetLastError());
@@ -2397,6 +2434,15 @@ const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
     return kKernelNames[eng->jit ? 1 : 0][k];
 }
 
+int mdp_engine_launched(const mdp_engine *eng, char *buf, size_t len)
+{
+    if (!eng || !buf || !len) return mdp_set_error(MDP_EINVAL, "null argument");
+    std::string all;
+    for (const std::string &k : eng->launched) all += (all.empty() ? "" : " ") + k;
+    snprintf(buf, len, "%s", all.c_str());
+    return (int)all.size();
+}
+
 int mdp_engine_get_info(const mdp_engine *eng, mdp_engine_info *info)
 {
     if (!eng || !info) return mdp_set_error(MDP_EINVAL, "null argument");
@@ -2469,10 +2515,13 @@ int mdp_engine_work_fact(const mdp_engine *eng, uint64_t ne, uint64_t nc, mdp_wo
     // and its multiply-add into the state vector, the final prior sum
     std::vector<int> wmax(kMaxDeg + 1, -1);
     const std::vector<uint32_t> &ud = eng->udesc_d.empty() ? eng->udesc : eng->udesc_d;
+    std::set<uint32_t> distinct;  // one descriptor = one transition value P(e, c)
     for (uint32_t d : ud) {
         const uint32_t nX = (d >> kOffBits) & 31u, nA = d >> 27;
         wmax[nA] = std::max(wmax[nA], (int)nX);
         w->use_pt += 2.0 * nX + 3.0;
+        w->use_pt_min += 2.0;  // the state update
+        if (distinct.insert(d).second) w->use_pt_min += 2.0 * nX + 1.0;  // the dot product, once
     }
     w->weight_pt = 2.0 * eng->maxA;
     for (int a = 0; a <= kMaxDeg; ++a)
@@ -2481,6 +2530,7 @@ int mdp_engine_work_fact(const mdp_engine *eng, uint64_t ne, uint64_t nc, mdp_wo
     const double per_c = w->z_c + w->pc_c + w->item_c + w->q_c;
     const double per_pt = w->weight_pt + w->use_pt + w->final_pt;
     w->flop = (double)nc * per_c + (double)ne * (double)nc * per_pt;
+    w->flop_min = (double)nc * per_c + (double)ne * (double)nc * (w->weight_pt + w->use_pt_min + w->final_pt);
     return MDP_OK;
 }
 

@@ -326,7 +326,7 @@ int fut_reserve(mdp_future *f, int nwg, uint32_t tfut)
 
 // one simulation (k_future + k_future_sum) into d_counts on stream st
 int fut_launch(mdp_future *f, uint64_t seed, uint64_t rep0, uint64_t nrep, uint32_t tfut,
-               unsigned long long *d_counts, hipStream_t st, bool sum)
+               unsigned long long *d_counts, hipStream_t st, bool sum, uint32_t *derr)
 {
     FutArgs a{};
     a.n = f->n;
@@ -347,7 +347,7 @@ int fut_launch(mdp_future *f, uint64_t seed, uint64_t rep0, uint64_t nrep, uint3
 #define FUT_CASE(NMV)                                                                                   \
     case NMV:                                                                                            \
         hipLaunchKernelGGL(k_future<NMV>, dim3(nwg), dim3(kFutBlock), lds, st, a, f->dMK, f->dsrc,    \
-                           f->dpcum, f->dmiss, f->dT, f->dpartial, f->derr);                            \
+                           f->dpcum, f->dmiss, f->dT, f->dpartial, derr);                               \
         break;
         FUT_CASE(8)
         FUT_CASE(16)
@@ -466,8 +466,10 @@ int mdp_future_create(const int32_t *last_row, uint32_t n, const double *post, u
             return mdp_set_error(MDP_EHIP, "colonisation table kernel failed on device %d", device);
         }
     }
-    if (hipMalloc((void **)&f->derr, sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(f->derr, 0, sizeof(uint32_t)) != hipSuccess ||
+    // look-back overflow flags: [0] the device path (read and cleared by
+    // mdp_future_check), [1] the host-returning calls (their own)
+    if (hipMalloc((void **)&f->derr, 2 * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(f->derr, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
         hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&f->ev0) != hipSuccess || hipEventCreate(&f->ev1) != hipSuccess) {
         mdp_future_destroy(f);
@@ -505,10 +507,9 @@ int mdp_future_simulate_device(mdp_future *f, uint64_t seed, uint64_t rep0, uint
     FUT_TRY(hipSetDevice(f->device));
     hipStream_t st = (hipStream_t)stream;  // as given: NULL is HIP's null stream
     if ((rc = fut_reserve(f, fut_grid(nrep), tfut))) return rc;
-    // the look-back overflow flag is cleared in stream order, so
-    // mdp_future_check reports exactly the launches since this one
-    FUT_TRY(hipMemsetAsync(f->derr, 0, sizeof(uint32_t), st));
-    return fut_launch(f, seed, rep0, nrep, tfut, (unsigned long long *)d_counts, st, true);
+    // the look-back overflow flag is sticky: mdp_future_check reads and
+    // clears it, so one check covers every launch since the previous check
+    return fut_launch(f, seed, rep0, nrep, tfut, (unsigned long long *)d_counts, st, true, f->derr);
 }
 
 int mdp_future_check(mdp_future *f, void *stream)
@@ -518,6 +519,7 @@ int mdp_future_check(mdp_future *f, void *stream)
     hipStream_t st = (hipStream_t)stream;
     uint32_t err = 0;
     FUT_TRY(hipMemcpyAsync(&err, f->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    FUT_TRY(hipMemsetAsync(f->derr, 0, sizeof(uint32_t), st));
     FUT_TRY(hipStreamSynchronize(st));
     if (err)
         return mdp_set_error(MDP_EUNSUPPORTED,
@@ -536,12 +538,12 @@ int mdp_future_simulate(mdp_future *f, uint64_t seed, uint64_t rep0, uint64_t nr
     FUT_TRY(hipSetDevice(f->device));
     if ((rc = fut_reserve(f, fut_grid(nrep), tfut))) return rc;
     if (nrep == 0) return MDP_OK;
-    FUT_TRY(hipMemsetAsync(f->derr, 0, sizeof(uint32_t), f->stream));
-    if ((rc = fut_launch(f, seed, rep0, nrep, tfut, f->dcounts, f->stream, true))) return rc;
+    FUT_TRY(hipMemsetAsync(f->derr + 1, 0, sizeof(uint32_t), f->stream));
+    if ((rc = fut_launch(f, seed, rep0, nrep, tfut, f->dcounts, f->stream, true, f->derr + 1))) return rc;
     std::vector<unsigned long long> h(tfut);
     uint32_t err = 0;
     FUT_TRY(hipMemcpyAsync(h.data(), f->dcounts, tfut * sizeof(unsigned long long), hipMemcpyDeviceToHost, f->stream));
-    FUT_TRY(hipMemcpyAsync(&err, f->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, f->stream));
+    FUT_TRY(hipMemcpyAsync(&err, f->derr + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, f->stream));
     FUT_TRY(hipStreamSynchronize(f->stream));
     if (err)
         return mdp_set_error(MDP_EUNSUPPORTED,
@@ -559,10 +561,10 @@ int mdp_future_time_kernel(mdp_future *f, uint64_t seed, uint64_t nrep, uint32_t
     if (!ms || reps <= 0 || nrep == 0) return mdp_set_error(MDP_EINVAL, "bad timing request");
     FUT_TRY(hipSetDevice(f->device));
     if ((rc = fut_reserve(f, fut_grid(nrep), tfut))) return rc;
-    if ((rc = fut_launch(f, seed, 0, nrep, tfut, f->dcounts, f->stream, false))) return rc;
+    if ((rc = fut_launch(f, seed, 0, nrep, tfut, f->dcounts, f->stream, false, f->derr + 1))) return rc;
     FUT_TRY(hipEventRecord(f->ev0, f->stream));
     for (int i = 0; i < reps; ++i)
-        if ((rc = fut_launch(f, seed, 0, nrep, tfut, f->dcounts, f->stream, false))) return rc;
+        if ((rc = fut_launch(f, seed, 0, nrep, tfut, f->dcounts, f->stream, false, f->derr + 1))) return rc;
     FUT_TRY(hipEventRecord(f->ev1, f->stream));
     FUT_TRY(hipEventSynchronize(f->ev1));
     float t = 0;

@@ -88,3 +88,26 @@ def random_obs(rng: np.random.Generator, n: int, T: int, nvar: int, pmiss: float
         if not obs[:, col].any():
             obs[rng.integers(T), col] = 1
     return obs
+
+
+def alternating_obs(rng: np.random.Generator, n: int, T: int, nvar: int, dense: int, sparse: int,
+                    nmiss: int = 0) -> np.ndarray:
+    """Observation matrix for surveys with many variable patches: years
+    alternate between ``dense`` occupied patches (of the ``nvar`` variable
+    columns) and at most ``sparse`` occupied ones, so states carry many
+    occupied patches while consecutive years overlap in at most ``sparse``
+    (the Q groups stay small).  ``nmiss`` unvisited patches (-1) go into
+    the sparse years."""
+    obs = np.zeros((T, n), dtype=np.int32)
+    cols = np.sort(rng.choice(n, size=nvar, replace=False))
+    for t in range(T):
+        k = dense if t % 2 == 0 else int(rng.integers(1, sparse + 1))
+        on = rng.choice(cols, size=k, replace=False)
+        obs[t, on] = 1
+        if t % 2 == 1 and nmiss:
+            free = np.setdiff1d(cols, on)
+            obs[t, rng.choice(free, size=min(nmiss, free.size), replace=False)] = -1
+    for col in cols:  # every chosen column variable at least once
+        if not obs[:, col].any():
+            obs[0, col] = 1
+    return obs

@@ -67,6 +67,9 @@ def lib():
                   ctypes.c_int, ctypes.c_double, ctypes.c_double, _dp, ctypes.c_uint32]
         h.orc_dieoff_lik.argtypes = common + [_dp]
         h.orc_loss_lik.argtypes = common + [_dp, ctypes.c_uint32, _dp]
+        h.orc_scenario_vec.argtypes = [ip, ctypes.c_uint32, ctypes.c_double, ctypes.c_float, ctypes.c_double,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_int, _dp]
         h.orc_kgrid.argtypes = [ctypes.c_uint32, ctypes.c_double, ctypes.c_double, _dp]
         h.orc_philox.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                  ctypes.POINTER(ctypes.c_uint32)]
@@ -238,6 +241,19 @@ def loss_lik(row, K, dsrc, e, c, ts=20, tdis=10, m=400.0, p=0.5, d=200.0):
     if rc:
         raise RuntimeError("orc_loss_lik failed")
     return out
+
+
+def scenario_vec(row, kind, K, e, c, ts=20, tdis=10, m=400.0, p=0.5, d=200.0, dsrc=0.0):
+    """One (e, c, K[, d]) point of the die-off / loss likelihood by vector
+    propagation (orc_scenario_vec): the reference's matrix entries, products
+    associated right to left, for n up to 20 patches."""
+    row = np.ascontiguousarray(row, dtype=np.int32)
+    out = ctypes.c_double()
+    rc = lib().orc_scenario_vec(row.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row.size, m, p, d, ts, tdis,
+                                e, c, K, dsrc, 1 if kind == "loss" else 0, ctypes.byref(out))
+    if rc:
+        raise RuntimeError("orc_scenario_vec failed")
+    return out.value
 
 
 # ---------------------------------------------------------------------------

@@ -256,3 +256,96 @@ int orc_loss_lik(const int32_t *row, uint32_t n, double m, float p, double d, in
 {
     return scenario(row, n, m, p, d, ts, tdis, e, c, K, nK, dsrc, nd, 1, out);
 }
+
+/* The same likelihood by vector propagation, for n up to 20 patches where the
+ * dense 2^n x 2^n products above are out of reach (the GPU's k_scn_big range,
+ * n = 13..16).  L = 1' PK^ts P^tdis w with w[ps_j] = pr_j, applied right to
+ * left: u <- Pe (Pc u) per year.  Every matrix entry is the reference's own
+ * expression (pije :51-64, pijc :66-83 / loss.c:86-105, with the colonisation
+ * sums s1 of a row computed once in pijc's l order), and each row's sum runs
+ * over k ascending as the dense row-major product does, skipping only the
+ * entries pije / pijc return as exact zeros (j not within the source state).
+ * What differs from the reference is the association of the products (matrix
+ * powers first there), so agreement is to rounding, not bitwise; it is
+ * checked against orc_dieoff_lik / orc_loss_lik at small n
+ * (tests/test_scenario_oracle.py).  out = L for one (e, c, K[, d]). */
+static void scn_apply(int n, const double *M, const double *src, double Ks, int loss, double e, double c, double K,
+                      const double *u, double *z, double *y)
+{
+    const int ns = 1 << n;
+    /* z = Pc u: row j, columns nw >= j bitwise.  pijc's per-patch factor
+     * pt + (1-pt)(1-pn)(1-pC) + (1-pt) pn pC takes one of two values per
+     * (k, pn) for a row (pt fixed): evaluated once with the same expression */
+    double fac[32][2];
+    for (int j = 0; j < ns; ++j) {
+        for (int k = 0; k < n; ++k) {
+            double s1 = 0;
+            for (int l = 0; l < n; ++l)
+                if (l != k) s1 += M[l * n + k] * bit(j, l, n);
+            double pc;
+            if (loss) {
+                s1 += src[k] * Ks;
+                pc = c * s1;
+            } else {
+                pc = c * s1 * K;
+            }
+            const double pC = pc > 1 ? 1 : pc;
+            const int pt = bit(j, k, n);
+            for (int pn = 0; pn < 2; ++pn)
+                fac[k][pn] = pt + (1 - pt) * (1 - pn) * (1 - pC) + (1 - pt) * pn * pC;
+        }
+        double acc = 0;
+        for (int nw = j; nw < ns; nw = (nw + 1) | j) {
+            double res = 1;
+            for (int k = 0; k < n; ++k) res *= fac[k][bit(nw, k, n)];
+            acc += res * u[nw];
+        }
+        z[j] = acc;
+    }
+    /* y = Pe z: row i, columns j <= i bitwise (ascending subsets); pije's
+     * pow(E, lost) * pow(1 - E, kept) from tables of the same pow values */
+    double E = loss ? e : e / K;
+    if (E > 1) E = 1;
+    double pe[33], pk[33];
+    for (int s = 0; s <= n; ++s) {
+        pe[s] = pow(E, s);
+        pk[s] = pow(1 - E, s);
+    }
+    for (int i = 0; i < ns; ++i) {
+        double acc = 0;
+        for (int j = 0;; j = (j - i) & i) {
+            acc += pe[__builtin_popcount(i & ~j)] * pk[__builtin_popcount(j)] * z[j];
+            if (j == i) break;
+        }
+        y[i] = acc;
+    }
+}
+
+int orc_scenario_vec(const int32_t *row, uint32_t n, double m, float p, double d, int ts, int tdis, double e,
+                     double c, double K, double dsrc, int loss, double *out)
+{
+    if (n == 0 || n > 20) return -1;
+    const int ns = 1 << n;
+    int *ps;
+    float *pr;
+    const int np = states_of(row, (int)n, p, &ps, &pr);
+    double *M = malloc(sizeof(double) * n * n), *src = malloc(sizeof(double) * n);
+    dispersal((int)n, m, d, M);
+    const double a = 1.0 / m;
+    for (uint32_t j = 0; j < n; ++j) src[j] = exp(-a * (j + 1) * dsrc);
+    double *u = calloc(ns, sizeof(double)), *z = malloc(sizeof(double) * ns), *y = malloc(sizeof(double) * ns);
+    for (int j = 0; j < np; ++j) u[ps[j]] += pr[j];
+    for (int t = 0; t < tdis; ++t) {  /* P = Pe Pc at K = 1, no source */
+        scn_apply((int)n, M, src, 0.0, 0, e, c, 1.0, u, z, y);
+        memcpy(u, y, sizeof(double) * ns);
+    }
+    for (int t = 0; t < ts; ++t) {    /* PK */
+        scn_apply((int)n, M, src, K, loss, e, c, loss ? 1.0 : K, u, z, y);
+        memcpy(u, y, sizeof(double) * ns);
+    }
+    double L = 0;
+    for (int i = 0; i < ns; ++i) L += u[i];
+    *out = L;
+    free(u), free(z), free(y), free(M), free(src), free(ps), free(pr);
+    return 0;
+}

@@ -105,6 +105,30 @@ def test_device_variant_matches_host(golden, tmp_path):
         assert f.time_kernel(50000, 40, seed=3, reps=3) > 0
 
 
+def test_lookback_overflow_flag_is_sticky(golden, tmp_path):
+    """A posterior with almost no mass makes later replicates look back past
+    the engine's limit: the device flag stays set across further launches
+    until mdp_future_check reads it (and clears it); the host form reports
+    its own launch."""
+    import torch
+    _, _, row = mdp.read_survey(golden / "occupancies.txt")
+    post = _post(golden, tmp_path, "occupancies.txt", s=21)
+    tiny = post * 1e-12
+    st = torch.cuda.current_stream().cuda_stream
+    out = torch.zeros(10, dtype=torch.int64, device="cuda:0")
+    with mdp.Future(row, tiny, m=400, d=100) as bad, mdp.Future(row, post, m=400, d=100) as good:
+        bad.simulate_device(out.data_ptr(), 200_000, 10, seed=1, stream=st)  # overflows
+        bad.simulate_device(out.data_ptr(), 100, 10, seed=1, stream=st)      # does not
+        with pytest.raises(_lib.MidaspomError):
+            bad.check(st)
+        bad.check(st)  # cleared by the previous check
+        good.simulate_device(out.data_ptr(), 1000, 10, seed=1, stream=st)
+        good.check(st)
+        with pytest.raises(_lib.MidaspomError):
+            bad.simulate(200_000, 10, seed=1)
+        bad.check(st)  # the host form's overflow does not leak into the device flag
+
+
 def test_large_ensemble_properties(golden, tmp_path):
     """Config-5 shape (10^6 replicates): counts are bounded, and the GPU total
     of a split run equals the whole run (size-independent properties)."""

@@ -290,7 +290,7 @@ def test_wide_path_matches_direct_path(golden, monkeypatch, fname, s):
     with mdp.Engine(model) as eng:
         assert eng.info()["variant"] >= 20000
         b = eng.loglik_grid(g, g)
-        assert set(eng.kernel_ms()) <= {"k_zrows", "k_wq", "k_forward"}
+        assert set(eng.kernel_ms()) <= {"k_zrows", "k_witems+k_wq", "k_fwd_wide"}
     assert_loglik_close(b, a, atol=1e-11)
 
 
@@ -527,13 +527,17 @@ def test_work_fact_per_point_terms_from_the_model(golden, fname):
     used, the prior sum 2 np_last - 1; flop = nc per-c + ne nc per-point."""
     model = mdp.Model.load(golden / fname)
     ids, ss = model.year_ids, model.short_state
-    use, mmax = 0.0, {}
+    use, use_min, mmax, seen = 0.0, 0.0, {}, set()
     for t in range(1, model.tmax):
         for b in ids[t]:
             for a in ids[t - 1]:
                 A, B = int(ss[a]), int(ss[b])
                 nX, nA = bin(A & B).count("1"), bin(A).count("1")
                 use += 2 * nX + 3
+                use_min += 2
+                if (A & B, B, nA) not in seen:  # P depends on (A & B, B, |A|) only
+                    seen.add((A & B, B, nA))
+                    use_min += 2 * nX + 1
                 mmax[nA] = max(mmax.get(nA, -1), nX)
     maxA = max(mmax) if mmax else 0
     weight = 2 * maxA + sum(m + 1 for m in mmax.values())
@@ -542,9 +546,10 @@ def test_work_fact_per_point_terms_from_the_model(golden, fname):
     with mdp.Engine(model) as eng:
         eng.set_grid(g, g)
         w = eng.work_fact(8, 8)
-    assert (w["use_pt"], w["weight_pt"], w["final_pt"]) == (use, weight, final)
+    assert (w["use_pt"], w["use_pt_min"], w["weight_pt"], w["final_pt"]) == (use, use_min, weight, final)
     per_c = w["z_c"] + w["pc_c"] + w["item_c"] + w["q_c"]
     assert w["flop"] == 8 * per_c + 64 * (use + weight + final)
+    assert w["flop_min"] == 8 * per_c + 64 * (use_min + weight + final)
 
 
 def test_wide_single_year():

@@ -292,3 +292,34 @@ def test_scenario_13_patches_split_invariance():
     assert np.isfinite(a).all() and (a > 0).all()
     close(a, b, rtol=1e-12)
     close(d, b, rtol=1e-12)
+
+
+@pytest.mark.parametrize("kind,n,npts", [("dieoff", 13, 8), ("loss", 13, 8), ("dieoff", 14, 4), ("loss", 14, 4),
+                                          ("dieoff", 16, 2)])
+def test_scenario_13_to_16_patches_vs_vector_oracle(kind, n, npts):
+    """n = 13..16 (k_scn_big, the default past 12 patches) against the
+    oracle's vector-propagation form (orc_scenario_vec: the reference's
+    matrix entries, products associated right to left) at sampled
+    (e, c, K[, d]) points with a multi-year event."""
+    from concurrent.futures import ThreadPoolExecutor
+    rng = np.random.default_rng(n)
+    row = rng.choice(np.array([-1, 0, 1], dtype=np.int32), size=n, p=[0.1, 0.35, 0.55]).astype(np.int32)
+    row[0] = 1
+    e, c, K = np.array([0.15, 0.5]), np.array([0.3, 0.8]), np.array([0.5, 4.0])
+    ts, tdis = 3, 2
+    ds = mdp.dgrid(2)
+    with mdp.Scenario(row, kind, m=400, d=100) as sc:
+        got = sc.lik(e, c, K, ts=ts, tdis=tdis, **({"dsrc": ds} if kind == "loss" else {}))
+    pts = [(ie, ic, iK, idd) for ie in range(2) for ic in range(2) for iK in range(2)
+           for idd in range(2 if kind == "loss" else 1)]
+    pts = [pts[i] for i in rng.choice(len(pts), size=npts, replace=False)]
+
+    def ref(pt):
+        ie, ic, iK, idd = pt
+        return oracle.scenario_vec(row, kind, K[iK], e[ie], c[ic], ts=ts, tdis=tdis, m=400.0, d=100.0,
+                                   dsrc=float(ds[idd]))
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        refs = list(ex.map(ref, pts))
+    for pt, r in zip(pts, refs):
+        g = got[pt] if kind == "loss" else got[pt[:3]]
+        close(np.array([g]), np.array([r]))

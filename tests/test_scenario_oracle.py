@@ -5,6 +5,7 @@ the product's host-side grids against the reference formulas."""
 from __future__ import annotations
 
 import numpy as np
+import pytest
 
 import midaspom_amd as mdp
 import oracle
@@ -40,3 +41,24 @@ def test_oracle_loss_manual_p5(golden, anchors):
     L = oracle.loss_lik(row, oracle.kgrid(f["s"]), mdp.dgrid(f["v"]), f["e"], f["c"], ts=20, tdis=f["a"],
                         m=f["m"], d=f["d"])
     assert np.array_equal(np.round(L, 6), np.array(a["values_6dp"]))
+
+
+def test_vector_oracle_matches_dense_oracle():
+    """orc_scenario_vec (vector propagation, the checker for n > 12 where the
+    dense products are out of reach) against the dense restatement on random
+    rows, both scenarios, ts / tdis including 0."""
+    rng = np.random.default_rng(11)
+    for trial in range(10):
+        n = int(rng.integers(1, 9))
+        row = rng.choice(np.array([-1, 0, 1], dtype=np.int32), size=n, p=[0.2, 0.3, 0.5]).astype(np.int32)
+        ts, tdis = int(rng.integers(0, 6)), int(rng.integers(0, 4))
+        e, c = float(rng.uniform(0, 1.2)), float(rng.uniform(0, 1.5))
+        K = float(rng.choice([0.3, 1.0, 7.0]))
+        m, d, p = float(rng.choice([100, 400])), float(rng.choice([50, 200])), float(rng.choice([0.5, 0.3]))
+        dense = oracle.dieoff_lik(row, np.array([K]), e, c, ts=ts, tdis=tdis, m=m, p=p, d=d)[0]
+        vec = oracle.scenario_vec(row, "dieoff", K, e, c, ts=ts, tdis=tdis, m=m, p=p, d=d)
+        assert vec == pytest.approx(dense, rel=1e-12, abs=1e-300), (trial, n)
+        ds = float(rng.choice([100.0, 800.0]))
+        dense = oracle.loss_lik(row, np.array([K]), np.array([ds]), e, c, ts=ts, tdis=tdis, m=m, p=p, d=d)[0, 0]
+        vec = oracle.scenario_vec(row, "loss", K, e, c, ts=ts, tdis=tdis, m=m, p=p, d=d, dsrc=ds)
+        assert vec == pytest.approx(dense, rel=1e-12, abs=1e-300), (trial, n)
