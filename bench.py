@@ -10,8 +10,9 @@ timed region.  Units = grid points x year transitions = s^2 (tmax - 1) per
 rank; value = units over all ranks / max-over-ranks wall time (weak scaling:
 each rank owns an s x s slab of an (N s) x s grid).
 Other modes: --config 3 (256 x 200, 1024^2), --config 4 (dieoff 256^3),
---config 5 (future, 10^6 replicates); --backend gloo rehearses N ranks on
-fewer GPUs (collectives through host memory).
+--config 5 (future, 10^6 replicates), --config 6 (a 200-year survey with
+~4 states a year: the chunked forward path); --backend gloo rehearses N
+ranks on fewer GPUs (collectives through host memory).
 
 Workload: 64 patches x 50 years (synthetic,
 Appendix C generator, md5-checked), 512 x 512 grid, -m 400 -d 100, FP64.
@@ -45,6 +46,9 @@ HBM_PEAK_GBS = 8000.0
 CONFIGS = {
     2: dict(gen=synth.CONFIG2, s=512, name="config2: 64 patches x 50 years, 512x512 (e,c) grid"),
     3: dict(gen=synth.CONFIG3, s=1024, name="config3: 256 patches x 200 years, 1024x1024 (e,c) grid"),
+    # not a BASELINE config: a 200-year survey with ~4 states a year (3 086
+    # forward uses, past one specialised kernel: the chunked forward path)
+    6: dict(gen=synth.LONG200, s=1024, name="long200: 64 patches x 200 years, 20% unvisited, 1024x1024 (e,c) grid"),
 }
 
 
@@ -569,6 +573,9 @@ def main():
             "flop_per_launch_survey_dense": work["flop_survey"],
             "falg_step_equiv_tflops": work["flop_survey"] / (dt / args.steps) / 1e12,
             "uses_per_point": info["nuses"],
+            # forward-kernel time per (grid point x forward use): compares
+            # series of different lengths (config 3 vs the chunked config 6)
+            "fwd_ps_per_point_use": fwd_ms * 1e9 / (s * s * max(1, info["nuses"])),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -40,6 +41,7 @@
 #include <new>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mdp_internal.h"
@@ -61,8 +63,10 @@ constexpr uint32_t kOffMask = (1u << kOffBits) - 1u;
 constexpr unsigned kWaitLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), other counters untouched
 constexpr size_t kLdsBudget = 120 * 1024;  // dynamic LDS of k_coefs
 constexpr size_t kFwdLds = 48 * 1024;      // max coefficient block staged by k_forward_lds
-constexpr uint32_t kJitMaxUses = 2048;     // larger programs use the generic kernels
+constexpr uint32_t kJitMaxUses = 2048;     // uses of one forward kernel; longer series run in chunks
+constexpr uint32_t kJitChunkUses = 1024;   // target uses per chunk (hipRTC time grows faster than the code)
 constexpr size_t kJitMaxLds = 64 * 1024;   // Pc row + Q block of the direct path
+constexpr size_t kJitChunkQ = kJitMaxLds / sizeof(double) - 2;  // gathered coefficients per chunk
 
 __constant__ double c_binom[kMaxDeg + 1][kMaxDeg + 1];
 
@@ -1137,6 +1141,14 @@ struct DevCtx {
     double zs_cmax = -1.0;  // c bound the uploaded zs was pruned for (-1: none yet)
     hipModule_t jit_mod[2] = {nullptr, nullptr};  // problem-specialised forward kernel [fused]
     hipFunction_t jit_fn[2] = {nullptr, nullptr};
+    // a long series: one forward kernel per chunk of years, the state vector
+    // handed over in vscr[state][c][e] (ldv e values per (state, c))
+    std::vector<hipModule_t> cmod;
+    std::vector<hipFunction_t> cfn;
+    std::vector<uint32_t *> cqidx;  // per chunk: gather indices into the Q row (null: whole row)
+    double *vscr = nullptr;
+    size_t cap_vscr = 0;
+    uint32_t ldv = 0;
     bool fused = false;  // this grid runs the fused forward kernel (no k_qrows)
     // wide path: per-chunk item factors, state-vector scratch, tables
     double *Pg = nullptr, *V = nullptr;
@@ -1169,6 +1181,9 @@ struct mdp_engine {
     double jit_flops_pt = 0;  // its FP64 flops per grid point (counted by the generator)
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
     std::vector<char> jit_code[2];  // forward kernel code objects [fused], compiled on demand
+    std::vector<MdpJitPlan> chunks;               // > 1: the series runs as chunks of years
+    std::vector<std::vector<char>> chunk_code;    // their code objects
+    bool qglobal = false;     // Q rows built by k_zrows + k_witems + k_wq (k_qrows' tables exceed the LDS)
     int fused_mode = -1;            // MDP_FUSED: -1 auto, 0, 1
     MdpJitPlan jit_plan;
     // direct path (jit): k_qrows computes Pc[j][b] for the needed (j, b)
@@ -1547,7 +1562,8 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     d.zs_cmax = cmax;
     d.zs_len = (uint32_t)(kmax * nj);
     d.zs_kmax = (uint32_t)kmax;
-    if (eng->wide) return MDP_OK;  // no fused kernel on the wide path
+    // no fused kernel on the wide path, for a chunked series or Q rows built in HBM
+    if (eng->wide || eng->qglobal || !eng->chunks.empty()) return MDP_OK;
     // the fused kernel's column tables: one contiguous image it copies to LDS
     // (with zpad, all KZ zs rows, zero past kmax: the kernel reads them unmasked)
     const MdpJitPlan &pl = eng->jit_plan;
@@ -1595,9 +1611,75 @@ int jit_build(mdp_engine *eng, bool fused)
     return MDP_OK;
 }
 
+// Compile every chunk kernel of a long series (threads: hipRTC programs are
+// independent).
+int jit_build_chunks(mdp_engine *eng)
+{
+    const size_t nch = eng->chunks.size();
+    if (eng->chunk_code.size() == nch) return MDP_OK;
+    std::vector<std::vector<char>> code(nch);
+    std::vector<std::string> logs(nch);
+    std::vector<int> rcs(nch, 0);
+    std::vector<std::string> srcs(nch);
+    double flops = 0.0;
+    for (size_t i = 0; i < nch; ++i) {
+        srcs[i] = mdp_jit_forward_source(eng->chunks[i]);
+        flops += eng->chunks[i].flops_pt;
+        if (const char *dump = getenv("MDP_JIT_DUMP"))
+            if (FILE *f = fopen((std::string(dump) + ".chunk" + std::to_string(i) + ".hip").c_str(), "w")) {
+                fputs(srcs[i].c_str(), f);
+                fclose(f);
+            }
+    }
+    {
+        std::vector<std::thread> th;
+        size_t nt = std::min<size_t>(8, nch);
+        if (const char *tv = getenv("MDP_JIT_THREADS")) nt = std::max<size_t>(1, std::min<size_t>(nch, atoi(tv)));
+        const bool verbose = getenv("MDP_JIT_VERBOSE") != nullptr;
+        for (size_t t = 0; t < nt; ++t)
+            th.emplace_back([&, t]() {
+                for (size_t i = t; i < nch; i += nt) {
+                    const auto t0 = std::chrono::steady_clock::now();
+                    rcs[i] = mdp_jit_compile(srcs[i], code[i], logs[i]);
+                    if (verbose)
+                        fprintf(stderr, "chunk %zu: %zu uses, %.2f s\n", i, eng->chunks[i].udesc.size(),
+                                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+                }
+            });
+        for (auto &x : th) x.join();
+    }
+    for (size_t i = 0; i < nch; ++i)
+        if (rcs[i]) {
+            eng->jit_log = logs[i];
+            return mdp_set_error(MDP_EHIP, "hipRTC compilation of forward chunk %zu failed: %s", i, logs[i].c_str());
+        }
+    eng->chunk_code = std::move(code);
+    eng->jit_epl = eng->chunks[0].epl;
+    eng->jit_flops_pt = flops;
+    return MDP_OK;
+}
+
 // Load a forward kernel variant into the device (compiling it if needed).
 int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 {
+    if (!eng->chunks.empty()) {  // a long series: its chunk kernels (never fused)
+        if (!d.cfn.empty()) return MDP_OK;
+        int rc = jit_build_chunks(eng);
+        if (rc) return rc;
+        HIP_TRY(hipSetDevice(d.device));
+        for (size_t i = 0; i < eng->chunks.size(); ++i) {
+            hipModule_t m;
+            hipFunction_t f;
+            HIP_TRY(hipModuleLoadData(&m, eng->chunk_code[i].data()));
+            d.cmod.push_back(m);
+            HIP_TRY(hipModuleGetFunction(&f, m, "mdp_fwd_jit"));
+            d.cfn.push_back(f);
+            uint32_t *qi = nullptr;
+            if (!eng->chunks[i].qidx.empty() && (rc = dev_upload(&qi, eng->chunks[i].qidx))) return rc;
+            d.cqidx.push_back(qi);
+        }
+        return MDP_OK;
+    }
     if (d.jit_fn[fused]) return MDP_OK;
     int rc = jit_build(eng, fused);
     if (rc) return rc;
@@ -1724,6 +1806,10 @@ void free_device(DevCtx &d)
     for (hipEvent_t ev : d.ev) (void)hipEventDestroy(ev);
     for (hipModule_t m : d.jit_mod)
         if (m) (void)hipModuleUnload(m);
+    for (hipModule_t m : d.cmod) (void)hipModuleUnload(m);
+    for (uint32_t *q : d.cqidx)
+        if (q) (void)hipFree(q);
+    if (d.vscr) (void)hipFree(d.vscr);
     if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
@@ -1738,13 +1824,15 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     HIP_TRY(hipSetDevice(d.device));
     int rc;
     if ((rc = dev_reserve(&d.e, &d.cap_e, ne)) || (rc = dev_reserve(&d.c, &d.cap_c, nc))) return rc;
-    if (eng->wide) {
+    const bool qglobal = eng->wide || eng->qglobal;  // Q rows from k_zrows + k_witems + k_wq
+    if (eng->wide || eng->jit) {
         double cmax = 0.0;
         for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
-        if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ)) ||
-            (rc = dev_reserve(&d.Zg, &d.cap_zg, (size_t)nc * eng->nj + 1)))
-            return rc;
+        if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ))) return rc;
         if (!(d.zs_cmax == cmax) && (rc = upload_qrows_tables(eng, d, cmax))) return rc;
+    }
+    if (qglobal) {
+        if ((rc = dev_reserve(&d.Zg, &d.cap_zg, (size_t)nc * eng->nj + 1))) return rc;
         // k_zrows stages kZRows rows of explicit columns in dynamic LDS
         const size_t zl = (size_t)kZRows * d.zs_kmax * sizeof(double);
         if (zl > kQrowsLdsMax)
@@ -1752,32 +1840,36 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
                                  d.zs_kmax);
         if (zl > 64 * 1024)
             HIP_TRY(hipFuncSetAttribute((const void *)k_zrows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)zl));
-        // c values per launch: item factors within kWidePgBytes, the two state
-        // vectors of every point of a launch within kWideVBytes
-        const size_t ne_pad = (size_t)std::max<uint32_t>(1u, (ne + kBlock - 1) / kBlock) * kBlock;
+        // c values per k_witems launch: item factors within kWidePgBytes
         const size_t cap_c = std::max<size_t>(1, std::min<size_t>(nc, 65535));
         d.wide_cb_items = (uint32_t)std::min(cap_c, std::max<size_t>(1, kWidePgBytes / 8 / std::max<size_t>(1, eng->nitems)));
+        if (const char *cv = getenv("MDP_WIDE_CB"))  // tests: force several launches per slot
+            d.wide_cb_items = std::min(d.wide_cb_items, (uint32_t)std::max(1, atoi(cv)));
+        if ((rc = dev_reserve(&d.Pg, &d.cap_pg, (size_t)d.wide_cb_items * eng->nitems + 1))) return rc;
+    }
+    if (eng->wide) {
+        // c values per k_fwd_wide launch: the two state vectors of every
+        // point of a launch within kWideVBytes
+        const size_t ne_pad = (size_t)std::max<uint32_t>(1u, (ne + kBlock - 1) / kBlock) * kBlock;
+        const size_t cap_c = std::max<size_t>(1, std::min<size_t>(nc, 65535));
         d.wide_cb_fwd = (uint32_t)std::min(cap_c, std::max<size_t>(1, kWideVBytes / 8 / (2 * (size_t)eng->npmax * ne_pad)));
-        if (const char *cv = getenv("MDP_WIDE_CB")) {  // tests: force several launches per slot
-            const uint32_t v = (uint32_t)std::max(1, atoi(cv));
-            d.wide_cb_items = std::min(d.wide_cb_items, v);
-            d.wide_cb_fwd = std::min(d.wide_cb_fwd, v);
-        }
-        if ((rc = dev_reserve(&d.Pg, &d.cap_pg, (size_t)d.wide_cb_items * eng->nitems + 1)) ||
-            (rc = dev_reserve(&d.V, &d.cap_v, 2 * (size_t)eng->npmax * d.wide_cb_fwd * ne_pad)))
-            return rc;
+        if (const char *cv = getenv("MDP_WIDE_CB"))
+            d.wide_cb_fwd = std::min(d.wide_cb_fwd, (uint32_t)std::max(1, atoi(cv)));
+        if ((rc = dev_reserve(&d.V, &d.cap_v, 2 * (size_t)eng->npmax * d.wide_cb_fwd * ne_pad))) return rc;
     } else if (eng->jit) {
-        double cmax = 0.0;
-        for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
-        // (no Zg: k_qrows and the fused kernel form their Z rows themselves)
-        if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ))) return rc;
-        if (!(d.zs_cmax == cmax) && (rc = upload_qrows_tables(eng, d, cmax))) return rc;
         // one e block per c column and a small per-c problem: the forward
-        // kernel computes its column's Q itself (one launch)
+        // kernel computes its column's Q itself (one launch); never for a
+        // chunked series or Q rows built in HBM
         const uint32_t gy = (ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
-        d.fused = fused_lds(eng, d.ct_len) <= kFusedLdsMax && d.zs_kmax <= eng->jit_plan.kzmax &&
-                  (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
+        d.fused = eng->chunks.empty() && !eng->qglobal && fused_lds(eng, d.ct_len) <= kFusedLdsMax &&
+                  d.zs_kmax <= eng->jit_plan.kzmax && (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
         if ((rc = jit_load(eng, d, d.fused))) return rc;
+        if (!eng->chunks.empty()) {  // the state vectors handed between chunks
+            d.ldv = gy * kBlock * (uint32_t)eng->jit_epl;
+            uint32_t nb = 1;  // most states at a chunk boundary
+            for (size_t i = 1; i < eng->chunks.size(); ++i) nb = std::max(nb, eng->chunks[i].np[0]);
+            if ((rc = dev_reserve(&d.vscr, &d.cap_vscr, (size_t)nb * nc * d.ldv))) return rc;
+        }
         // c values per k_qrows workgroup: enough workgroups for every CU, within the LDS
         uint32_t cb = nc >= 1024 ? 4u : nc >= 512 ? 2u : 1u;  // power of two
         cb = std::min(cb, eng->nvar <= 8 ? 4u : eng->nvar <= 16 ? 2u : 1u);  // registers (k_qrows)
@@ -1856,14 +1948,30 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
         unsigned long long *st = d.stamps[2];
         const double *cv = d.c, *ctab = d.coltab;
         uint32_t ctl = d.ct_len, kmax = d.zs_kmax;
-        void *args[] = {(void *)&Qrow, (void *)&prior0, (void *)&ev,  (void *)&ne, (void *)&nc,
-                        (void *)&out,  (void *)&ld,     (void *)&one, (void *)&st, (void *)&cv,
-                        (void *)&ctab, (void *)&ctl,    (void *)&kmax};
+        double *vscr = d.vscr;
+        uint32_t ldv = d.ldv;
+        const uint32_t *qidx = nullptr;
+        void *args[] = {(void *)&Qrow, (void *)&prior0, (void *)&ev,  (void *)&ne,   (void *)&nc,
+                        (void *)&out,  (void *)&ld,     (void *)&one, (void *)&st,   (void *)&cv,
+                        (void *)&ctab, (void *)&ctl,    (void *)&kmax, (void *)&vscr, (void *)&ldv,
+                        (void *)&qidx};
         const uint64_t gy = (d.ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
         const uint32_t fc = d.fused ? (uint32_t)eng->jit_plan.fused_cols : 1u;
         const uint64_t nb = gy * ((d.nc + fc - 1) / fc);  // e blocks x column groups
         if (nb * kBlock * fc > 0xffffffffull)
             return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
+        if (!eng->chunks.empty()) {  // a long series: its chunks in order on the stream
+            const size_t nch = d.cfn.size();
+            for (size_t i = 0; i < nch; ++i) {
+                qidx = d.cqidx[i];
+                HIP_TRY(hipExtModuleLaunchKernel(d.cfn[i], (uint32_t)(nb * kBlock), 1, 1, kBlock, 1, 1, 0, s, args,
+                                                 nullptr, i == 0 ? t_kev.start : nullptr,
+                                                 i + 1 == nch ? t_kev.stop : nullptr, 0));
+            }
+            note_launch(eng, "mdp_fwd_jit<reading,maxA%u,chunks%zu%s>", eng->maxA, nch,
+                        eng->chunks[0].qidx.empty() ? "" : ",gather");
+            return MDP_OK;
+        }
         const uint32_t dyn = d.fused ? (d.ct_len + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch
         HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kBlock * fc), 1, 1, kBlock * fc, 1, 1, dyn, s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));
@@ -1954,9 +2062,9 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, uint
 // Does kernel slot k (0: Q rows / k_zpv, 1: k_coefs, 2: forward) run on this path?
 bool slot_active(const mdp_engine *eng, const DevCtx &d, int k)
 {
-    if (eng->wide) return k == 2 || eng->nitems;
+    if (eng->wide || (eng->jit && eng->qglobal)) return k == 2 || eng->nitems;
     // the direct path computes its Z rows inside k_qrows (slot 0 idle); the
-    // wide path keeps k_zrows for its item kernel
+    // wide path (and Q rows built in HBM) keeps k_zrows for its item kernel
     if (eng->jit) return k == 2 || (k == 1 && eng->nitems && !d.fused);
     return k != 1 || eng->nuses;
 }
@@ -1964,7 +2072,7 @@ bool slot_active(const mdp_engine *eng, const DevCtx &d, int k)
 int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hipStream_t s)
 {
     if (!slot_active(eng, d, k)) return MDP_OK;
-    if (eng->wide && k > 0) return launch_wide(eng, d, k, out, ld, s);
+    if ((eng->wide && k > 0) || (eng->jit && eng->qglobal && k == 1)) return launch_wide(eng, d, k, out, ld, s);
     if (k == 2) return launch_forward(eng, d, out, ld, s);
     if ((eng->jit || eng->wide) && k == 0) {  // Z rows
         const uint32_t kmax = d.zs_kmax;
@@ -2104,6 +2212,79 @@ int collect_times(mdp_engine *eng, DevCtx &d)
     return MDP_OK;
 }
 
+// Split a long series into chunks of whole years for the hipRTC forward
+// kernel: at most `U` uses per chunk (straight-line code stays a bounded
+// size), preferring a boundary year with one state (the smallest hand-over)
+// in the last quarter of a chunk.  With `gather`, each chunk stages only the
+// Q groups its uses read (at most kJitChunkQ doubles, a chunk-local layout of
+// even-aligned groups) instead of the whole Q row.
+int plan_chunks(mdp_engine *eng, uint32_t U, bool gather)
+{
+    const MdpJitPlan &base = eng->jit_plan;
+    const std::vector<uint32_t> &np = eng->np;
+    const std::vector<uint32_t> &ud = eng->udesc_d;
+    const uint32_t T = eng->tmax;
+    const int epl = base.epl > 0 ? base.epl : mdp_jit_default_epl(ud);
+    auto gsize = [](uint32_t d) { return (((d >> kOffBits) & 31u) + 2u) & ~1u; };  // nX + 1, even
+    eng->chunks.clear();
+    uint32_t t0 = 0;
+    size_t u0 = 0;
+    while (t0 + 1 < T) {
+        size_t cur = 0, qloc = 0, u1 = u0, best_u1 = 0;
+        uint32_t t1 = t0, best_t1 = 0;
+        std::set<uint32_t> loc;
+        while (t1 + 1 < T) {
+            const size_t nu = (size_t)np[t1] * np[t1 + 1];
+            size_t addq = 0;
+            std::set<uint32_t> fresh;
+            if (gather)
+                for (size_t u = u1; u < u1 + nu; ++u) {
+                    const uint32_t off = ud[u] & kOffMask;
+                    if (!loc.count(off) && fresh.insert(off).second) addq += gsize(ud[u]);
+                }
+            if (cur > 0 && (cur + nu > U || (gather && qloc + addq > kJitChunkQ))) break;
+            cur += nu;
+            qloc += addq;
+            loc.insert(fresh.begin(), fresh.end());
+            u1 += nu;
+            ++t1;
+            if (np[t1] == 1 && 4 * cur >= 3 * (size_t)U) {
+                best_t1 = t1;
+                best_u1 = u1;
+            }
+        }
+        if (t1 + 1 < T && best_t1 && best_t1 < t1) {
+            t1 = best_t1;
+            u1 = best_u1;
+        }
+        MdpJitPlan c = base;
+        c.fused = false;
+        c.epl = epl;
+        c.np.assign(np.begin() + t0, np.begin() + t1 + 1);
+        c.udesc.assign(ud.begin() + u0, ud.begin() + u1);
+        c.first = t0 == 0;
+        c.last = t1 + 1 == T;
+        if (gather) {  // chunk-local Q layout, groups in first-use order
+            std::map<uint32_t, uint32_t> lo;
+            c.qidx.clear();
+            for (uint32_t &d : c.udesc) {
+                const uint32_t off = d & kOffMask;
+                auto it = lo.find(off);
+                if (it == lo.end()) {
+                    it = lo.emplace(off, (uint32_t)c.qidx.size()).first;
+                    for (uint32_t m = 0; m < gsize(d); ++m) c.qidx.push_back(off + std::min(m, (d >> kOffBits) & 31u));
+                }
+                d = (d & ~kOffMask) | it->second;
+            }
+            c.ldq_row = base.ldQ;
+        }
+        eng->chunks.push_back(std::move(c));
+        t0 = t1;
+        u0 = u1;
+    }
+    return eng->chunks.empty() ? mdp_set_error(MDP_EUNSUPPORTED, "no forward chunks") : MDP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2145,14 +2326,20 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
         const char *jv = getenv("MDP_JIT");
         const bool want = !eng->wide && !(jv && !strcmp(jv, "0"));
         bool want_jit = want && build_direct_plan(eng, p) == MDP_OK;
-        if (want_jit) {  // colonisation rows without pruning must fit the LDS
-            const uint32_t z = ((eng->n - eng->nvar) + 7u) & ~7u;
-            (void)z;
-            want_jit = qrows_lds(eng, 1) <= kQrowsLdsMax;
-        }
+        // k_qrows keeps every table of its c values in LDS; larger problems
+        // build their Q rows in HBM (k_zrows + k_witems + k_wq, the same bits)
+        const char *qg = getenv("MDP_QGLOBAL");
+        eng->qglobal = want_jit && (qrows_lds(eng, 1) > kQrowsLdsMax || (qg && atoi(qg) != 0));
         eng->ldQ = ((size_t)eng->ncoef_d + 1) & ~(size_t)1;
-        if (want_jit && eng->nuses > 0 && eng->nuses <= kJitMaxUses &&
-            eng->ldQ * sizeof(double) <= kJitMaxLds) {
+        // a series longer than kJitMaxUses uses (or a Q row past the LDS) runs
+        // as chunks of years (MDP_JIT_CHUNK / MDP_JIT_GATHER force them)
+        uint32_t chunk_uses = kJitChunkUses;
+        const char *cv = getenv("MDP_JIT_CHUNK");
+        if (cv) chunk_uses = (uint32_t)std::max(1, atoi(cv));
+        const char *gv = getenv("MDP_JIT_GATHER");
+        const bool gather = eng->ldQ * sizeof(double) > kJitMaxLds || (gv && atoi(gv) != 0);
+        const bool chunked = eng->nuses > kJitMaxUses || gather || (cv && eng->nuses > chunk_uses);
+        if (want_jit && eng->nuses > 0) {
             MdpJitPlan &plan = eng->jit_plan;
             plan.np = eng->np;
             plan.udesc = eng->udesc_d;
@@ -2200,6 +2387,19 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
                 const size_t kz = std::max<size_t>(8, kmax_max);
                 plan.zpad = fused_lds(eng, ((plan.off_zs + kz * eng->nj) + 127) & ~(size_t)127) <= kFusedLdsMax;
             }
+            if (chunked && (rc = plan_chunks(eng, chunk_uses, gather))) {
+                delete eng;
+                return rc;
+            }
+            if (jit_check && ndev == 0 && chunked) {
+                const int r = jit_build_chunks(eng);
+                if (!r)
+                    mdp_set_error(MDP_ENODEV, "no HIP device available (forward kernels compiled; %zu chunks%s; "
+                                  "nj %u nitems %u ldQ %zu qglobal %d)", eng->chunks.size(), gather ? ", gathered Q" : "",
+                                  plan.nj, plan.nitems, (size_t)plan.ldQ, (int)eng->qglobal);
+                delete eng;
+                return r ? r : MDP_ENODEV;
+            }
             if (jit_check && ndev == 0) {
                 const int r0 = jit_build(eng, false), r1 = r0 ? r0 : jit_build(eng, true);
                 uint32_t ipr = 0;  // most items of one row
@@ -2214,7 +2414,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
                 delete eng;
                 return r1 ? r1 : MDP_ENODEV;
             }
-            if (jit_build(eng, eng->fused_mode == 1) == MDP_OK) eng->jit = true;
+            if ((chunked ? jit_build_chunks(eng) : jit_build(eng, eng->fused_mode == 1)) == MDP_OK) eng->jit = true;
             else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the generic kernel:\n%s\n",
                          eng->jit_log.c_str());
         }
@@ -2429,6 +2629,8 @@ const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
     if (!eng || k < 0 || k >= 3) return "";
     if (eng->wide) return k < 2 && !eng->nitems ? "" : kKernelNames[2][k];
+    if (eng->jit && eng->qglobal)  // Q rows built in HBM, then the hipRTC forward kernel
+        return k < 2 && !eng->nitems ? "" : k == 2 ? "k_forward" : kKernelNames[2][k];
     // direct path: Z rows inside k_qrows (slot 0 idle); fused: one kernel
     if (eng->jit && (k == 0 || (k == 1 && (eng->devs.empty() || eng->devs[0].fused)))) return "";
     return kKernelNames[eng->jit ? 1 : 0][k];

@@ -93,18 +93,37 @@ std::map<uint64_t, std::vector<char>> g_code;  // in-process code-object cache
 
 }  // namespace
 
-std::string mdp_jit_forward_source(MdpJitPlan &pl)
+namespace {
+
+// weight table: every (|A|, m) a transition needs, W = x^{|A|-m} y^m
+int weight_index(const std::vector<uint32_t> &udesc, std::map<std::pair<uint32_t, uint32_t>, int> &widx,
+                 uint32_t &dmax)
 {
-    // weight table: every (|A|, m) a transition needs, W = x^{|A|-m} y^m
-    std::map<std::pair<uint32_t, uint32_t>, int> widx;
-    uint32_t dmax = 0;
-    for (uint32_t d : pl.udesc) {
+    dmax = 0;
+    for (uint32_t d : udesc) {
         const uint32_t nX = (d >> 22) & 31u, nA = d >> 27;
         dmax = nA > dmax ? nA : dmax;
         for (uint32_t m = 0; m <= nX; ++m) widx.emplace(std::make_pair(nA, m), 0);
     }
     int nw = 0;
     for (auto &kv : widx) kv.second = nw++;
+    return nw;
+}
+
+}  // namespace
+
+int mdp_jit_default_epl(const std::vector<uint32_t> &udesc)
+{
+    std::map<std::pair<uint32_t, uint32_t>, int> widx;
+    uint32_t dmax;
+    return weight_index(udesc, widx, dmax) <= 64 ? 2 : 1;
+}
+
+std::string mdp_jit_forward_source(MdpJitPlan &pl)
+{
+    std::map<std::pair<uint32_t, uint32_t>, int> widx;
+    uint32_t dmax = 0;
+    const int nw = weight_index(pl.udesc, widx, dmax);
     const int EPL = pl.epl > 0 ? pl.epl : (nw <= 64 ? 2 : 1);
     pl.epl = EPL;
     const uint32_t np0 = pl.np[0];
@@ -112,7 +131,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     for (uint32_t x : pl.np) npmax = x > npmax ? x : npmax;
     std::ostringstream o;
     o << kPrelude;
-    o << "#define EPL " << EPL << "\n#define LDQ " << pl.ldQ << "\n#define NPMAX " << npmax
+    const bool gather = !pl.qidx.empty();
+    const size_t ldq_local = gather ? ((pl.qidx.size() + 1) & ~(size_t)1) : pl.ldQ;
+    o << "#define EPL " << EPL << "\n#define LDQ " << ldq_local << "\n#define LDQG "
+      << (gather ? pl.ldq_row : pl.ldQ) << "\n#define NQG " << pl.qidx.size() << "\n#define NPMAX " << npmax
       << "\n#define DMAX " << dmax << "\n#define NW " << (nw ? nw : 1) << "\n";
     // diagnostic phase stamps: s_memtime (slots 0-3) and s_memrealtime (6, 7)
     auto stamp = [&](int slot) {
@@ -138,7 +160,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
       << "void mdp_fwd_jit(\n"
          "    const double *__restrict__ Qrow, double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
          "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps,\n"
-         "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax)\n{\n"
+         "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax,\n"
+         "    double *__restrict__ vscr, u32 ldv, const u32 *__restrict__ qidx)\n{\n"
          "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ + 2];\n"
       << stamp(6) << stamp(0) <<
          // XCD-aware order: the dispatcher deals blocks round-robin over the 8
@@ -177,9 +200,13 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         for (auto &kv : widx)
             w << "        W[i][" << kv.second << "] = xp[" << (kv.first.first - kv.first.second) << "] * yp["
               << kv.first.second << "];\n";
-        w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < " << np0
-          << " ? 1.0 : 0.0;\n"
-             "    }\n";
+        if (pl.first)
+            w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < " << np0
+              << " ? 1.0 : 0.0;\n";
+        else  // the previous chunk's end vector (ldv covers every lane's e)
+            w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < " << np0
+              << " ? vscr[((size_t)k * nc + ic) * ldv + ie[i]] : 0.0;\n";
+        w << "    }\n";
         wblock = w.str();
     }
     o << "    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n";
@@ -206,9 +233,31 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        }\n"
              "    }\n";
     };
-    if (!pl.fused) {
+    if (!pl.fused && !gather) {
         stage("Ql", "Qrow + (size_t)ic * LDQ", "LDQ");  // this column's Q row (k_qrows)
         o << stamp(1);
+    } else if (!pl.fused) {
+        // this chunk's coefficients gathered from the column's Q row: every
+        // load in flight before the (unconditional) stores, as in stage()
+        o << "    {\n"
+             "        const double *src_ = Qrow + (size_t)ic * LDQG;\n"
+             "        constexpr u32 NK = (NQG + NT - 1) / NT;\n"
+             "        u32 x_[NK];\n"
+             "        double t_[NK];\n"
+             "#pragma unroll\n"
+             "        for (u32 k = 0; k < NK; ++k) {\n"
+             "            const u32 i = threadIdx.x + k * NT;\n"
+             "            x_[k] = qidx[i < NQG ? i : 0];\n"
+             "        }\n"
+             "#pragma unroll\n"
+             "        for (u32 k = 0; k < NK; ++k) t_[k] = src_[x_[k]];\n"
+             "#pragma unroll\n"
+             "        for (u32 k = 0; k < NK; ++k) {\n"
+             "            const u32 i = threadIdx.x + k * NT;\n"
+             "            Ql[i < NQG ? i : LDQ] = t_[k];\n"
+             "        }\n"
+             "    }\n"
+          << stamp(1);
     } else {
         // the k_qrows phases for this one c value (spom_engine.hip k_qrows):
         // Z per hidden-state row, Pc per item, Q per entry -- all in LDS.
@@ -422,7 +471,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         }
     }
     // flops per point: weight table, transitions (below), prior sum
-    double flops = 2.0 * dmax + (double)nw + 2.0 * npmax;
+    double flops = 2.0 * dmax + (double)nw + (pl.last ? 2.0 * npmax : 0.0);
     std::vector<uint32_t> slot_key(nslot, 0);
     std::vector<size_t> slot_next(nslot, SIZE_MAX);  // SIZE_MAX: free / dead
     // returns the expression for use u, emitting "pc[i][s] = P;" first when
@@ -475,14 +524,22 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         o << "    }\n";
     }
     o << "    }}\n" << stamp(3) << "#define NPLAST " << pl.np.back() << "\n";
-    o << "#pragma unroll\n"
-         "    for (int i = 0; i < EPL; ++i) {\n"
-         "        double L = 0.0;\n"
-         "#pragma unroll\n"
-         "        for (int l = 0; l < NPLAST; ++l) L += v[i][l] * prior0;\n"
-         "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
-         "    }\n"
-      << stamp(7) << "}\n";
+    if (pl.last)
+        o << "#pragma unroll\n"
+             "    for (int i = 0; i < EPL; ++i) {\n"
+             "        double L = 0.0;\n"
+             "#pragma unroll\n"
+             "        for (int l = 0; l < NPLAST; ++l) L += v[i][l] * prior0;\n"
+             "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
+             "    }\n";
+    else  // hand the end vector to the next chunk
+        o << "    if (ic < nc) {\n"
+             "#pragma unroll\n"
+             "        for (int i = 0; i < EPL; ++i)\n"
+             "#pragma unroll\n"
+             "            for (int l = 0; l < NPLAST; ++l) vscr[((size_t)l * nc + ic) * ldv + ie[i]] = v[i][l];\n"
+             "    }\n";
+    o << stamp(7) << "}\n";
     pl.flops_pt = flops;
     o << "// EPL_CHOSEN " << EPL << "\n";
     return o.str();

@@ -31,7 +31,20 @@ struct MdpJitPlan {
     int slots = 8;                // registers caching transitions that recur (0: none)
     int wpe = 0;                  // minimum waves per SIMD asked of the compiler (0: its default)
     double flops_pt = 0;          // out: FP64 flops per grid point of the generated code
+    // a chunk of a long series (main_MIDASPOM.c:371-384 has no length limit):
+    // np / udesc cover years [t0, t1] of the series; a chunk that is not the
+    // first reads its start vector from the scratch vscr[state][c][e], one
+    // that is not the last stores its end vector there instead of the output
+    bool first = true, last = true;
+    // gather staging: Ql[i] = Qrow[qidx[i]] (udesc offsets are then into
+    // this chunk's own layout); empty: the whole Q row of ldQ doubles
+    std::vector<uint32_t> qidx;
+    size_t ldq_row = 0;           // Q row stride when gathering (the k_qrows row)
 };
+
+// Grid points per lane for a program of these uses (2, or 1 when the weight
+// table is large); chunks of one series share it, as they share a scratch.
+int mdp_jit_default_epl(const std::vector<uint32_t> &udesc);
 
 // HIP source of `mdp_fwd_jit` for this plan; sets plan.epl when it was 0.
 std::string mdp_jit_forward_source(MdpJitPlan &plan);

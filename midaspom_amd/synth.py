@@ -20,6 +20,10 @@ CONFIG3 = dict(n=256, T=200, nvar=8, e=0.1, c=0.05, m=400, d=100, pmiss=0.03, se
 # its states (quirk Q1, main_MIDASPOM.c:244) and the MPI build reports
 # Ltot -153.68039 at -s 17 (main_MIDASPOM_MPI.c:262).
 Q1_MID = dict(CONFIG2, v0=28)
+# A 200-year survey with about four possible states per year (20 % of the
+# variable patches unvisited): 3 086 forward uses per grid point, past the
+# 2 048 of one specialised kernel -- the engine runs it as chunks of years.
+LONG200 = dict(CONFIG2, T=200, pmiss=0.2, seed=11)
 MD5 = {
     "config2": "6bd6f4bf7e69d794078d9c5718cda157",
     "config3": "5cf6ad09063e720a952fcd4c32b47030",
