@@ -64,6 +64,7 @@ def main(argv=None) -> int:
 
     a = parse_args(sys.argv[1:] if argv is None else argv)
     rank, world, local = mdist.env_rank_world()
+    mpi = world > 1 or mdist.under_launcher()
     root = rank == 0
 
     def out(text, all_ranks=False):
@@ -71,7 +72,7 @@ def main(argv=None) -> int:
             sys.stdout.write(text)
             sys.stdout.flush()
 
-    if world > 1:  # unguarded in the MPI build: every rank prints it (:78)
+    if mpi:  # unguarded in the MPI build: every rank prints it (:78)
         out("------ MIDASPOM, beta MPI version ------\n-> N. Alcala, E. M. Cole, and N. A. Rosenberg <-\n",
             all_ranks=True)
     else:
@@ -89,10 +90,10 @@ def main(argv=None) -> int:
         sys.stderr.write(f"\nmidaspom: {exc}\n")
         return 2
     out("done\n")
-    _print_problem(model, out, mpi=world > 1)
+    _print_problem(model, out, mpi=mpi)
     start = time.time()
 
-    if world == 1:
+    if not mpi:
         out("Starting parallel likelihood computation\n")
         ngpu = a.g if a.g is not None else int(os.environ.get("MIDASPOM_GPUS", "0"))
         with mdp.Engine(model, n_devices=max(0, ngpu)) as eng:  # 0: the current device
@@ -132,13 +133,13 @@ def main(argv=None) -> int:
         if not root:
             return 0
 
-    finish(lik, win, a.o, world, out)
+    finish(lik, win, a.o, mpi, out)
     elapsed = int(time.time()) - int(start)
     out(f"done\n Total running time: {elapsed / 60.0:.2f} min\n")
     return 0
 
 
-def finish(lik, win, path, world, out):
+def finish(lik, win, path, mpi, out):
     """Normalise and write (main_MIDASPOM.c:413-436); the MPI build writes
     raw log-likelihoods instead when Ltot == 0 (main_MIDASPOM_MPI.c:527)."""
     import midaspom_amd as mdp
@@ -146,7 +147,7 @@ def finish(lik, win, path, world, out):
     ltot = mdp.log_total(lik, win)
     out(f"Total log-likelihood={ltot:.5f}\n")
     out(f"Writing output in file {path}... ")
-    mdp.write_posterior(path, lik, ltot, raw=(world > 1 and ltot == 0))
+    mdp.write_posterior(path, lik, ltot, raw=bool(mpi) and ltot == 0)
     return ltot
 
 

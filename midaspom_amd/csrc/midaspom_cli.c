@@ -8,10 +8,15 @@
  * same bit layout (%.20lf\t per cell, \n per row).  The grid loop :341-395
  * runs on the GPU through the C ABI in include/midaspom.h.
  *
- * Extensions: -g <N> (or MIDASPOM_GPUS=N) spreads the e rows over N GPUs of
- * this node (contiguous slabs as main_MIDASPOM_MPI.c:361-368).
+ * Extensions: -g <N> (or MIDASPOM_GPUS=N) splits the e rows into N
+ * contiguous slabs (main_MIDASPOM_MPI.c:361-368) dealt round-robin over the
+ * node's visible GPUs (N may exceed them: slabs then share a GPU, each on
+ * its own stream).  MIDASPOM_TIMING=1 prints where the wall time went
+ * (parse, HIP start-up, engine set-up incl. hipRTC, grid, Ltot, write) to
+ * stderr.
  */
 #include <ctype.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <time.h>
@@ -19,8 +24,17 @@
 
 #include "midaspom.h"
 
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 int main(int argc, char **argv)
 {
+    const double t_start = now_s();
+    const int timing = getenv("MIDASPOM_TIMING") && atoi(getenv("MIDASPOM_TIMING")) != 0;
     printf("------ MIDASPOM, beta version ------\n-> N. Alcala, E. M. Cole, and N. A. Rosenberg <-\n");
 
     float prior_occ = 0.5f;            /* -p, float32 as :66 */
@@ -108,19 +122,37 @@ int main(int argc, char **argv)
     time_t start, end;
     time(&start);
     printf("Starting parallel likelihood computation\n");
+    const double t_parsed = now_s();
     mdp_engine *eng = NULL;
-    rc = mdp_engine_create(&pb, NULL, ngpu > 0 ? ngpu : 0, &eng);
+    int *devs = NULL;
+    if (ngpu > 0) {  /* slabs round-robin over the visible GPUs */
+        const int nvis = mdp_device_count();
+        devs = (int *)malloc(sizeof(int) * (size_t)ngpu);
+        if (!devs) {
+            fprintf(stderr, "midaspom: out of host memory\n");
+            return 2;
+        }
+        for (int i = 0; i < ngpu; i++) devs[i] = nvis > 0 ? i % nvis : i;
+    } else {
+        (void)mdp_device_count();  /* HIP start-up, timed on its own */
+    }
+    const double t_hip = now_s();
+    rc = mdp_engine_create(&pb, devs, ngpu > 0 ? ngpu : 0, &eng);
+    const double t_setup = now_s();
     if (!rc) rc = mdp_loglik_grid(eng, grid, nstep, grid, nstep, lik);
+    free(devs);
     if (rc) {
         fprintf(stderr, "midaspom: %s\n", mdp_last_error());
         mdp_engine_destroy(eng);
         return 3;
     }
     mdp_engine_destroy(eng);
+    const double t_grid = now_s();
     for (unsigned ie = 0; ie < nstep; ie++) printf("%.2f%% done\n", ((float)ie + 1) * 100.0 / nstep);
     printf("end likelihood computation\n");
 
     const double ltot = mdp_log_total(lik, nstep, win);
+    const double t_ltot = now_s();
     printf("Total log-likelihood=%.5lf\n", ltot);
     printf("Writing output in file %s... ", fout);
     rc = mdp_write_posterior(fout, lik, nstep, ltot, 0);
@@ -128,6 +160,11 @@ int main(int argc, char **argv)
         fprintf(stderr, "midaspom: %s\n", mdp_last_error());
         return 2;
     }
+    if (timing)
+        fprintf(stderr,
+                "midaspom timing (s): parse %.3f hip_init %.3f setup %.3f grid %.3f ltot %.3f write %.3f total %.3f\n",
+                t_parsed - t_start, t_hip - t_parsed, t_setup - t_hip, t_grid - t_setup, t_ltot - t_grid,
+                now_s() - t_ltot, now_s() - t_start);
     time(&end);
     printf("done\n Total running time: %.2lf min\n", difftime(end, start) / 60.0);
     free(grid);

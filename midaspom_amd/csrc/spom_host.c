@@ -15,10 +15,12 @@
  *   mdp_write_posterior                :427-436  (+ main_MIDASPOM_MPI.c:527)
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "mdp_internal.h"
 
@@ -266,34 +268,165 @@ double mdp_grid(uint32_t s, double lo, double hi, double *g)
     return win;
 }
 
+/* ------------------------------------------------------------------ */
+/* host threads for the per-cell work of a large grid (exp, formatting) */
+/* ------------------------------------------------------------------ */
+
+/* OMP_NUM_THREADS when set, else the online CPUs, at most 16; one thread
+ * below 64 Ki cells */
+static unsigned host_threads(size_t cells)
+{
+    if (cells < (1u << 16)) return 1;
+    long nt = sysconf(_SC_NPROCESSORS_ONLN);
+    const char *ev = getenv("OMP_NUM_THREADS");
+    if (ev && atoi(ev) > 0) nt = atoi(ev);
+    if (nt > 16) nt = 16;
+    return nt < 1 ? 1u : (unsigned)nt;
+}
+
+typedef struct {
+    void *arg;
+    void (*fn)(void *, size_t, size_t);
+    size_t i0, i1;
+} host_job;
+
+static void *host_job_run(void *p)
+{
+    host_job *j = (host_job *)p;
+    j->fn(j->arg, j->i0, j->i1);
+    return NULL;
+}
+
+/* fn(arg, i0, i1) over [0, n) in nt contiguous ranges */
+static void host_parallel(unsigned nt, size_t n, void *arg, void (*fn)(void *, size_t, size_t))
+{
+    if (nt > n) nt = n ? (unsigned)n : 1u;
+    host_job jobs[16];
+    pthread_t th[16];
+    int started[16] = {0};
+    for (unsigned t = 0; t < nt; ++t) {
+        jobs[t].arg = arg;
+        jobs[t].fn = fn;
+        jobs[t].i0 = n * t / nt;
+        jobs[t].i1 = n * (t + 1) / nt;
+    }
+    for (unsigned t = 1; t < nt; ++t) started[t] = pthread_create(&th[t], NULL, host_job_run, &jobs[t]) == 0;
+    host_job_run(&jobs[0]);
+    for (unsigned t = 1; t < nt; ++t) {
+        if (started[t]) pthread_join(th[t], NULL);
+        else host_job_run(&jobs[t]);  /* no thread: run it here */
+    }
+}
+
+typedef struct {
+    const double *lik;
+    double *ex;
+} exp_arg;
+
+static void exp_range(void *p, size_t i0, size_t i1)
+{
+    exp_arg *a = (exp_arg *)p;
+    for (size_t i = i0; i < i1; ++i) a->ex[i] = exp(a->lik[i]);
+}
+
+/* main_MIDASPOM.c:413-425.  The exps of a large grid are evaluated in
+ * threads; the weighted sum runs in the reference's order (k outer, l
+ * inner), so Ltot is bit-identical to the sequential form. */
 double mdp_log_total(const double *lik, uint32_t s, double win)
 {
+    const size_t cells = (size_t)s * s;
+    const unsigned nt = host_threads(cells);
+    double *ex = nt > 1 ? (double *)malloc(sizeof(double) * cells) : NULL;
+    if (ex) {
+        exp_arg a = {lik, ex};
+        host_parallel(nt, cells, &a, exp_range);
+    }
     double acc = 0;
     for (uint32_t k = 0; k < s; k++) {
         const double wk = (k == 0 || k == s - 1) ? 0.5 : 1.0;
         for (uint32_t l = 0; l < s; l++) {
             double w = wk;
             if (l == 0 || l == s - 1) w *= 0.5;
-            acc += exp(lik[(size_t)k * s + l]) * w;
+            const size_t i = (size_t)k * s + l;
+            acc += (ex ? ex[i] : exp(lik[i])) * w;
         }
     }
+    free(ex);
     return 2 * log(win) + log(acc);
 }
 
+typedef struct {
+    const double *lik;
+    uint32_t s;
+    double ltot;
+    int raw;
+    char **buf;     /* per row range: the formatted text */
+    size_t *len;
+    size_t nparts;  /* rows are split into nparts ranges */
+    int fail;
+} fmt_arg;
+
+static void fmt_range(void *p, size_t q0, size_t q1)
+{
+    fmt_arg *a = (fmt_arg *)p;
+    for (size_t q = q0; q < q1; ++q) {
+        const uint32_t r0 = (uint32_t)((size_t)a->s * q / a->nparts), r1 = (uint32_t)((size_t)a->s * (q + 1) / a->nparts);
+        size_t cap = (size_t)(r1 - r0) * (a->s * 26u + 1u) + 64, used = 0;
+        char *b = (char *)malloc(cap);
+        if (!b) {
+            a->fail = 1;
+            continue;
+        }
+        for (uint32_t i = r0; i < r1; i++) {
+            for (uint32_t j = 0; j <= a->s; j++) {
+                /* room for one cell: %.20lf of the largest double is 331 bytes */
+                if (cap - used < 400) {
+                    cap = cap * 2 + 1024;
+                    char *nb = (char *)realloc(b, cap);
+                    if (!nb) {
+                        free(b);
+                        a->fail = 1;
+                        return;
+                    }
+                    b = nb;
+                }
+                if (j == a->s) {
+                    b[used++] = '\n';
+                    break;
+                }
+                const double v = a->lik[(size_t)i * a->s + j];
+                used += (size_t)snprintf(b + used, cap - used, "%.20lf\t", a->raw ? v : exp(v - a->ltot));
+            }
+        }
+        a->buf[q] = b;
+        a->len[q] = used;
+    }
+}
+
+/* main_MIDASPOM.c:427-436 (raw: the MPI build's Ltot == 0 branch,
+ * main_MIDASPOM_MPI.c:527).  Rows of a large grid are formatted in threads
+ * and written in order: the bytes are those of the sequential writer. */
 int mdp_write_posterior(const char *path, const double *lik, uint32_t s, double ltot, int raw)
 {
     FILE *f = fopen(path, "wb");
     if (!f) return mdp_set_error(MDP_EIO, "cannot open output file '%s'", path);
-    static __thread char line[1 << 16];
-    setvbuf(f, NULL, _IOFBF, 1 << 20);
-    for (uint32_t i = 0; i < s; i++) {
-        for (uint32_t j = 0; j < s; j++) {
-            const double v = lik[(size_t)i * s + j];
-            int len = snprintf(line, sizeof line, "%.20lf\t", raw ? v : exp(v - ltot));
-            fwrite(line, 1, (size_t)len, f);
-        }
-        fputc('\n', f);
+    const unsigned nt = host_threads((size_t)s * s);
+    const size_t nparts = nt > 1 ? (size_t)nt * 4 : 1;  /* a few ranges per thread */
+    fmt_arg a = {lik, s, ltot, raw, (char **)calloc(nparts, sizeof(char *)), (size_t *)calloc(nparts, sizeof(size_t)),
+                 nparts, 0};
+    int rc = MDP_OK;
+    if (!a.buf || !a.len) {
+        rc = mdp_set_error(MDP_ENOMEM, "out of host memory");
+    } else {
+        host_parallel(nt, nparts, &a, fmt_range);
+        if (a.fail) rc = mdp_set_error(MDP_ENOMEM, "out of host memory");
+        for (size_t q = 0; q < nparts && !rc; ++q)
+            if (a.len[q] && fwrite(a.buf[q], 1, a.len[q], f) != a.len[q]) rc = mdp_set_error(MDP_EIO, "write to '%s' failed", path);
     }
-    if (fclose(f) != 0) return mdp_set_error(MDP_EIO, "write to '%s' failed", path);
-    return MDP_OK;
+    if (a.buf)
+        for (size_t q = 0; q < nparts; ++q) free(a.buf[q]);
+    free(a.buf);
+    free(a.len);
+    if (fclose(f) != 0 && !rc) rc = mdp_set_error(MDP_EIO, "write to '%s' failed", path);
+    return rc;
 }

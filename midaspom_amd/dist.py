@@ -66,6 +66,13 @@ def env_rank_world():
         int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def under_launcher() -> bool:
+    """Started by torchrun (the `mpirun -np N` of the _MPI programs): the
+    drop-ins then behave as the MPI builds even for N = 1 (banner, per-rank
+    lines, the gather), as `mpirun -np 1 MIDASPOM_MPI.out` does."""
+    return "WORLD_SIZE" in os.environ and "RANK" in os.environ
+
+
 def gpu_slab_compute(model, device_index: int):
     """compute(e_slab, c) on this rank's GPU through the C ABI; the result
     stays in HBM (a torch tensor) until the gather."""

@@ -115,7 +115,7 @@ def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     rank, world, local = mdist.env_rank_world()
     root = rank == 0
-    mpi = world > 1
+    mpi = world > 1 or mdist.under_launcher()
 
     def out(text, all_ranks=False):
         if root or all_ranks:

@@ -127,7 +127,7 @@ def main(argv=None) -> int:
     kind = argv[0]
     rank, world, local = mdist.env_rank_world()
     root = rank == 0
-    mpi = world > 1
+    mpi = world > 1 or mdist.under_launcher()
 
     def out(text, all_ranks=False):
         if root or all_ranks:

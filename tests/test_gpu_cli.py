@@ -85,6 +85,71 @@ def test_torchrun_cli_two_ranks(golden, tmp_path):
     # nextid after the dispersal matrix is checked in tests/test_cli_host.py)
 
 
+def test_compiled_cli_slabs_round_robin_over_devices(golden, tmp_path):
+    """-g 3 on a box with fewer GPUs: the three e-row slabs are dealt
+    round-robin over the visible devices (one engine device context and
+    stream each, main_MIDASPOM_MPI.c:361-368); the file equals -g 1's byte
+    for byte.  MIDASPOM_TIMING=1 reports the wall-time split on stderr."""
+    inp = str(golden / "config2_64x50.txt")
+    outs = {}
+    for g in ("1", "3"):
+        out = tmp_path / f"g{g}.txt"
+        r = subprocess.run([str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", "203", "-g", g, "-i", inp,
+                            "-o", str(out)], capture_output=True, text=True, timeout=180,
+                           env=dict(os.environ, MIDASPOM_TIMING="1"))
+        assert r.returncode == 0, r.stderr
+        assert "midaspom timing (s): parse" in r.stderr and " write " in r.stderr
+        outs[g] = out.read_bytes()
+    assert outs["1"] == outs["3"]
+
+
+def test_engine_several_contexts_one_device(golden):
+    """mdp_loglik_grid over several device contexts (here all on device 0):
+    the multi-device branch, slabs on their own streams, same result."""
+    import numpy as np
+    import midaspom_amd as mdp
+    model = mdp.Model.load(golden / "config3_256x200.txt")
+    g, _ = mdp.grid(157)
+    with mdp.Engine(model, devices=[0]) as eng:
+        one = eng.loglik_grid(g, g)
+    with mdp.Engine(model, devices=[0, 0, 0, 0]) as eng:
+        assert eng.info()["n_devices"] == 4
+        four = eng.loglik_grid(g, g)
+    assert np.array_equal(one, four)
+
+
+@pytest.mark.parametrize("prog", ["midaspom_amd", "midaspom_amd.scenario", "midaspom_amd.future"])
+def test_torchrun_one_rank_rccl(golden, tmp_path, prog):
+    """`torchrun --nproc-per-node 1 ... --backend nccl` (the launcher starts
+    the rank before any GPU call): RCCL initialises and the gather / reduce
+    runs, as `mpirun -np 1 MIDASPOM_MPI.out` runs the MPI program; the file
+    equals the single-process one byte for byte."""
+    inp = str(golden / "occupancies.txt")
+    if prog == "midaspom_amd":
+        args = [*FLAGS]
+    elif prog == "midaspom_amd.scenario":
+        args = ["dieoff", *SCN_FLAGS["dieoff"]]
+    else:
+        post = tmp_path / "post.txt"
+        r = subprocess.run([str(_lib.CLI_PATH), *FLAGS, "-i", inp, "-o", str(post)], capture_output=True, text=True,
+                           timeout=180)
+        assert r.returncode == 0, r.stderr
+        args = ["-a", "20", "-m", "400", "-d", "100", "-q", str(post), "-n", "20000", "-r", "77"]
+    single, multi = tmp_path / "single.txt", tmp_path / "multi.txt"
+    r1 = subprocess.run([sys.executable, "-m", prog, *args, "-i", inp, "-o", str(single)],
+                        capture_output=True, text=True, timeout=180, env=_env(), cwd=ROOT)
+    assert r1.returncode == 0, r1.stderr
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", prog, *(args[:1] if prog.endswith("scenario") else []), "--backend", "nccl",
+           *(args[1:] if prog.endswith("scenario") else args), "-i", inp, "-o", str(multi)]
+    r2 = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    assert multi.read_bytes() == single.read_bytes()
+    assert "Gathering data from 0 proc... " in r2.stdout
+    assert "process 1/1" in r2.stdout
+
+
 SCN_FLAGS = {"dieoff": ["-a", "10", "-e", "0.3", "-c", "0.4", "-m", "400", "-d", "100", "-s", "21"],
              "loss": ["-a", "10", "-e", "0.3", "-c", "0.4", "-m", "400", "-d", "100", "-s", "13", "-v", "5"]}
 

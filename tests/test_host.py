@@ -84,6 +84,30 @@ def test_log_total_and_writer_bitexact(tmp_path):
     assert (tmp_path / "a.txt").read_bytes() == (tmp_path / "b.txt").read_bytes()
 
 
+@pytest.mark.parametrize("threads", ["1", "3", "16"])
+def test_threaded_normaliser_and_writer_bitexact(tmp_path, monkeypatch, threads):
+    """Grids past 64 Ki cells take the threaded exps and row formatting:
+    Ltot and every byte of the file equal the oracle's sequential forms,
+    including -inf / NaN cells, huge values (a long %.20lf) and odd sizes."""
+    monkeypatch.setenv("OMP_NUM_THREADS", threads)
+    rng = np.random.default_rng(5)
+    s = 263
+    lik = rng.normal(-30, 8, (s, s))
+    lik[0, :7] = -np.inf
+    g, win = mdp.grid(s)
+    lt = mdp.log_total(lik, win)
+    assert lt == oracle.ltot(lik, win)
+    mdp.write_posterior(tmp_path / "a.txt", lik, lt)
+    oracle.write_posterior(tmp_path / "b.txt", lik, lt)
+    assert (tmp_path / "a.txt").read_bytes() == (tmp_path / "b.txt").read_bytes()
+    # the raw branch prints log-likelihoods as they are: NaN, -inf, a 1e300
+    # (a 321-character cell)
+    lik[100, 3], lik[7, 9] = np.nan, 1e300
+    mdp.write_posterior(tmp_path / "r.txt", lik, 0.0, raw=True)
+    ref = "".join("".join(f"{v:.20f}\t" for v in row) + "\n" for row in lik)
+    assert (tmp_path / "r.txt").read_text() == ref
+
+
 def test_writer_all_nan(tmp_path):
     s = 4
     lik = np.full((s, s), -np.inf)
