@@ -18,13 +18,13 @@ def test_ltot_zero_raw_branch(tmp_path):
     g, win = mdp.grid(2, 0.0, 1.0)
     assert win == 1.0
     buf = io.StringIO()
-    ltot = cli.finish(lik, win, tmp_path / "mpi.txt", 2, lambda t, all_ranks=False: buf.write(t))
+    ltot = cli.finish(lik, win, tmp_path / "mpi.txt", True, lambda t, all_ranks=False: buf.write(t))
     assert ltot == 0.0
     assert buf.getvalue().startswith("Total log-likelihood=0.00000\n")
     assert (tmp_path / "mpi.txt").read_text() == "0.00000000000000000000\t" * 2 + "\n" + \
         "0.00000000000000000000\t" * 2 + "\n"
     # single process (MIDASPOM.out has no raw branch): exp(0 - 0) = 1
-    cli.finish(lik + 0.0, win, tmp_path / "one.txt", 1, lambda t, all_ranks=False: None)
+    cli.finish(lik + 0.0, win, tmp_path / "one.txt", False, lambda t, all_ranks=False: None)
     assert (tmp_path / "one.txt").read_text() == ("1.00000000000000000000\t" * 2 + "\n") * 2
 
 
