@@ -65,25 +65,47 @@ def _pmc_traffic(cfg):
 
 
 def host_info():
-    """nproc, the cores this process may use, and the CPU model."""
-    model = "unknown"
+    """The host's CPUs as SURVEY §8(d) asks them stated: the model, logical
+    CPUs and physical cores of the machine, the CPUs this process may run on
+    (affinity) and the CPU time it may use (the cgroup quota: on the GPU
+    pool a one-GPU job gets 16 CPUs' worth of a 2 x 64-core EPYC, whatever
+    its affinity says)."""
+    model, phys = "unknown", set()
     try:
+        cur = {}
         for ln in Path("/proc/cpuinfo").read_text().splitlines():
-            if ln.startswith("model name"):
+            if ln.startswith("model name") and model == "unknown":
                 model = ln.split(":", 1)[1].strip()
-                break
+            elif ln.startswith("physical id"):
+                cur["p"] = ln.split(":", 1)[1].strip()
+            elif ln.startswith("core id"):
+                phys.add((cur.get("p"), ln.split(":", 1)[1].strip()))
     except OSError:
         pass
     try:
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
-    return {"nproc": os.cpu_count() or 1, "usable_cores": usable, "cpu_model": model}
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count() or 1, "logical_cpus": os.cpu_count() or 1,
+            "physical_cores": len(phys) or None, "usable_cores": usable, "cgroup_cpu_quota": quota,
+            "cpu_model": model}
 
 
 def _all_threads():
-    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-                      host_info()["usable_cores"]))
+    """Every CPU this job can use: the affinity set, capped by the cgroup
+    CPU quota (threads past the quota only time-share it)."""
+    h = host_info()
+    n = h["usable_cores"]
+    if h["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(h["cgroup_cpu_quota"])))
+    return max(1, n)
 
 
 def _oracle_leg(om, g_e, g_c, lik_gpu, ltot_gpu, tmax, threads, budget_s, per_pt):
@@ -122,11 +144,20 @@ def cli_walls(cfg_inputs, tmpdir):
     cache = Path(tempfile.mkdtemp(prefix="mdp_jitcache_", dir=tmpdir))
     for name, (inp, s) in cfg_inputs.items():
         for leg in ("cold", "warm"):
-            env = dict(os.environ, MDP_JIT_CACHE=str(cache / name))
+            # cold: an empty code-object cache and no compiler-side cache
+            # (ROCm's comgr keeps its own, which this process has warmed)
+            env = dict(os.environ, MDP_JIT_CACHE=str(cache / name), MIDASPOM_TIMING="1",
+                       **({"AMD_COMGR_CACHE": "0"} if leg == "cold" else {}))
             t0 = time.perf_counter()
             r = subprocess.run([str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", str(s), "-i", str(inp),
-                                "-o", str(Path(tmpdir) / f"{name}.post")], env=env, capture_output=True)
+                                "-o", str(Path(tmpdir) / f"{name}.post")], env=env, capture_output=True, text=True)
             out[f"{name}_cli_{leg}_s"] = time.perf_counter() - t0 if r.returncode == 0 else None
+            # the CLI's own split (MIDASPOM_TIMING): parse, HIP start-up,
+            # engine set-up (hipRTC), grid, Ltot, write
+            for ln in r.stderr.splitlines():
+                if ln.startswith("midaspom timing (s):"):
+                    v = ln.split(":", 1)[1].split()
+                    out[f"{name}_cli_{leg}_split_s"] = {v[i]: float(v[i + 1]) for i in range(0, len(v) - 1, 2)}
     orc = ROOT / "oracle" / "_build" / "orc_main"
     if orc.exists() and "config1" in cfg_inputs:
         inp, s = cfg_inputs["config1"]
@@ -152,14 +183,22 @@ def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, tmpdir, budget_s
     one, _ = _oracle_leg(om, g_e, g_c, lik_gpu, ltot_gpu, tmax, 1, budget_s, per_pt)
     allc, parity = _oracle_leg(om, g_e, g_c, lik_gpu, ltot_gpu, tmax, threads, budget_s, per_pt)
     cfg1 = ROOT / "tests" / "golden" / "occupancies.txt"
+    hi = host_info()
     res = {
         "value": allc["value"], "unit": "grid-point-timestep evals/s", "cores": threads, "kind": "port",
-        "sample": f"{allc['sample']}, {threads} threads, {allc['wall_s']:.1f} s",
+        "sample": f"{allc['sample']}, {threads} threads (all this job may use: affinity {hi['usable_cores']}, "
+                  f"cgroup quota {hi['cgroup_cpu_quota']} CPUs), {allc['wall_s']:.1f} s",
         "one_core": {"value": one["value"], "sample": f"{one['sample']}, 1 thread, {one['wall_s']:.1f} s"},
+        # not measured: what the whole machine's physical cores would give at
+        # the measured one-core rate (an upper estimate for a node-wide CPU run)
+        "whole_host_estimate": {"value": one["value"] * (hi["physical_cores"] or 1),
+                                "basis": f"one-core rate x {hi['physical_cores']} physical cores (extrapolated)"},
         "dgemm": "naive row-major triple loop (oracle/spom_oracle.c); the reference itself needs CBLAS, "
                  "which this image lacks (DESIGN.md §7)",
         **host_info(),
-        "end_to_end": cli_walls({"config1": (cfg1, 50), "config2": (input_path, 512)}, tmpdir),
+        "end_to_end": cli_walls({"config1": (cfg1, 50), "config2": (input_path, 512),
+                                 "config3": (synth.write(Path(tmpdir) / "config3.txt", **synth.CONFIG3), 1024)},
+                                tmpdir),
     }
     return res, parity
 
@@ -261,7 +300,7 @@ def bench_future(args, world, rank, dev):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle
-        threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
+        threads = _all_threads()
         t0 = time.perf_counter()
         oracle.future_counts(row, post, tfut=tfut, nrep=2000, m=400.0, d=100.0, seed=seed, threads=1)
         per = (time.perf_counter() - t0) / 2000

@@ -169,7 +169,7 @@ int mdp_engine_work(const mdp_engine *engine, uint64_t ne, uint64_t nc, double *
  * state multiply-add), the prior sum (2 np_last - 1).  use_pt counts a
  * transition that recurs at every use; use_pt_min is the algorithmic
  * minimum: each distinct transition's dot product once per point (2 nX + 1)
- * plus every use's state update (2) -- the hipRTC kernel caches recurring
+ * plus the state updates, npc (2 npp - 1) per year -- the hipRTC kernel caches recurring
  * transitions and executes between the two.  flop = nc * per-c + ne * nc *
  * per-point, flop_min the same with use_pt_min.  The per-c terms are zero on
  * the generic path (MDP_JIT=0), which has no direct plan. */

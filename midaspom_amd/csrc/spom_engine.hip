@@ -2722,9 +2722,10 @@ int mdp_engine_work_fact(const mdp_engine *eng, uint64_t ne, uint64_t nc, mdp_wo
         const uint32_t nX = (d >> kOffBits) & 31u, nA = d >> 27;
         wmax[nA] = std::max(wmax[nA], (int)nX);
         w->use_pt += 2.0 * nX + 3.0;
-        w->use_pt_min += 2.0;  // the state update
         if (distinct.insert(d).second) w->use_pt_min += 2.0 * nX + 1.0;  // the dot product, once
     }
+    // the state updates v'[l] = sum_k v[k] P[k][l]: npc (2 npp - 1) per year
+    for (uint32_t t = 1; t < eng->tmax; ++t) w->use_pt_min += (double)eng->np[t] * (2.0 * eng->np[t - 1] - 1.0);
     w->weight_pt = 2.0 * eng->maxA;
     for (int a = 0; a <= kMaxDeg; ++a)
         if (wmax[a] >= 0) w->weight_pt += (double)(wmax[a] + 1);

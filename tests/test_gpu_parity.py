@@ -534,11 +534,11 @@ def test_work_fact_per_point_terms_from_the_model(golden, fname):
                 A, B = int(ss[a]), int(ss[b])
                 nX, nA = bin(A & B).count("1"), bin(A).count("1")
                 use += 2 * nX + 3
-                use_min += 2
                 if (A & B, B, nA) not in seen:  # P depends on (A & B, B, |A|) only
                     seen.add((A & B, B, nA))
                     use_min += 2 * nX + 1
                 mmax[nA] = max(mmax.get(nA, -1), nX)
+        use_min += len(ids[t]) * (2 * len(ids[t - 1]) - 1)  # the state updates of year t
     maxA = max(mmax) if mmax else 0
     weight = 2 * maxA + sum(m + 1 for m in mmax.values())
     final = 2 * len(ids[-1]) - 1
