@@ -201,6 +201,11 @@ int mdp_engine_get_info(const mdp_engine *engine, mdp_engine_info *info);
  * most len bytes (NUL-terminated) and returns the full length. */
 int mdp_engine_launched(const mdp_engine *engine, char *buf, size_t len);
 
+/* y[i] = log(x[i]) on the current device with the forward kernels' own FP64
+ * log (a range reduction and an atanh series; the hipRTC kernels use it for
+ * log L), for its accuracy test against the host's libm. */
+int mdp_log_check(const double *x, double *y, size_t n);
+
 /* ------------------------------------------------------------------ */
 /* Scenario likelihoods: in-situ die-off and habitat loss              */
 /* (main_MIDASPOM_dieoff.c / main_MIDASPOM_loss.c)     */

@@ -109,6 +109,7 @@ SIGNATURES = [
     ("mdp_engine_work_fact", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(Work)]),
     ("mdp_engine_get_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(EngineInfo)]),
     ("mdp_engine_launched", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
+    ("mdp_log_check", ctypes.c_int, [c_dbl_p, c_dbl_p, ctypes.c_size_t]),
     ("mdp_engine_diag_report", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
     ("mdp_last_error", ctypes.c_char_p, []),
     ("mdp_abi_version", ctypes.c_int, []),

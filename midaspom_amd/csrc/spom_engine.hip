@@ -2355,6 +2355,8 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             // compile the variant a small grid uses now (the other on demand)
             if (const char *fv = getenv("MDP_FUSED")) eng->fused_mode = atoi(fv) != 0;
             if (const char *cv = getenv("MDP_FUSED_COLS")) plan.fused_cols = std::max(1, std::min(4, atoi(cv)));
+            if (const char *cv = getenv("MDP_JIT_HACK")) plan.hack = atoi(cv);
+            if (const char *cv = getenv("MDP_FAST_LOG")) plan.fast_log = atoi(cv) != 0;
             plan.nj = eng->nj;
             plan.nvar = eng->nvar;
             plan.nitems = eng->nitems;
@@ -2569,6 +2571,28 @@ int mdp_engine_diag_report(mdp_engine *eng, char *buf, size_t len)
             w = snprintf(buf + used, len - used, " ph%d=%.0f", q, nb ? mean[q] / nb : 0.0);
             if (w > 0) used = std::min(len - 1, used + (size_t)w);
         }
+        {   // block start / end spread (wall clock): percentiles, and the latest start per XCD
+            std::vector<double> st0, en;
+            double xmax[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (size_t b = 0; b < d.nst[k]; ++b) {
+                const unsigned long long *st = &h[b * kStampSlots];
+                if (!st[6] || !st[7] || st[7] < st[6] || st[6] < rs0) continue;
+                st0.push_back((st[6] - rs0) * 0.01);
+                en.push_back((st[7] - rs0) * 0.01);
+                xmax[b % 8] = std::max(xmax[b % 8], (st[6] - rs0) * 0.01);
+            }
+            if (!st0.empty()) {
+                std::sort(st0.begin(), st0.end());
+                std::sort(en.begin(), en.end());
+                auto pc = [](const std::vector<double> &v, double f) { return v[(size_t)(f * (v.size() - 1))]; };
+                w = snprintf(buf + used, len - used,
+                             " start_us p10=%.2f p50=%.2f p90=%.2f p99=%.2f end_us p1=%.2f p50=%.2f max=%.2f "
+                             "xcd_last_start_us=%.2f,%.2f,%.2f,%.2f,%.2f,%.2f,%.2f,%.2f",
+                             pc(st0, 0.1), pc(st0, 0.5), pc(st0, 0.9), pc(st0, 0.99), pc(en, 0.01), pc(en, 0.5),
+                             en.back(), xmax[0], xmax[1], xmax[2], xmax[3], xmax[4], xmax[5], xmax[6], xmax[7]);
+                if (w > 0) used = std::min(len - 1, used + (size_t)w);
+            }
+        }
         if (k == 2 && nb && !eng->jit) {  // forward: cycles summed over run ops / general ops (wave 0)
             double cr = 0, cg = 0;
             for (size_t b = 0; b < d.nst[k]; ++b) {
@@ -2634,6 +2658,41 @@ const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
     // direct path: Z rows inside k_qrows (slot 0 idle); fused: one kernel
     if (eng->jit && (k == 0 || (k == 1 && (eng->devs.empty() || eng->devs[0].fused)))) return "";
     return kKernelNames[eng->jit ? 1 : 0][k];
+}
+
+int mdp_log_check(const double *x, double *y, size_t n)
+{
+    if ((n && (!x || !y))) return mdp_set_error(MDP_EINVAL, "null argument");
+    if (!n) return MDP_OK;
+    std::vector<char> code;
+    std::string log;
+    if (mdp_jit_compile(mdp_jit_log_source(), code, log) != 0)
+        return mdp_set_error(MDP_EHIP, "hipRTC compilation of mdp_log failed: %s", log.c_str());
+    hipModule_t mod = nullptr;
+    hipFunction_t fn;
+    double *dx = nullptr, *dy = nullptr;
+    int rc = MDP_OK;
+    auto fail = [&](hipError_t e, const char *what) {
+        rc = mdp_set_error(MDP_EHIP, "%s failed: %s", what, hipGetErrorString(e));
+    };
+    hipError_t e;
+    if ((e = hipModuleLoadData(&mod, code.data())) != hipSuccess) fail(e, "hipModuleLoadData");
+    else if ((e = hipModuleGetFunction(&fn, mod, "mdp_log_apply")) != hipSuccess) fail(e, "hipModuleGetFunction");
+    else if ((e = hipMalloc((void **)&dx, n * sizeof(double))) != hipSuccess) fail(e, "hipMalloc");
+    else if ((e = hipMalloc((void **)&dy, n * sizeof(double))) != hipSuccess) fail(e, "hipMalloc");
+    else if ((e = hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess) fail(e, "hipMemcpy");
+    else {
+        unsigned long long nn = n;
+        void *args[] = {(void *)&dx, (void *)&dy, (void *)&nn};
+        const uint32_t nb = (uint32_t)((n + kBlock - 1) / kBlock);
+        if ((e = hipModuleLaunchKernel(fn, nb, 1, 1, kBlock, 1, 1, 0, nullptr, args, nullptr)) != hipSuccess)
+            fail(e, "hipModuleLaunchKernel");
+        else if ((e = hipMemcpy(y, dy, n * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) fail(e, "hipMemcpy");
+    }
+    (void)hipFree(dx);
+    (void)hipFree(dy);
+    if (mod) (void)hipModuleUnload(mod);
+    return rc;
 }
 
 int mdp_engine_launched(const mdp_engine *eng, char *buf, size_t len)

@@ -33,6 +33,46 @@ namespace {
 const char *kPrelude = R"SRC(
 typedef unsigned int u32;
 #define KBLOCK 256
+// log x = k ln2 + log m, x = 2^k m with m in [sqrt(1/2), sqrt(2)): log m =
+// 2 atanh(s), s = (m - 1) / (m + 1), |s| <= 0.1716, the odd series to s^21
+// (remainder below 2^-62 of the sum).  About 20 FP64 operations and no
+// table, a fraction of the library log's cost; within 2 ulp of it
+// (tests/test_gpu_parity.py::test_engine_log_accuracy).
+__device__ __forceinline__ double mdp_log(double x)
+{
+    if (!(x > 0.0) || x == __builtin_inf()) return x == 0.0 ? -__builtin_inf() : (x > 0.0 ? x : __builtin_nan(""));
+    int k = 0;
+    if (x < 0x1p-1022) {  // subnormal: scale into the normal range
+        x *= 0x1p54;
+        k = -54;
+    }
+    const unsigned long long ix = (unsigned long long)__double_as_longlong(x);
+    k += (int)(ix >> 52) - 1023;
+    double m = __longlong_as_double((long long)((ix & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
+    if (m > 1.4142135623730951) {
+        m *= 0.5;
+        ++k;
+    }
+    const double f = m - 1.0, d = m + 1.0;
+    double r = __builtin_amdgcn_rcp(d);  // 1 / d: one Newton step, then a corrected quotient
+    r = fma(fma(-d, r, 1.0), r, r);
+    double s = f * r;
+    s = fma(fma(-d, s, f), r, s);
+    const double z = s * s;
+    double p = 1.0 / 21.0;
+    p = fma(p, z, 1.0 / 19.0);
+    p = fma(p, z, 1.0 / 17.0);
+    p = fma(p, z, 1.0 / 15.0);
+    p = fma(p, z, 1.0 / 13.0);
+    p = fma(p, z, 1.0 / 11.0);
+    p = fma(p, z, 1.0 / 9.0);
+    p = fma(p, z, 1.0 / 7.0);
+    p = fma(p, z, 1.0 / 5.0);
+    p = fma(p, z, 1.0 / 3.0);
+    const double lm = fma(2.0 * s, z * p, 2.0 * s);  // 2 s (1 + z p)
+    const double kd = (double)k;
+    return fma(kd, 0x1.62e42fefa39efp-1, fma(kd, 0x1.abc9e3b39803fp-56, lm));
+}
 )SRC";
 
 uint64_t fnv1a(const std::string &s)
@@ -133,6 +173,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     o << kPrelude;
     const bool gather = !pl.qidx.empty();
     const size_t ldq_local = gather ? ((pl.qidx.size() + 1) & ~(size_t)1) : pl.ldQ;
+    o << "#define LOGF(x) " << (pl.fast_log ? "mdp_log(x)" : "log(x)") << "\n";
     o << "#define EPL " << EPL << "\n#define LDQ " << ldq_local << "\n#define LDQG "
       << (gather ? pl.ldq_row : pl.ldQ) << "\n#define NQG " << pl.qidx.size() << "\n#define NPMAX " << npmax
       << "\n#define DMAX " << dmax << "\n#define NW " << (nw ? nw : 1) << "\n";
@@ -153,6 +194,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
           << std::max<uint32_t>(1u, pl.qmaxlen) << "\n#define QUN " << std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)
           << "\n#define NSTG "
           << std::max<uint32_t>(1u, (pl.ct_max / 2 + 256u * pl.fused_cols - 1) / (256u * pl.fused_cols)) << "\n";
+    // columns per workgroup (KBLOCK threads each; the fused variant).  Two
+    // columns per reading workgroup (both Q rows staged, the pair's results
+    // stored as one 16-byte store per row through LDS) was measured slower on
+    // configs 2 and 3, so the reading variant takes one.
     const int FC = pl.fused ? (pl.fused_cols > 0 ? pl.fused_cols : 1) : 1;
     o << "#define FC " << FC << "\n#define NT (KBLOCK * FC)\n";
     o << "extern \"C\" __global__ __launch_bounds__(NT) "
@@ -524,13 +569,23 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         o << "    }\n";
     }
     o << "    }}\n" << stamp(3) << "#define NPLAST " << pl.np.back() << "\n";
-    if (pl.last)
+    if (pl.last && (pl.hack == 1 || pl.hack == 2))  // measurement only: the result is never stored
         o << "#pragma unroll\n"
              "    for (int i = 0; i < EPL; ++i) {\n"
              "        double L = 0.0;\n"
              "#pragma unroll\n"
              "        for (int l = 0; l < NPLAST; ++l) L += v[i][l] * prior0;\n"
-             "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
+          << (pl.hack == 1 ? "        if (L == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
+                           : "        const double lg_ = LOGF(L);\n"
+                             "        if (lg_ == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = lg_;\n")
+          << "    }\n";
+    else if (pl.last)
+        o << "#pragma unroll\n"
+             "    for (int i = 0; i < EPL; ++i) {\n"
+             "        double L = 0.0;\n"
+             "#pragma unroll\n"
+             "        for (int l = 0; l < NPLAST; ++l) L += v[i][l] * prior0;\n"
+             "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = LOGF(L);\n"
              "    }\n";
     else  // hand the end vector to the next chunk
         o << "    if (ic < nc) {\n"
@@ -543,6 +598,15 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     pl.flops_pt = flops;
     o << "// EPL_CHOSEN " << EPL << "\n";
     return o.str();
+}
+
+std::string mdp_jit_log_source()
+{
+    return std::string(kPrelude) +
+           "extern \"C\" __global__ void mdp_log_apply(const double *__restrict__ x, double *__restrict__ y, "
+           "unsigned long long n)\n{\n"
+           "    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;\n"
+           "    if (i < n) y[i] = mdp_log(x[i]);\n}\n";
 }
 
 int mdp_jit_compile(const std::string &src, std::vector<char> &code, std::string &log)

@@ -14,6 +14,8 @@ struct MdpJitPlan {
     // three phases for one c value) instead of reading Q rows
     bool fused = false;
     int fused_cols = 2;  // c columns per fused workgroup (KBLOCK threads each)
+    bool fast_log = true;  // mdp_log (prelude) instead of the library log for log L
+    int hack = 0;  // measurement-only builds (MDP_JIT_HACK; results wrong): 1 = no log, no stores; 2 = no stores
     uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
     // items, qstart, qitem, the Z-row series coefficients [nj][8], then
@@ -48,6 +50,10 @@ int mdp_jit_default_epl(const std::vector<uint32_t> &udesc);
 
 // HIP source of `mdp_fwd_jit` for this plan; sets plan.epl when it was 0.
 std::string mdp_jit_forward_source(MdpJitPlan &plan);
+
+// A kernel mdp_log_apply(x, y, n): y[i] = mdp_log(x[i]) with the forward
+// kernels' own log (the prelude), for the accuracy test.
+std::string mdp_jit_log_source();
 
 // Compile (or fetch from the memory / disk cache) a gfx950 code object.
 // Returns 0 on success; on failure `log` holds the compiler output.

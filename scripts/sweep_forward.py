@@ -37,7 +37,7 @@ ap.add_argument("--diag", action="store_true")
 args = ap.parse_args()
 torch.cuda.set_device(0)
 tmp = Path(tempfile.mkdtemp())
-KEYS = ("MDP_JIT", "MDP_EPL", "MDP_JIT_WINDOW", "MDP_FWD", "MDP_DIAG", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED",
+KEYS = ("MDP_JIT", "MDP_EPL", "MDP_QROWS_XCD", "MDP_JIT_EFAST", "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_JIT_WINDOW", "MDP_FWD", "MDP_DIAG", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED",
         "MDP_JIT_SMEM", "MDP_FUSED_COLS", "MDP_JIT_WPE", "MDP_JIT_HACK", "MDP_JIT_STORE")
 for cfgid in [int(x) for x in args.configs.split(",")]:
     gen, s = (synth.CONFIG2, 512) if cfgid == 2 else (synth.CONFIG3, 1024)
@@ -46,7 +46,7 @@ for cfgid in [int(x) for x in args.configs.split(",")]:
     g, _ = mdp.grid(s)
     ref = None
     for var in [v for v in args.variants.split(";") if v]:
-        for k in KEYS:
+        for k in [k for k in os.environ if k.startswith("MDP_")]:  # every engine knob, not only KEYS
             os.environ.pop(k, None)
         env = dict(kv.split("=") for kv in var.split(","))
         if args.diag:
@@ -61,13 +61,14 @@ for cfgid in [int(x) for x in args.configs.split(",")]:
         for _ in range(3):
             eng.run(out.data_ptr(), s, st)
         torch.cuda.synchronize()
-        eng.set_profiling(True)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             eng.run(out.data_ptr(), s, st)
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / args.steps
-        ms = eng.kernel_ms()
+        # kernel durations without per-launch events (bench.py's measure)
+        ms = eng.time_kernels(out.data_ptr(), s, st, reps=args.steps)
+        torch.cuda.synchronize()
         w = eng.work(s, s)
         o = out.cpu().numpy()
         if ref is None:
@@ -84,5 +85,9 @@ for cfgid in [int(x) for x in args.configs.split(",")]:
         if args.diag:
             eng.run(out.data_ptr(), s, st)
             torch.cuda.synchronize()
-            print(eng.diag_report(), flush=True)
+            print("after idle:", eng.diag_report(), flush=True)
+            for _ in range(20):  # steady state: the report shows the last of 20 back-to-back runs
+                eng.run(out.data_ptr(), s, st)
+            torch.cuda.synchronize()
+            print("back to back:", eng.diag_report(), flush=True)
         eng.close()

@@ -41,7 +41,19 @@ void run(int threads, size_t ldsb, const char *tag)
         auto mm = std::minmax_element(h.begin(), h.end());
         if (rep) spread += (*mm.second - *mm.first) * 0.01;  // us
     }
-    printf("%-34s threads=%4d lds=%6zu  start spread %.2f us\n", tag, threads, ldsb, spread / 5);
+    // back to back: 20 launches, no synchronisation between them; the
+    // stamps are the last launch's
+    double spread2 = 0;
+    for (int rep = 0; rep < 5; ++rep) {
+        for (int i = 0; i < 20; ++i)
+            hipLaunchKernelGGL(k_ramp<NREG>, dim3(256), dim3(threads), ldsb, 0, t, sink, 2000);
+        hipDeviceSynchronize();
+        hipMemcpy(h.data(), t, 256 * 8, hipMemcpyDeviceToHost);
+        auto mm = std::minmax_element(h.begin(), h.end());
+        spread2 += (*mm.second - *mm.first) * 0.01;
+    }
+    printf("%-34s threads=%4d lds=%6zu  start spread after idle %.2f us, back to back %.2f us\n", tag, threads,
+           ldsb, spread / 5, spread2 / 5);
     hipFree(t);
     hipFree(sink);
 }
