@@ -1178,6 +1178,7 @@ struct mdp_engine {
     bool qrows_xcd = true;    // k_qrows deals c ranges XCD-aware (MDP_QROWS_XCD=0: blockIdx order)
     double wide_flops_pt = 0; // its FP64 flops per grid point
     int jit_epl = 1;          // its grid points per lane
+    uint32_t jit_kblock = kBlock;  // its threads per column
     double jit_flops_pt = 0;  // its FP64 flops per grid point (counted by the generator)
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
     std::vector<char> jit_code[2];  // forward kernel code objects [fused], compiled on demand
@@ -1598,6 +1599,7 @@ int jit_build(mdp_engine *eng, bool fused)
     plan.fused = fused;
     const std::string src = mdp_jit_forward_source(plan);
     eng->jit_epl = plan.epl;
+    eng->jit_kblock = (uint32_t)plan.kblock;
     eng->jit_flops_pt = plan.flops_pt;
     if (const char *dump = getenv("MDP_JIT_DUMP")) {  // <path>.hip (reading) / <path>.fused.hip
         if (FILE *f = fopen((std::string(dump) + (fused ? ".fused.hip" : ".hip")).c_str(), "w")) {
@@ -1655,6 +1657,7 @@ int jit_build_chunks(mdp_engine *eng)
         }
     eng->chunk_code = std::move(code);
     eng->jit_epl = eng->chunks[0].epl;
+    eng->jit_kblock = (uint32_t)eng->chunks[0].kblock;
     eng->jit_flops_pt = flops;
     return MDP_OK;
 }
@@ -1860,12 +1863,12 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         // one e block per c column and a small per-c problem: the forward
         // kernel computes its column's Q itself (one launch); never for a
         // chunked series or Q rows built in HBM
-        const uint32_t gy = (ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
+        const uint32_t gy = (ne + eng->jit_kblock * eng->jit_epl - 1) / (eng->jit_kblock * eng->jit_epl);
         d.fused = eng->chunks.empty() && !eng->qglobal && fused_lds(eng, d.ct_len) <= kFusedLdsMax &&
                   d.zs_kmax <= eng->jit_plan.kzmax && (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
         if ((rc = jit_load(eng, d, d.fused))) return rc;
         if (!eng->chunks.empty()) {  // the state vectors handed between chunks
-            d.ldv = gy * kBlock * (uint32_t)eng->jit_epl;
+            d.ldv = gy * eng->jit_kblock * (uint32_t)eng->jit_epl;
             uint32_t nb = 1;  // most states at a chunk boundary
             for (size_t i = 1; i < eng->chunks.size(); ++i) nb = std::max(nb, eng->chunks[i].np[0]);
             if ((rc = dev_reserve(&d.vscr, &d.cap_vscr, (size_t)nb * nc * d.ldv))) return rc;
@@ -1955,16 +1958,17 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
                         (void *)&out,  (void *)&ld,     (void *)&one, (void *)&st,   (void *)&cv,
                         (void *)&ctab, (void *)&ctl,    (void *)&kmax, (void *)&vscr, (void *)&ldv,
                         (void *)&qidx};
-        const uint64_t gy = (d.ne + kBlock * eng->jit_epl - 1) / (kBlock * eng->jit_epl);
+        const uint32_t kb = eng->jit_kblock;
+        const uint64_t gy = (d.ne + kb * eng->jit_epl - 1) / (kb * eng->jit_epl);
         const uint32_t fc = d.fused ? (uint32_t)eng->jit_plan.fused_cols : 1u;
         const uint64_t nb = gy * ((d.nc + fc - 1) / fc);  // e blocks x column groups
-        if (nb * kBlock * fc > 0xffffffffull)
+        if (nb * kb * fc > 0xffffffffull)
             return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
         if (!eng->chunks.empty()) {  // a long series: its chunks in order on the stream
             const size_t nch = d.cfn.size();
             for (size_t i = 0; i < nch; ++i) {
                 qidx = d.cqidx[i];
-                HIP_TRY(hipExtModuleLaunchKernel(d.cfn[i], (uint32_t)(nb * kBlock), 1, 1, kBlock, 1, 1, 0, s, args,
+                HIP_TRY(hipExtModuleLaunchKernel(d.cfn[i], (uint32_t)(nb * kb), 1, 1, kb, 1, 1, 0, s, args,
                                                  nullptr, i == 0 ? t_kev.start : nullptr,
                                                  i + 1 == nch ? t_kev.stop : nullptr, 0));
             }
@@ -1973,7 +1977,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
             return MDP_OK;
         }
         const uint32_t dyn = d.fused ? (d.ct_len + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch
-        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kBlock * fc), 1, 1, kBlock * fc, 1, 1, dyn, s, args,
+        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kb * fc), 1, 1, kb * fc, 1, 1, dyn, s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));
         note_launch(eng, "mdp_fwd_jit<%s,maxA%u>", d.fused ? "fused" : "reading", eng->maxA);
         return MDP_OK;
@@ -2357,6 +2361,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (const char *cv = getenv("MDP_FUSED_COLS")) plan.fused_cols = std::max(1, std::min(4, atoi(cv)));
             if (const char *cv = getenv("MDP_JIT_HACK")) plan.hack = atoi(cv);
             if (const char *cv = getenv("MDP_FAST_LOG")) plan.fast_log = atoi(cv) != 0;
+            if (const char *cv = getenv("MDP_JIT_KBLOCK")) plan.kblock = atoi(cv) == 512 ? 512 : 256;
             plan.nj = eng->nj;
             plan.nvar = eng->nvar;
             plan.nitems = eng->nitems;

@@ -32,7 +32,6 @@ namespace {
 
 const char *kPrelude = R"SRC(
 typedef unsigned int u32;
-#define KBLOCK 256
 // log x = k ln2 + log m, x = 2^k m with m in [sqrt(1/2), sqrt(2)): log m =
 // 2 atanh(s), s = (m - 1) / (m + 1), |s| <= 0.1716, the odd series to s^21
 // (remainder below 2^-62 of the sum).  About 20 FP64 operations and no
@@ -174,6 +173,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     const bool gather = !pl.qidx.empty();
     const size_t ldq_local = gather ? ((pl.qidx.size() + 1) & ~(size_t)1) : pl.ldQ;
     o << "#define LOGF(x) " << (pl.fast_log ? "mdp_log(x)" : "log(x)") << "\n";
+    o << "#define KBLOCK " << (pl.kblock > 0 ? pl.kblock : 256) << "\n";  // threads per column
     o << "#define EPL " << EPL << "\n#define LDQ " << ldq_local << "\n#define LDQG "
       << (gather ? pl.ldq_row : pl.ldQ) << "\n#define NQG " << pl.qidx.size() << "\n#define NPMAX " << npmax
       << "\n#define DMAX " << dmax << "\n#define NW " << (nw ? nw : 1) << "\n";
@@ -193,7 +193,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
           << "\n#define QML "
           << std::max<uint32_t>(1u, pl.qmaxlen) << "\n#define QUN " << std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)
           << "\n#define NSTG "
-          << std::max<uint32_t>(1u, (pl.ct_max / 2 + 256u * pl.fused_cols - 1) / (256u * pl.fused_cols)) << "\n";
+          << std::max<uint32_t>(1u, (pl.ct_max / 2 + (uint32_t)pl.kblock * pl.fused_cols - 1) /
+                                       ((uint32_t)pl.kblock * pl.fused_cols)) << "\n";
     // columns per workgroup (KBLOCK threads each; the fused variant).  Two
     // columns per reading workgroup (both Q rows staged, the pair's results
     // stored as one 16-byte store per row through LDS) was measured slower on

@@ -26,6 +26,7 @@ struct MdpJitPlan {
     uint32_t qmaxlen = 0;  // most items of one Q entry
     uint32_t ct_max = 0;  // largest column-table image (doubles), for the register staging
     int epl = 0;                  // grid points per lane (0: 2 unless the weight table is large)
+    int kblock = 256;             // threads per column (256 or 512)
     int window = 8;               // transitions per scheduling region
     bool diag = false;            // record s_memtime phase stamps (MDP_DIAG)
     bool xcd = true;              // XCD-aware block order
