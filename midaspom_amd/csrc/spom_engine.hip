@@ -65,6 +65,8 @@ constexpr size_t kLdsBudget = 120 * 1024;  // dynamic LDS of k_coefs
 constexpr size_t kFwdLds = 48 * 1024;      // max coefficient block staged by k_forward_lds
 constexpr uint32_t kJitMaxUses = 2048;     // uses of one forward kernel; longer series run in chunks
 constexpr uint32_t kJitChunkUses = 1024;   // target uses per chunk (hipRTC time grows faster than the code)
+constexpr uint32_t kVldsMaxStates = 64;     // wide years the specialised kernel takes (states in LDS)
+constexpr uint32_t kVldsMaxUses = 16384;    // ... up to this many uses (hipRTC time)
 constexpr size_t kJitMaxLds = 64 * 1024;   // Pc row + Q block of the direct path
 constexpr size_t kJitChunkQ = kJitMaxLds / sizeof(double) - 2;  // gathered coefficients per chunk
 
@@ -1564,7 +1566,7 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     d.zs_len = (uint32_t)(kmax * nj);
     d.zs_kmax = (uint32_t)kmax;
     // no fused kernel on the wide path, for a chunked series or Q rows built in HBM
-    if (eng->wide || eng->qglobal || !eng->chunks.empty()) return MDP_OK;
+    if (eng->wide || eng->qglobal || !eng->chunks.empty() || eng->jit_plan.vlds) return MDP_OK;
     // the fused kernel's column tables: one contiguous image it copies to LDS
     // (with zpad, all KZ zs rows, zero past kmax: the kernel reads them unmasked)
     const MdpJitPlan &pl = eng->jit_plan;
@@ -1864,7 +1866,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         // kernel computes its column's Q itself (one launch); never for a
         // chunked series or Q rows built in HBM
         const uint32_t gy = (ne + eng->jit_kblock * eng->jit_epl - 1) / (eng->jit_kblock * eng->jit_epl);
-        d.fused = eng->chunks.empty() && !eng->qglobal && fused_lds(eng, d.ct_len) <= kFusedLdsMax &&
+        d.fused = eng->chunks.empty() && !eng->qglobal && !eng->jit_plan.vlds && fused_lds(eng, d.ct_len) <= kFusedLdsMax &&
                   d.zs_kmax <= eng->jit_plan.kzmax && (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
         if ((rc = jit_load(eng, d, d.fused))) return rc;
         if (!eng->chunks.empty()) {  // the state vectors handed between chunks
@@ -2222,7 +2224,7 @@ int collect_times(mdp_engine *eng, DevCtx &d)
 // in the last quarter of a chunk.  With `gather`, each chunk stages only the
 // Q groups its uses read (at most kJitChunkQ doubles, a chunk-local layout of
 // even-aligned groups) instead of the whole Q row.
-int plan_chunks(mdp_engine *eng, uint32_t U, bool gather)
+int plan_chunks(mdp_engine *eng, uint32_t U, bool gather, size_t qlimit)
 {
     const MdpJitPlan &base = eng->jit_plan;
     const std::vector<uint32_t> &np = eng->np;
@@ -2246,7 +2248,7 @@ int plan_chunks(mdp_engine *eng, uint32_t U, bool gather)
                     const uint32_t off = ud[u] & kOffMask;
                     if (!loc.count(off) && fresh.insert(off).second) addq += gsize(ud[u]);
                 }
-            if (cur > 0 && (cur + nu > U || (gather && qloc + addq > kJitChunkQ))) break;
+            if (cur > 0 && (cur + nu > U || (gather && qloc + addq > qlimit))) break;
             cur += nu;
             qloc += addq;
             loc.insert(fresh.begin(), fresh.end());
@@ -2328,7 +2330,18 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
     if (const char *ev = getenv("MDP_DIAG")) eng->diag = atoi(ev) != 0;
     {
         const char *jv = getenv("MDP_JIT");
-        const bool want = !eng->wide && !(jv && !strcmp(jv, "0"));
+        const bool jit_off = jv && !strcmp(jv, "0");
+        // years of 17-64 states: the specialised forward kernel with its
+        // state vectors in LDS (plan.vlds), unless the series is so long that
+        // hipRTC would take minutes; MDP_WIDE=1 forces the wide kernels
+        const char *wv0 = getenv("MDP_WIDE");
+        const bool wide_forced = wv0 && atoi(wv0) != 0;
+        bool vlds = false;
+        if (eng->wide && !wide_forced && !jit_off && eng->npmax <= kVldsMaxStates && eng->nuses <= kVldsMaxUses) {
+            eng->wide = false;
+            vlds = true;
+        }
+        const bool want = !eng->wide && !jit_off;
         bool want_jit = want && build_direct_plan(eng, p) == MDP_OK;
         // k_qrows keeps every table of its c values in LDS; larger problems
         // build their Q rows in HBM (k_zrows + k_witems + k_wq, the same bits)
@@ -2341,10 +2354,20 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
         const char *cv = getenv("MDP_JIT_CHUNK");
         if (cv) chunk_uses = (uint32_t)std::max(1, atoi(cv));
         const char *gv = getenv("MDP_JIT_GATHER");
-        const bool gather = eng->ldQ * sizeof(double) > kJitMaxLds || (gv && atoi(gv) != 0);
+        // coefficients a forward kernel may stage: what the LDS leaves beside
+        // the wide years' state vectors (npmax x 256 lanes) when they are there
+        const size_t qlimit = vlds ? std::min(kJitChunkQ, (kQrowsLdsMax - (size_t)eng->npmax * kBlock * sizeof(double) -
+                                                         2048) / sizeof(double))
+                                   : kJitChunkQ;
+        const bool gather = eng->ldQ > qlimit || (gv && atoi(gv) != 0);
         const bool chunked = eng->nuses > kJitMaxUses || gather || (cv && eng->nuses > chunk_uses);
         if (want_jit && eng->nuses > 0) {
             MdpJitPlan &plan = eng->jit_plan;
+            if (vlds) {  // the wide years' states in LDS: one point per lane, never fused
+                plan.vlds = true;
+                plan.epl = 1;
+                eng->fused_mode = 0;
+            }
             plan.np = eng->np;
             plan.udesc = eng->udesc_d;
             plan.ldQ = eng->ldQ;
@@ -2394,7 +2417,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
                 const size_t kz = std::max<size_t>(8, kmax_max);
                 plan.zpad = fused_lds(eng, ((plan.off_zs + kz * eng->nj) + 127) & ~(size_t)127) <= kFusedLdsMax;
             }
-            if (chunked && (rc = plan_chunks(eng, chunk_uses, gather))) {
+            if (chunked && (rc = plan_chunks(eng, chunk_uses, gather, qlimit))) {
                 delete eng;
                 return rc;
             }
@@ -2422,8 +2445,15 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
                 return r1 ? r1 : MDP_ENODEV;
             }
             if ((chunked ? jit_build_chunks(eng) : jit_build(eng, eng->fused_mode == 1)) == MDP_OK) eng->jit = true;
-            else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the generic kernel:\n%s\n",
-                         eng->jit_log.c_str());
+            else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the %s kernels:\n%s\n",
+                         vlds ? "wide" : "generic", eng->jit_log.c_str());
+        }
+        if (vlds && !eng->jit) {  // no specialised kernel after all: the wide kernels take the problem
+            eng->wide = true;
+            eng->qglobal = false;
+            eng->chunks.clear();
+        } else if (vlds) {
+            eng->variant = (eng->npmax <= 32 ? 32u : 64u) * 100u + eng->deg;
         }
     }
     if (eng->wide) {

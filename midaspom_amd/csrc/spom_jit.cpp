@@ -163,7 +163,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     std::map<std::pair<uint32_t, uint32_t>, int> widx;
     uint32_t dmax = 0;
     const int nw = weight_index(pl.udesc, widx, dmax);
-    const int EPL = pl.epl > 0 ? pl.epl : (nw <= 64 ? 2 : 1);
+    const int EPL = pl.vlds ? 1 : pl.epl > 0 ? pl.epl : (nw <= 64 ? 2 : 1);
     pl.epl = EPL;
     const uint32_t np0 = pl.np[0];
     uint32_t npmax = 1;
@@ -246,16 +246,23 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         for (auto &kv : widx)
             w << "        W[i][" << kv.second << "] = xp[" << (kv.first.first - kv.first.second) << "] * yp["
               << kv.first.second << "];\n";
+        const char *vdst = pl.vlds ? "Vl[k * KBLOCK + tid]" : "v[i][k]";
         if (pl.first)
-            w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < " << np0
+            w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) " << vdst << " = k < " << np0
               << " ? 1.0 : 0.0;\n";
         else  // the previous chunk's end vector (ldv covers every lane's e)
-            w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) v[i][k] = k < " << np0
+            w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) " << vdst << " = k < " << np0
               << " ? vscr[((size_t)k * nc + ic) * ldv + ie[i]] : 0.0;\n";
         w << "    }\n";
         wblock = w.str();
     }
     o << "    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n";
+    if (pl.vlds)  // wide years: the states of lane tid at Vl[k][tid] (EPL 1)
+        o << "    __shared__ double Vl[NPMAX * KBLOCK];\n";
+    // the state k of point i, as an expression
+    auto vref = [&](uint32_t k) {
+        return pl.vlds ? "Vl[" + std::to_string(k) + " * KBLOCK + tid]" : "v[i][" + std::to_string(k) + "]";
+    };
     // stage n (compile-time, even) doubles from src (16-byte aligned) into the
     // LDS array dst, which has a double2 of scratch past n: every load is
     // issued before any store, and the stores are unconditional, so the
@@ -489,8 +496,12 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     // opaque scalar move, so instruction selection can neither merge regions
     // nor hoist every transition's reads to the top (which spills).
     const int window = pl.window > 0 ? pl.window : 8;
-    const char *guard =
-        "    { u32 g_; asm volatile(\"s_mov_b32 %0, %1\" : \"=s\"(g_) : \"s\"(one)); if (g_) {\n";
+    // (with the states in LDS the guard also clobbers memory, so a state
+    // loaded in one region is reloaded in the next rather than held in a
+    // register across the year)
+    const char *guard = pl.vlds
+        ? "    { u32 g_; asm volatile(\"s_mov_b32 %0, %1\" : \"=s\"(g_) : \"s\"(one) : \"memory\"); if (g_) {\n"
+        : "    { u32 g_; asm volatile(\"s_mov_b32 %0, %1\" : \"=s\"(g_) : \"s\"(one)); if (g_) {\n";
     if (pl.slots > 0) o << "    double pc[EPL][" << pl.slots << "];\n";
     o << guard;
     int since = 0;
@@ -544,7 +555,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     size_t u = 0;
     for (size_t t = 1; t < pl.np.size(); ++t) {
         const uint32_t npp = pl.np[t - 1], npc = pl.np[t];
-        if (npp == 1 && npc == 1) {
+        if (npp == 1 && npc == 1 && !pl.vlds) {
             std::string pre;
             const std::string e = use_expr(u++, pre);
             o << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
@@ -557,7 +568,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             for (uint32_t k = 0; k < npp; ++k) {
                 std::string pre;
                 const std::string e = use_expr(u++, pre);
-                o << "    for (int i = 0; i < EPL; ++i) { " << pre << "n[i][" << l << "] = fma(v[i][" << k << "], "
+                o << "    for (int i = 0; i < EPL; ++i) { " << pre << "n[i][" << l << "] = fma(" << vref(k) << ", "
                   << e << ", " << (k ? "n[i][" + std::to_string(l) + "]" : std::string("0.0")) << "); }\n";
                 flops += k ? 2.0 : 1.0;
                 fence();
@@ -566,16 +577,17 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         // the final sum runs over the last year's states), so they are not
         // zeroed: that was ~5 % of the forward's VALU issue on config 3
         o << "    for (int i = 0; i < EPL; ++i) {\n";
-        for (uint32_t l = 0; l < npc; ++l) o << "        v[i][" << l << "] = n[i][" << l << "];\n";
+        for (uint32_t l = 0; l < npc; ++l) o << "        " << vref(l) << " = n[i][" << l << "];\n";
         o << "    }\n";
     }
-    o << "    }}\n" << stamp(3) << "#define NPLAST " << pl.np.back() << "\n";
+    o << "    }}\n" << stamp(3) << "#define NPLAST " << pl.np.back() << "\n"
+      << (pl.vlds ? "#define VREF(l) Vl[(l) * KBLOCK + tid]\n" : "#define VREF(l) v[i][l]\n");
     if (pl.last && (pl.hack == 1 || pl.hack == 2))  // measurement only: the result is never stored
         o << "#pragma unroll\n"
              "    for (int i = 0; i < EPL; ++i) {\n"
              "        double L = 0.0;\n"
              "#pragma unroll\n"
-             "        for (int l = 0; l < NPLAST; ++l) L += v[i][l] * prior0;\n"
+             "        for (int l = 0; l < NPLAST; ++l) L += VREF(l) * prior0;\n"
           << (pl.hack == 1 ? "        if (L == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
                            : "        const double lg_ = LOGF(L);\n"
                              "        if (lg_ == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = lg_;\n")
@@ -585,7 +597,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    for (int i = 0; i < EPL; ++i) {\n"
              "        double L = 0.0;\n"
              "#pragma unroll\n"
-             "        for (int l = 0; l < NPLAST; ++l) L += v[i][l] * prior0;\n"
+             "        for (int l = 0; l < NPLAST; ++l) L += VREF(l) * prior0;\n"
              "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = LOGF(L);\n"
              "    }\n";
     else  // hand the end vector to the next chunk
@@ -593,7 +605,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "#pragma unroll\n"
              "        for (int i = 0; i < EPL; ++i)\n"
              "#pragma unroll\n"
-             "            for (int l = 0; l < NPLAST; ++l) vscr[((size_t)l * nc + ic) * ldv + ie[i]] = v[i][l];\n"
+             "            for (int l = 0; l < NPLAST; ++l) vscr[((size_t)l * nc + ic) * ldv + ie[i]] = VREF(l);\n"
              "    }\n";
     o << stamp(7) << "}\n";
     pl.flops_pt = flops;

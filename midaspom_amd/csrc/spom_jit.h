@@ -27,6 +27,10 @@ struct MdpJitPlan {
     uint32_t ct_max = 0;  // largest column-table image (doubles), for the register staging
     int epl = 0;                  // grid points per lane (0: 2 unless the weight table is large)
     int kblock = 256;             // threads per column (256 or 512)
+    // states of wide years (more than 16 per year): the state vector in LDS
+    // (one column per lane), each year's new states accumulated in
+    // registers; every year takes the general form (EPL 1)
+    bool vlds = false;
     int window = 8;               // transitions per scheduling region
     bool diag = false;            // record s_memtime phase stamps (MDP_DIAG)
     bool xcd = true;              // XCD-aware block order

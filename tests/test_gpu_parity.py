@@ -218,20 +218,38 @@ def _wide_obs(rng, n, T, missing):
     return obs
 
 
+def _wide_engine_run(model, e, c, path, monkeypatch):
+    """Run on the named path and check it ran: "default" (years of 17-64
+    states: the specialised kernel with its states in LDS; more: the wide
+    kernels) or "wide" (MDP_WIDE=1: k_witems + k_wq + k_fwd_wide)."""
+    monkeypatch.delenv("MDP_WIDE", raising=False)
+    if path == "wide":
+        monkeypatch.setenv("MDP_WIDE", "1")
+    with mdp.Engine(model) as eng:
+        got = eng.loglik_grid(e, c)
+        launched, info = eng.launched(), eng.info()
+    if path == "wide" or model.npstates.max() > 64:
+        assert info["variant"] >= 20000 and "k_fwd_wide" in launched, launched
+    else:
+        assert 10000 <= info["variant"] < 20000, info
+        assert any(k.startswith("mdp_fwd_jit<reading") for k in launched), launched
+    return got
+
+
+@pytest.mark.parametrize("path", ["default", "wide"])
 @pytest.mark.parametrize("missing", [{0: 5}, {3: 5}, {2: 6}, {4: 6}, {0: 8}, {3: 8}, {1: 5, 2: 6}, {0: 6, 4: 7}])
-def test_wide_years_vs_oracle(missing):
+def test_wide_years_vs_oracle(missing, path, monkeypatch):
     """Years with more than 4 missing patches (> 16 states), in year 0, in
     later years, in consecutive years: the reference expands 2^k states for
-    any k (main_MIDASPOM.c:225-251) and propagates them (:371-384); the engine
-    routes such problems to the wide path."""
+    any k (main_MIDASPOM.c:225-251) and propagates them (:371-384); up to 64
+    states the specialised kernel keeps them in LDS, beyond that (and forced)
+    the wide kernels run."""
     rng = np.random.default_rng(sum(100 * y + k for y, k in missing.items()))
     obs = _wide_obs(rng, 12, 5, missing)
     model = mdp.Model.from_obs(obs)
     assert model.npstates.max() == 2 ** max(missing.values())
     g, _ = mdp.grid(5)
-    with mdp.Engine(model) as eng:
-        assert eng.info()["variant"] >= 20000  # the wide path
-        got = eng.loglik_grid(g, g)
+    got = _wide_engine_run(model, g, g, path, monkeypatch)
     ref = oracle.OracleModel.from_obs(obs).loglik_grid(g, g, threads=16)
     assert np.isfinite(ref).sum() >= 9
     assert_loglik_close(got, ref)
@@ -252,25 +270,26 @@ def test_random_wide_problems(seed, monkeypatch):
     e, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.2])))
     c, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.5])))
     ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c, threads=16)
-    for cb in (None, "1"):
+    for path, cb in (("default", None), ("wide", None), ("wide", "1")):
         if cb:
             monkeypatch.setenv("MDP_WIDE_CB", cb)
-        with mdp.Engine(model) as eng:
-            assert eng.info()["variant"] >= 20000
-            got = eng.loglik_grid(e, c)
+        got = _wide_engine_run(model, e, c, path, monkeypatch)
         assert_loglik_close(got, ref)
 
 
-def test_wide_survey_series_sampled(tmp_path):
+@pytest.mark.parametrize("path", ["default", "wide"])
+def test_wide_survey_series_sampled(tmp_path, path, monkeypatch):
     """A survey-like series (the Appendix C generator, config-2 shape, 45 %
     of the variable patches unvisited in each year: 2-64 states per year,
-    wide years back to back) on a 128 x 128 grid, sampled against the oracle."""
+    wide years back to back, 7 264 uses: the specialised kernel in chunks
+    with its states in LDS, and the wide kernels) on a 128 x 128 grid,
+    sampled against the oracle."""
     cfg = dict(synth.CONFIG2, pmiss=0.45, seed=5, T=30)
     f = synth.write(tmp_path / "wide.txt", **cfg)
     model = mdp.Model.load(f)
     assert model.npstates.max() == 64
     g, _ = mdp.grid(128)
-    got = gpu_grid(model, g)
+    got = _wide_engine_run(model, g, g, path, monkeypatch)
     rng = np.random.default_rng(3)
     ie, ic = rng.integers(0, 128, 64), rng.integers(0, 128, 64)
     ie[:4], ic[:4] = [0, 127, 0, 127], [0, 0, 127, 127]
