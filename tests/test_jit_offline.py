@@ -58,14 +58,24 @@ def test_forward_kernels_compile_offline(src, tmp_path):
 
 
 @pytest.mark.skipif(gpu_available(), reason="offline planning check runs on CPU-only hosts")
-def test_wide_years_plan_offline():
-    """A year with 6 missing patches (64 states) plans onto the wide path
-    instead of being refused (main_MIDASPOM.c:225-251 takes any count)."""
+@pytest.mark.parametrize("row0,wide,expect", [
+    ([1, -1, -1, -1, -1, -1, -1, 1], "", "forward kernels compiled"),   # 64 states: LDS-state kernel
+    ([1, -1, -1, -1, -1, -1, -1, 1], "1", "wide path planned"),         # forced onto the wide kernels
+    ([-1, -1, -1, -1, -1, -1, -1, 1], "", "wide path planned"),         # 128 states: the wide kernels
+])
+def test_wide_years_plan_offline(row0, wide, expect):
+    """Years with 6-7 missing patches (64 / 128 states) plan instead of
+    being refused (main_MIDASPOM.c:225-251 takes any count): up to 64
+    states on the specialised kernel with its states in LDS, beyond that
+    (or with MDP_WIDE=1) on the wide kernels."""
     code = (f"import sys; sys.path.insert(0, {str(ROOT)!r})\n"
             "import numpy as np, midaspom_amd as mdp\n"
-            "obs = np.array([[1, -1, -1, -1, -1, -1, -1, 1], [1, 1, 0, 1, 0, 1, 1, 0], [1, 0, 0, 1, 1, 1, 0, 1]])\n"
+            f"obs = np.array([{row0!r}, [1, 1, 0, 1, 0, 1, 1, 0], [1, 0, 0, 1, 1, 1, 0, 1]])\n"
             "try:\n    mdp.Engine(mdp.Model.from_obs(obs), devices=[0])\n"
-            "except mdp.MidaspomError as ex:\n    assert 'wide path planned' in str(ex), str(ex); print('ok')\n")
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, MDP_JIT_CHECK="1"),
-                       capture_output=True, text=True, timeout=120)
+            f"except mdp.MidaspomError as ex:\n    assert {expect!r} in str(ex), str(ex); print('ok')\n")
+    env = dict(os.environ, MDP_JIT_CHECK="1")
+    env.pop("MDP_WIDE", None)
+    if wide:
+        env["MDP_WIDE"] = wide
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
