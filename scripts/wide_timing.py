@@ -1,8 +1,11 @@
-"""Time the wide forward path (years with more than 16 states) on survey-like
-series: the Appendix C generator with many unvisited patches per year.
-Prints one JSON line per case: kernel times, step time, and the oracle's
-per-point CPU cost on a small sample (1 thread)."""
+"""Time the paths for years with more than 16 states on survey-like series
+(the Appendix C generator with many unvisited patches per year): the
+specialised kernel with its states in LDS (default up to 64 states) and the
+wide kernels (MDP_WIDE=1).  Prints one JSON line per case and path: kernel
+times, step time, the FP64 rate of the generated / wide work, and the
+oracle's per-point CPU cost on a small sample (1 thread)."""
 import json
+import os
 import sys
 import tempfile
 import time
@@ -18,12 +21,17 @@ import oracle  # noqa: E402
 from midaspom_amd import synth  # noqa: E402
 
 tmp = Path(tempfile.mkdtemp())
-for pmiss, T, s in [(0.45, 30, 512), (0.6, 50, 256)]:
+for pmiss, T, s, path in [(0.45, 30, 512, "default"), (0.45, 30, 512, "wide"), (0.6, 50, 256, "default")]:
+    os.environ.pop("MDP_WIDE", None)
+    if path == "wide":
+        os.environ["MDP_WIDE"] = "1"
     cfg = dict(synth.CONFIG2, pmiss=pmiss, seed=5, T=T)
     f = synth.write(tmp / f"w{pmiss}.txt", **cfg)
     model = mdp.Model.load(f)
     g, _ = mdp.grid(s)
+    t0 = time.perf_counter()
     eng = mdp.Engine(model, devices=[0])
+    t_create = time.perf_counter() - t0
     eng.set_grid(g, g)
     out = torch.empty((s, s), dtype=torch.float64, device="cuda")
     for _ in range(2):
@@ -39,8 +47,13 @@ for pmiss, T, s in [(0.45, 30, 512), (0.6, 50, 256)]:
     t0 = time.perf_counter()
     om.loglik_points(g[1:9], g[1:9], threads=1)
     per_pt = (time.perf_counter() - t0) / 8
-    print(json.dumps({"pmiss": pmiss, "years": T, "grid": s, "npstates_max": int(model.npstates.max()),
-                      "nuses": eng.info()["nuses"], "variant": eng.info()["variant"], "step_ms": step * 1e3,
-                      "kernel_ms": kms, "gpu_points_per_s": s * s / step, "oracle_points_per_s_1core": 1 / per_pt}),
+    w = eng.work(s, s)
+    fwd = [v for k, v in kms.items() if k in ("k_forward", "k_fwd_wide")]
+    print(json.dumps({"pmiss": pmiss, "years": T, "grid": s, "path": path, "npstates_max": int(model.npstates.max()),
+                      "nuses": eng.info()["nuses"], "variant": eng.info()["variant"], "create_s": t_create,
+                      "launched": sorted(eng.launched()), "step_ms": step * 1e3,
+                      "kernel_ms": kms, "fwd_tflops": w["flop_impl"] / (fwd[0] * 1e-3) / 1e12 if fwd else None,
+                      "fwd_frac_fp64": w["flop_impl"] / (fwd[0] * 1e-3) / 78.6e12 if fwd else None,
+                      "gpu_points_per_s": s * s / step, "oracle_points_per_s_1core": 1 / per_pt}),
           flush=True)
     eng.close()
