@@ -65,7 +65,8 @@ constexpr size_t kLdsBudget = 120 * 1024;  // dynamic LDS of k_coefs
 constexpr size_t kFwdLds = 48 * 1024;      // max coefficient block staged by k_forward_lds
 constexpr uint32_t kJitMaxUses = 2048;     // uses of one forward kernel; longer series run in chunks
 constexpr uint32_t kJitChunkUses = 1024;   // target uses per chunk (hipRTC time grows faster than the code)
-constexpr uint32_t kVldsMaxStates = 64;     // wide years the specialised kernel takes (states in LDS)
+constexpr uint32_t kVldsMaxStates = 64;     // wide years the specialised kernel takes (states in LDS;
+                                            // 128-state years compile to MB-sized programs)
 constexpr uint32_t kVldsMaxUses = 16384;    // ... up to this many uses (hipRTC time)
 constexpr size_t kJitMaxLds = 64 * 1024;   // Pc row + Q block of the direct path
 constexpr size_t kJitChunkQ = kJitMaxLds / sizeof(double) - 2;  // gathered coefficients per chunk
@@ -1960,17 +1961,19 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
                         (void *)&out,  (void *)&ld,     (void *)&one, (void *)&st,   (void *)&cv,
                         (void *)&ctab, (void *)&ctl,    (void *)&kmax, (void *)&vscr, (void *)&ldv,
                         (void *)&qidx};
-        const uint32_t kb = eng->jit_kblock;
+        // threads per e block: kb (x 2 with the split state-vector kernel)
+        const uint32_t kb = eng->jit_kblock, spl = eng->jit_plan.vlds && (eng->jit_plan.vsplit == 2 || eng->jit_plan.vsplit == 4)
+                                                      ? (uint32_t)eng->jit_plan.vsplit : 1u;
         const uint64_t gy = (d.ne + kb * eng->jit_epl - 1) / (kb * eng->jit_epl);
         const uint32_t fc = d.fused ? (uint32_t)eng->jit_plan.fused_cols : 1u;
         const uint64_t nb = gy * ((d.nc + fc - 1) / fc);  // e blocks x column groups
-        if (nb * kb * fc > 0xffffffffull)
+        if (nb * kb * fc * spl > 0xffffffffull)
             return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
         if (!eng->chunks.empty()) {  // a long series: its chunks in order on the stream
             const size_t nch = d.cfn.size();
             for (size_t i = 0; i < nch; ++i) {
                 qidx = d.cqidx[i];
-                HIP_TRY(hipExtModuleLaunchKernel(d.cfn[i], (uint32_t)(nb * kb), 1, 1, kb, 1, 1, 0, s, args,
+                HIP_TRY(hipExtModuleLaunchKernel(d.cfn[i], (uint32_t)(nb * kb * spl), 1, 1, kb * spl, 1, 1, 0, s, args,
                                                  nullptr, i == 0 ? t_kev.start : nullptr,
                                                  i + 1 == nch ? t_kev.stop : nullptr, 0));
             }
@@ -1979,7 +1982,8 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
             return MDP_OK;
         }
         const uint32_t dyn = d.fused ? (d.ct_len + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch
-        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kb * fc), 1, 1, kb * fc, 1, 1, dyn, s, args,
+        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kb * fc * spl), 1, 1, kb * fc * spl, 1, 1, dyn,
+                                         s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));
         note_launch(eng, "mdp_fwd_jit<%s,maxA%u>", d.fused ? "fused" : "reading", eng->maxA);
         return MDP_OK;
@@ -2337,7 +2341,10 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
         const char *wv0 = getenv("MDP_WIDE");
         const bool wide_forced = wv0 && atoi(wv0) != 0;
         bool vlds = false;
-        if (eng->wide && !wide_forced && !jit_off && eng->npmax <= kVldsMaxStates && eng->nuses <= kVldsMaxUses) {
+        uint32_t vlds_max_uses = kVldsMaxUses;
+        if (const char *mv = getenv("MDP_VLDS_MAXUSES")) vlds_max_uses = (uint32_t)std::max(0, atoi(mv));
+        const uint32_t vkb = kBlock;  // points per workgroup (their states: npmax x vkb doubles of LDS)
+        if (eng->wide && !wide_forced && !jit_off && eng->npmax <= kVldsMaxStates && eng->nuses <= vlds_max_uses) {
             eng->wide = false;
             vlds = true;
         }
@@ -2356,7 +2363,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
         const char *gv = getenv("MDP_JIT_GATHER");
         // coefficients a forward kernel may stage: what the LDS leaves beside
         // the wide years' state vectors (npmax x 256 lanes) when they are there
-        const size_t qlimit = vlds ? std::min(kJitChunkQ, (kQrowsLdsMax - (size_t)eng->npmax * kBlock * sizeof(double) -
+        const size_t qlimit = vlds ? std::min(kJitChunkQ, (kQrowsLdsMax - (size_t)eng->npmax * vkb * sizeof(double) -
                                                          2048) / sizeof(double))
                                    : kJitChunkQ;
         const bool gather = eng->ldQ > qlimit || (gv && atoi(gv) != 0);
@@ -2366,7 +2373,10 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (vlds) {  // the wide years' states in LDS: one point per lane, never fused
                 plan.vlds = true;
                 plan.epl = 1;
+                plan.kblock = (int)vkb;
+                plan.window = 16;
                 eng->fused_mode = 0;
+                if (const char *sv = getenv("MDP_VSPLIT")) plan.vsplit = atoi(sv) == 1 ? 1 : atoi(sv) == 2 ? 2 : 4;
             }
             plan.np = eng->np;
             plan.udesc = eng->udesc_d;
@@ -2384,7 +2394,8 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (const char *cv = getenv("MDP_FUSED_COLS")) plan.fused_cols = std::max(1, std::min(4, atoi(cv)));
             if (const char *cv = getenv("MDP_JIT_HACK")) plan.hack = atoi(cv);
             if (const char *cv = getenv("MDP_FAST_LOG")) plan.fast_log = atoi(cv) != 0;
-            if (const char *cv = getenv("MDP_JIT_KBLOCK")) plan.kblock = atoi(cv) == 512 ? 512 : 256;
+            if (const char *cv = getenv("MDP_JIT_SQ")) plan.sq = atoi(cv) != 0;
+            if (const char *cv = getenv("MDP_JIT_KBLOCK"); cv && !vlds) plan.kblock = atoi(cv) == 512 ? 512 : 256;
             plan.nj = eng->nj;
             plan.nvar = eng->nvar;
             plan.nitems = eng->nitems;
@@ -2453,7 +2464,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             eng->qglobal = false;
             eng->chunks.clear();
         } else if (vlds) {
-            eng->variant = (eng->npmax <= 32 ? 32u : 64u) * 100u + eng->deg;
+            eng->variant = (eng->npmax <= 32 ? 32u : eng->npmax <= 64 ? 64u : 128u) * 100u + eng->deg;
         }
     }
     if (eng->wide) {

@@ -171,6 +171,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     std::ostringstream o;
     o << kPrelude;
     const bool gather = !pl.qidx.empty();
+    const bool sq = pl.sq && !pl.fused;
     const size_t ldq_local = gather ? ((pl.qidx.size() + 1) & ~(size_t)1) : pl.ldQ;
     o << "#define LOGF(x) " << (pl.fast_log ? "mdp_log(x)" : "log(x)") << "\n";
     o << "#define KBLOCK " << (pl.kblock > 0 ? pl.kblock : 256) << "\n";  // threads per column
@@ -200,7 +201,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     // stored as one 16-byte store per row through LDS) was measured slower on
     // configs 2 and 3, so the reading variant takes one.
     const int FC = pl.fused ? (pl.fused_cols > 0 ? pl.fused_cols : 1) : 1;
-    o << "#define FC " << FC << "\n#define NT (KBLOCK * FC)\n";
+    // target split (vlds): SPL waves per 64 points, wave group `half`
+    // accumulating the new states l with l % SPL == half
+    const int SPL = pl.vlds && (pl.vsplit == 2 || pl.vsplit == 4) ? pl.vsplit : 1;
+    o << "#define FC " << FC << "\n#define SPL " << SPL << "\n#define NT (KBLOCK * FC * SPL)\n";
     o << "extern \"C\" __global__ __launch_bounds__(NT) "
       << (pl.wpe > 0 ? "__attribute__((amdgpu_waves_per_eu(" + std::to_string(pl.wpe) + "))) " : std::string())
       << "void mdp_fwd_jit(\n"
@@ -220,9 +224,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    const u32 half = threadIdx.x / KBLOCK, tid = threadIdx.x % KBLOCK;\n"
          // (column group, e block): FC columns x KBLOCK*EPL e values per workgroup
       << (pl.efast ? "    const u32 gy = (ne + KBLOCK * EPL - 1) / (KBLOCK * EPL), ic0 = lb / gy * FC, by = lb % gy;\n"
-                   : "    const u32 ncb = (nc + FC - 1) / FC, ic0 = lb % ncb * FC, by = lb / ncb;\n") <<
-         "    const u32 ic = ic0 + half;\n"
-         "    const double *Qh = Ql + half * LDQ;\n"
+                   : "    const u32 ncb = (nc + FC - 1) / FC, ic0 = lb % ncb * FC, by = lb / ncb;\n")
+      << (SPL > 1 || FC == 1 ? "    const u32 ic = ic0;\n" : "    const u32 ic = ic0 + half;\n")
+      << (sq ? "    const double *Qh = Qrow + (size_t)(ic < nc ? ic : 0) * LDQG;\n"
+             : SPL > 1 ? "    const double *Qh = Ql;\n" : "    const double *Qh = Ql + half * LDQ;\n") <<
          // this lane's e values: issued first, their latency hides under the prologue
          "    u32 ie[EPL];\n    double ev[EPL];\n"
          "#pragma unroll\n"
@@ -247,16 +252,17 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             w << "        W[i][" << kv.second << "] = xp[" << (kv.first.first - kv.first.second) << "] * yp["
               << kv.first.second << "];\n";
         const char *vdst = pl.vlds ? "Vl[k * KBLOCK + tid]" : "v[i][k]";
+        // (split: the state k set by wave group k % SPL)
+        const char *kloop = SPL > 1 ? "#pragma unroll\n        for (int k = half; k < NPMAX; k += SPL) "
+                                    : "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) ";
         if (pl.first)
-            w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) " << vdst << " = k < " << np0
-              << " ? 1.0 : 0.0;\n";
+            w << kloop << vdst << " = k < " << np0 << " ? 1.0 : 0.0;\n";
         else  // the previous chunk's end vector (ldv covers every lane's e)
-            w << "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) " << vdst << " = k < " << np0
-              << " ? vscr[((size_t)k * nc + ic) * ldv + ie[i]] : 0.0;\n";
+            w << kloop << vdst << " = k < " << np0 << " ? vscr[((size_t)k * nc + ic) * ldv + ie[i]] : 0.0;\n";
         w << "    }\n";
         wblock = w.str();
     }
-    o << "    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][NPMAX];\n";
+    o << "    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][(NPMAX + SPL - 1) / SPL];\n";
     if (pl.vlds)  // wide years: the states of lane tid at Vl[k][tid] (EPL 1)
         o << "    __shared__ double Vl[NPMAX * KBLOCK];\n";
     // the state k of point i, as an expression
@@ -286,7 +292,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        }\n"
              "    }\n";
     };
-    if (!pl.fused && !gather) {
+    if (sq) {
+        // (no staging: the coefficients are read where they are used)
+    } else if (!pl.fused && !gather) {
         stage("Ql", "Qrow + (size_t)ic * LDQ", "LDQ");  // this column's Q row (k_qrows)
         o << stamp(1);
     } else if (!pl.fused) {
@@ -483,12 +491,15 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     o << "    __syncthreads();\n"
       << stamp(2);
     // P = sum_m Q[off+m] W[|A|][m] as an expression for point i
+    // (scalar Q with gathered chunks: the chunk-local offset mapped back to
+    // the Q row's own)
+    auto qoff = [&](uint32_t i) { return std::to_string(sq && gather ? pl.qidx[i] : i); };
     auto pexpr = [&](uint32_t d) {
         const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u, nA = d >> 27;
-        std::string e = "Qh[" + std::to_string(off) + "] * W[i][" +
+        std::string e = "Qh[" + qoff(off) + "] * W[i][" +
                         std::to_string(widx[std::make_pair(nA, 0u)]) + "]";
         for (uint32_t m = 1; m <= nX; ++m)
-            e = "fma(Qh[" + std::to_string(off + m) + "], W[i][" +
+            e = "fma(Qh[" + qoff(off + m) + "], W[i][" +
                 std::to_string(widx[std::make_pair(nA, m)]) + "], " + e + ")";
         return e;
     };
@@ -502,7 +513,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     const char *guard = pl.vlds
         ? "    { u32 g_; asm volatile(\"s_mov_b32 %0, %1\" : \"=s\"(g_) : \"s\"(one) : \"memory\"); if (g_) {\n"
         : "    { u32 g_; asm volatile(\"s_mov_b32 %0, %1\" : \"=s\"(g_) : \"s\"(one)); if (g_) {\n";
-    if (pl.slots > 0) o << "    double pc[EPL][" << pl.slots << "];\n";
+    const int nslot = pl.slots > 0 ? pl.slots : 0;
+    if (nslot > 0) o << "    double pc[EPL][" << nslot << "];\n";
     o << guard;
     int since = 0;
     auto fence = [&]() {
@@ -511,44 +523,70 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             since = 0;
         }
     };
-    // Transition cache: a use whose pair (same descriptor = same P) recurs
-    // within kHorizon uses keeps its P in one of pl.slots registers; later
-    // uses read it.  Slots are evicted farthest-next-use first.  The P values
-    // are computed exactly as inline, so results do not change.
+    // The order in which each wave group emits the uses: the register
+    // kernel in use order (per new state l, ascending k); with the states in
+    // LDS, per year source-major (for k: for the group's l), so a region
+    // reads each state once and its accumulations are independent chains.
+    // Each n[l] still sums ascending k, so the order changes no bits.
     const size_t nu = pl.udesc.size();
-    const int nslot = pl.slots > 0 ? pl.slots : 0;
-    const size_t kHorizon = 64;
-    std::vector<size_t> next_use(nu, SIZE_MAX);
+    std::vector<std::vector<size_t>> seq(SPL);
     {
+        size_t ub = 0;
+        for (size_t t = 1; t < pl.np.size(); ++t) {
+            const uint32_t npp = pl.np[t - 1], npc = pl.np[t];
+            if (!pl.vlds)
+                for (size_t j = 0; j < (size_t)npp * npc; ++j) seq[0].push_back(ub + j);
+            else
+                for (int h = 0; h < SPL; ++h)
+                    for (uint32_t k = 0; k < npp; ++k)
+                        for (uint32_t l = h; l < npc; l += SPL) seq[h].push_back(ub + (size_t)l * npp + k);
+            ub += (size_t)npp * npc;
+        }
+    }
+    // Transition cache: a use whose pair (same descriptor = same P) recurs
+    // within kHorizon of its group's uses keeps its P in one of pl.slots
+    // registers; later uses read it.  Slots are evicted farthest-next-use
+    // first.  The P values are computed exactly as inline, so results do not
+    // change.  Positions count within the use's wave group.
+    const size_t kHorizon = 64;
+    std::vector<int> grp(nu, 0);
+    std::vector<size_t> pos(nu, 0), next_pos(nu, SIZE_MAX);
+    for (int h = 0; h < SPL; ++h) {
         std::map<uint32_t, size_t> last;
-        for (size_t i = nu; i-- > 0;) {
-            auto it = last.find(pl.udesc[i]);
-            if (it != last.end()) next_use[i] = it->second;
-            last[pl.udesc[i]] = i;
+        for (size_t p = seq[h].size(); p-- > 0;) {
+            const size_t u = seq[h][p];
+            grp[u] = h;
+            pos[u] = p;
+            auto it = last.find(pl.udesc[u]);
+            if (it != last.end()) next_pos[u] = it->second;
+            last[pl.udesc[u]] = p;
         }
     }
     // flops per point: weight table, transitions (below), prior sum
     double flops = 2.0 * dmax + (double)nw + (pl.last ? 2.0 * npmax : 0.0);
-    std::vector<uint32_t> slot_key(nslot, 0);
-    std::vector<size_t> slot_next(nslot, SIZE_MAX);  // SIZE_MAX: free / dead
+    std::vector<std::vector<uint32_t>> slot_key(SPL, std::vector<uint32_t>(nslot, 0));
+    std::vector<std::vector<size_t>> slot_next(SPL, std::vector<size_t>(nslot, SIZE_MAX));  // SIZE_MAX: free / dead
     // returns the expression for use u, emitting "pc[i][s] = P;" first when
     // the use fills a slot (inside the caller's per-point loop)
     auto use_expr = [&](size_t u, std::string &pre) -> std::string {
         const uint32_t d = pl.udesc[u];
+        const size_t p = pos[u], np_ = next_pos[u];
+        std::vector<uint32_t> &skey = slot_key[grp[u]];
+        std::vector<size_t> &snext = slot_next[grp[u]];
         for (int sl = 0; sl < nslot; ++sl)
-            if (slot_next[sl] == u && slot_key[sl] == d) {
-                slot_next[sl] = next_use[u];
+            if (snext[sl] == p && skey[sl] == d) {
+                snext[sl] = np_;
                 return "pc[i][" + std::to_string(sl) + "]";
             }
         flops += 2.0 * ((d >> 22) & 31u) + 1.0;  // nX FMAs + 1 MUL
         const std::string e = pexpr(d);
-        if (nslot == 0 || next_use[u] == SIZE_MAX || next_use[u] - u > kHorizon) return "(" + e + ")";
+        if (nslot == 0 || np_ == SIZE_MAX || np_ - p > kHorizon) return "(" + e + ")";
         int best = 0;
         for (int sl = 1; sl < nslot; ++sl)
-            if (slot_next[sl] > slot_next[best]) best = sl;
-        if (slot_next[best] != SIZE_MAX && slot_next[best] <= next_use[u]) return "(" + e + ")";
-        slot_key[best] = d;
-        slot_next[best] = next_use[u];
+            if (snext[sl] > snext[best]) best = sl;
+        if (snext[best] != SIZE_MAX && snext[best] <= np_) return "(" + e + ")";
+        skey[best] = d;
+        snext[best] = np_;
         pre = "pc[i][" + std::to_string(best) + "] = " + e + "; ";
         return "pc[i][" + std::to_string(best) + "]";
     };
@@ -561,6 +599,52 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             o << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
             flops += 1.0;
             fence();
+            continue;
+        }
+        if (pl.vlds) {
+            // states in LDS: wave group h accumulates the new states l = h,
+            // h + SPL, ... (a wave-uniform branch when split), source-major;
+            // with the split a barrier either side of the write-back (each
+            // lane otherwise touches only its own column of Vl)
+            const size_t ubase = u;
+            const bool split = SPL > 1;
+            if (split) o << "    }}\n";
+            for (int h = 0; h < SPL; ++h) {
+                if (split) {
+                    o << (h == 0 ? std::string("    if (half == 0) {\n")
+                          : h + 1 < SPL ? "    } else if (half == " + std::to_string(h) + ") {\n"
+                                        : std::string("    } else {\n"))
+                      << guard;
+                    since = 0;
+                }
+                for (uint32_t k = 0; k < npp; ++k)
+                    for (uint32_t l = h; l < npc; l += SPL) {
+                        std::string pre;
+                        const std::string e = use_expr(ubase + (size_t)l * npp + k, pre);
+                        const std::string acc = "n[i][" + std::to_string(l / SPL) + "]";
+                        o << "    for (int i = 0; i < EPL; ++i) { " << pre << acc << " = fma(" << vref(k) << ", " << e
+                          << ", " << (k ? acc : std::string("0.0")) << "); }\n";
+                        flops += k ? 2.0 : 1.0;
+                        fence();
+                    }
+                if (split) o << "    }}\n";
+            }
+            if (split) o << "    }\n    __syncthreads();\n";
+            o << "    for (int i = 0; i < EPL; ++i) {\n";
+            for (int h = 0; h < SPL; ++h) {
+                if (split)
+                    o << (h == 0 ? std::string("        if (half == 0) {\n")
+                          : h + 1 < SPL ? "        } else if (half == " + std::to_string(h) + ") {\n"
+                                        : std::string("        } else {\n"));
+                for (uint32_t l = h; l < npc; l += SPL)
+                    o << "            " << vref(l) << " = n[i][" << l / SPL << "];\n";
+            }
+            o << (split ? "        }\n    }\n    __syncthreads();\n" : "    }\n");
+            if (split) {
+                o << guard;
+                since = 0;
+            }
+            u = ubase + (size_t)npp * npc;
             continue;
         }
         // general year: n[.][l] = sum_k v[.][k] P[k][l] in ascending k
@@ -593,19 +677,22 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                              "        if (lg_ == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = lg_;\n")
           << "    }\n";
     else if (pl.last)
-        o << "#pragma unroll\n"
+        o << "    if (SPL == 1 || half == 0) {\n"
+             "#pragma unroll\n"
              "    for (int i = 0; i < EPL; ++i) {\n"
              "        double L = 0.0;\n"
              "#pragma unroll\n"
              "        for (int l = 0; l < NPLAST; ++l) L += VREF(l) * prior0;\n"
              "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = LOGF(L);\n"
+             "    }\n"
              "    }\n";
     else  // hand the end vector to the next chunk
         o << "    if (ic < nc) {\n"
              "#pragma unroll\n"
              "        for (int i = 0; i < EPL; ++i)\n"
              "#pragma unroll\n"
-             "            for (int l = 0; l < NPLAST; ++l) vscr[((size_t)l * nc + ic) * ldv + ie[i]] = VREF(l);\n"
+             "            for (int l = 0; l < NPLAST; ++l)\n"
+             "                if (SPL == 1 || l % SPL == (int)half) vscr[((size_t)l * nc + ic) * ldv + ie[i]] = VREF(l);\n"
              "    }\n";
     o << stamp(7) << "}\n";
     pl.flops_pt = flops;

@@ -31,10 +31,20 @@ struct MdpJitPlan {
     // (one column per lane), each year's new states accumulated in
     // registers; every year takes the general form (EPL 1)
     bool vlds = false;
+    // with vlds: waves per 64 points (1, 2 or 4); with S > 1 the workgroup
+    // holds S waves for each 64 points, wave group h accumulating the new
+    // states l = h mod S of a year (1/S of the accumulators each, so more
+    // waves per SIMD fit beside the LDS state vectors), a barrier either
+    // side of the write-back
+    int vsplit = 4;
     int window = 8;               // transitions per scheduling region
     bool diag = false;            // record s_memtime phase stamps (MDP_DIAG)
     bool xcd = true;              // XCD-aware block order
     bool efast = true;            // e blocks of one column group dispatched back to back (same XCD)
+    // reading variant: the transitions' Q coefficients read straight from the
+    // column's Q row in global memory (wave-uniform addresses: scalar loads
+    // into SGPRs, FMA operands) instead of staged in LDS (MDP_JIT_SQ)
+    bool sq = false;
     int slots = 8;                // registers caching transitions that recur (0: none)
     int wpe = 0;                  // minimum waves per SIMD asked of the compiler (0: its default)
     double flops_pt = 0;          // out: FP64 flops per grid point of the generated code

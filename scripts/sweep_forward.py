@@ -1,4 +1,5 @@
-"""Time the engine's kernels under environment variants on configs 2 and 3.
+"""Time the engine's kernels under environment variants on configs 2, 3 and 6
+(LONG200).
 
 Usage (GPU box):
   python scripts/sweep_forward.py [--steps K] [--configs 2,3] [--diag]
@@ -40,7 +41,7 @@ tmp = Path(tempfile.mkdtemp())
 KEYS = ("MDP_JIT", "MDP_EPL", "MDP_QROWS_XCD", "MDP_JIT_EFAST", "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_JIT_WINDOW", "MDP_FWD", "MDP_DIAG", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED",
         "MDP_JIT_SMEM", "MDP_FUSED_COLS", "MDP_JIT_WPE", "MDP_JIT_HACK", "MDP_JIT_STORE")
 for cfgid in [int(x) for x in args.configs.split(",")]:
-    gen, s = (synth.CONFIG2, 512) if cfgid == 2 else (synth.CONFIG3, 1024)
+    gen, s = {2: (synth.CONFIG2, 512), 3: (synth.CONFIG3, 1024), 6: (synth.LONG200, 512)}[cfgid]
     f = synth.write(tmp / f"c{cfgid}.txt", **gen)
     model = mdp.Model.load(f)
     g, _ = mdp.grid(s)

@@ -1,6 +1,7 @@
 """Time the paths for years with more than 16 states on survey-like series
 (the Appendix C generator with many unvisited patches per year): the
-specialised kernel with its states in LDS (default up to 64 states) and the
+specialised kernel with its states in LDS (default up to 64 states; two waves per
+64 points splitting each year's new states, or one with MDP_VSPLIT=1) and the
 wide kernels (MDP_WIDE=1).  Prints one JSON line per case and path: kernel
 times, step time, the FP64 rate of the generated / wide work, and the
 oracle's per-point CPU cost on a small sample (1 thread)."""
@@ -21,10 +22,20 @@ import oracle  # noqa: E402
 from midaspom_amd import synth  # noqa: E402
 
 tmp = Path(tempfile.mkdtemp())
-for pmiss, T, s, path in [(0.45, 30, 512, "default"), (0.45, 30, 512, "wide"), (0.6, 50, 256, "default")]:
-    os.environ.pop("MDP_WIDE", None)
-    if path == "wide":
-        os.environ["MDP_WIDE"] = "1"
+PATHS = {  # path name -> engine knobs
+    "default": {}, "nosplit": {"MDP_VSPLIT": "1"}, "split2": {"MDP_VSPLIT": "2"}, "split4": {"MDP_VSPLIT": "4"},
+    "sq": {"MDP_JIT_SQ": "1"}, "split2_sq": {"MDP_VSPLIT": "2", "MDP_JIT_SQ": "1"},
+    "split4_sq": {"MDP_VSPLIT": "4", "MDP_JIT_SQ": "1"}, "wide": {"MDP_WIDE": "1"},
+}
+CASES = [(0.45, 30, 512, p) for p in os.environ.get("WIDE_PATHS", "default,nosplit,sq,wide").split(",")]
+CASES.append((0.6, 50, 256, "default"))
+for pmiss, T, s, path in CASES:
+    for k in [k for k in os.environ if k.startswith("MDP_")]:
+        os.environ.pop(k, None)
+    # "name" or "name:KNOB=V:KNOB=V" (extra engine knobs on top of the path's)
+    name, *extra = path.split(":")
+    os.environ.update(PATHS[name])
+    os.environ.update(dict(kv.split("=") for kv in extra))
     cfg = dict(synth.CONFIG2, pmiss=pmiss, seed=5, T=T)
     f = synth.write(tmp / f"w{pmiss}.txt", **cfg)
     model = mdp.Model.load(f)
@@ -48,12 +59,15 @@ for pmiss, T, s, path in [(0.45, 30, 512, "default"), (0.45, 30, 512, "wide"), (
     om.loglik_points(g[1:9], g[1:9], threads=1)
     per_pt = (time.perf_counter() - t0) / 8
     w = eng.work(s, s)
+    fa = eng.work_fact(s, s)  # the algorithmic minimum (each distinct transition once per point)
     fwd = [v for k, v in kms.items() if k in ("k_forward", "k_fwd_wide")]
     print(json.dumps({"pmiss": pmiss, "years": T, "grid": s, "path": path, "npstates_max": int(model.npstates.max()),
                       "nuses": eng.info()["nuses"], "variant": eng.info()["variant"], "create_s": t_create,
                       "launched": sorted(eng.launched()), "step_ms": step * 1e3,
                       "kernel_ms": kms, "fwd_tflops": w["flop_impl"] / (fwd[0] * 1e-3) / 1e12 if fwd else None,
                       "fwd_frac_fp64": w["flop_impl"] / (fwd[0] * 1e-3) / 78.6e12 if fwd else None,
+                      "fwd_frac_min": s * s * (fa["weight_pt"] + fa["use_pt_min"] + fa["final_pt"]) / (fwd[0] * 1e-3)
+                      / 78.6e12 if fwd else None,
                       "gpu_points_per_s": s * s / step, "oracle_points_per_s_1core": 1 / per_pt}),
           flush=True)
     eng.close()
