@@ -455,6 +455,8 @@ def main():
     ap.add_argument("--grid4", type=int, default=256, help="config 4 grid points per axis")
     ap.add_argument("--replicates", type=int, default=1_000_000, help="config 5 ensemble size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layout", default="ce", choices=["ce", "ec"],
+                    help="device layout of log L: ce = [c][e] (coalesced stores, default), ec = [e][c] rows")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     args = ap.parse_args()
 
@@ -495,6 +497,10 @@ def main():
 
     eng = mdp.Engine(model, devices=[dev.index])
     eng.set_grid(g_e, g_c)
+    # the slab's log L in HBM: [c][e] by default (each workgroup's e values of
+    # one column contiguous, so its stores coalesce; mdp_engine_set_layout),
+    # or the reference's [e][c] rows; the slab is s x s either way
+    eng.set_layout(args.layout)
     out = torch.empty((s, s), dtype=torch.float64, device=dev)
     gathered = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -579,7 +585,8 @@ def main():
         "data": "synthetic (SURVEY.md Appendix C generator, md5-checked input)",
         "config": {"workload": cfg["name"], "patches": model.n, "years": tmax, "grid": [world * s, s],
                    "per_rank_grid": [s, s], "nvar": model.nvar, "nstates": model.nstates,
-                   "nextid": model.nextid, "parallelism": f"e-row slabs x{world}" + (", RCCL gather" if world > 1 else "")},
+                   "nextid": model.nextid, "parallelism": f"e-row slabs x{world}" + (", RCCL gather" if world > 1 else ""),
+                   "layout": "[c][e] (mdp_engine_set_layout CE)" if args.layout == "ce" else "[e][c]"},
         # the reference's job shape: ONE pass over the grid plus the single
         # gather of the slabs (main_MIDASPOM_MPI.c:361-368, 482-506), median of 3
         "job": {"ms": job_ms, "value": world * s * s * (tmax - 1) / (job_ms * 1e-3),
@@ -622,6 +629,8 @@ def main():
         eng.run(lik.data_ptr(), s, stream)
         torch.cuda.synchronize(dev)
         lik_h = lik.cpu().numpy()
+        if args.layout == "ce":  # [c][e] -> the reference's lik[e][c]
+            lik_h = np.ascontiguousarray(lik_h.T)
         ltot = mdp.log_total(lik_h, win)
         cpu, parity = cpu_baseline(inp, g_e, g_c, lik_h, ltot, tmax, tmpdir)
         result["cpu_baseline"] = cpu

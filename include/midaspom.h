@@ -36,7 +36,7 @@ extern "C" {
 #define MDP_ENODEV (-5)       /* no usable GPU                             */
 #define MDP_EUNSUPPORTED (-6) /* problem outside the engine's limits       */
 
-#define MDP_ABI_VERSION 5
+#define MDP_ABI_VERSION 6
 
 /* ------------------------------------------------------------------ */
 /* Host model: parse + state enumeration (the reference's L2 layer)    */
@@ -121,7 +121,15 @@ int mdp_loglik_grid(mdp_engine *engine, const double *e, uint32_t ne, const doub
 /* Device-resident variant for single-device engines (one process per GPU):
  * upload the grid once, then compute into caller-owned device memory
  * d_out[ie*ld_out + ic] on `stream` (hipStream_t; NULL = HIP's null stream).
- * mdp_engine_run is asynchronous w.r.t. the host. */
+ * mdp_engine_run is asynchronous w.r.t. the host.
+ * mdp_engine_set_layout (ABI 6) selects the layout mdp_engine_run writes:
+ * MDP_LAYOUT_EC (default) d_out[ie*ld_out + ic], the reference's lik[i][j]
+ * (main_MIDASPOM.c:390); MDP_LAYOUT_CE d_out[ic*ld_out + ie] (ld_out >= ne),
+ * where each workgroup's e values of one c column are contiguous, so its
+ * stores coalesce.  Same kernels and values; mdp_loglik_grid is always EC. */
+#define MDP_LAYOUT_EC 0
+#define MDP_LAYOUT_CE 1
+int mdp_engine_set_layout(mdp_engine *engine, int layout);
 int mdp_engine_set_grid(mdp_engine *engine, const double *e, uint32_t ne, const double *c,
                         uint32_t nc);
 int mdp_engine_run(mdp_engine *engine, double *d_out, uint32_t ld_out, void *stream);

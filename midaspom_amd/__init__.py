@@ -172,6 +172,12 @@ class Engine:
         check(lib().mdp_engine_set_grid(self._h, _dptr(e), e.size, _dptr(c), c.size))
         self.ne, self.nc = e.size, c.size
 
+    def set_layout(self, layout: str) -> None:
+        """Layout ``run`` writes: "ec" (default) out[ie*ld + ic], the
+        reference's lik[i][j]; "ce" out[ic*ld + ie] (ld >= ne), whose stores
+        coalesce (``mdp_engine_set_layout``)."""
+        check(lib().mdp_engine_set_layout(self._h, {"ec": 0, "ce": 1}[layout]))
+
     def run(self, d_out: int, ld_out: int, stream: int = 0) -> None:
         """Compute into device memory at address ``d_out`` (e.g. a torch
         tensor's data_ptr()) on hipStream ``stream``, used as given: 0 is

@@ -701,7 +701,7 @@ template <int NPMAX, int DEG, int EPL>
 __global__ __launch_bounds__(kBlock) void k_forward(
     const double *__restrict__ R, size_t ldR, const uint32_t *__restrict__ prog, uint32_t nprog,
     uint32_t np0, double prior0, const double *__restrict__ evals, uint32_t ne,
-    double *__restrict__ out, uint32_t ld_out)
+    double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
 {
     constexpr int RS = DEG + 1;
     constexpr int RSP = (DEG + 2) & ~1;  // per-transition stride in R
@@ -801,7 +801,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(
         double L = 0.0;
 #pragma unroll
         for (int l = 0; l < NPMAX; ++l) L += v[i][l] * prior0;
-        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + ic] = log(L);
+        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = log(L);
     }
 }
 
@@ -815,7 +815,7 @@ template <int NPMAX, int DEG, int EPL>
 __global__ __launch_bounds__(kBlock) void k_forward_lds(
     const double *__restrict__ R, size_t ldR, const uint32_t *__restrict__ prog, uint32_t nprog,
     uint32_t np0, double prior0, const double *__restrict__ evals, uint32_t ne,
-    double *__restrict__ out, uint32_t ld_out, unsigned long long *__restrict__ stamps)
+    double *__restrict__ out, uint32_t ld_out, uint32_t out_cs, unsigned long long *__restrict__ stamps)
 {
     constexpr int RS = DEG + 1;
     constexpr int RSP = (DEG + 2) & ~1;
@@ -929,7 +929,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_lds(
         double L = 0.0;
 #pragma unroll
         for (int l = 0; l < NPMAX; ++l) L += v[i][l] * prior0;
-        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + ic] = log(L);
+        if (ie[i] < ne) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = log(L);
     }
     MDP_STAMP(stamps, 2);
     MDP_RSTAMP(stamps, 7);
@@ -1010,7 +1010,8 @@ constexpr uint32_t kWideLB = 4;
 __global__ __launch_bounds__(kBlock) void k_fwd_wide(
     const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ udesc,
     const uint32_t *__restrict__ np, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
-    uint32_t c0, uint32_t maxA, double *__restrict__ V, uint32_t npmax, double *__restrict__ out, uint32_t ld_out)
+    uint32_t c0, uint32_t maxA, double *__restrict__ V, uint32_t npmax, double *__restrict__ out, uint32_t ld_out,
+    uint32_t out_cs)
 {
     extern __shared__ double xy[];  // [2][maxA + 1][kBlock]: x^r, y^r per lane
     const uint32_t ie = blockIdx.x * kBlock + threadIdx.x, cl = blockIdx.y, ic = c0 + cl;
@@ -1066,7 +1067,7 @@ __global__ __launch_bounds__(kBlock) void k_fwd_wide(
     }
     double L = 0.0;
     for (uint32_t l = 0; l < npp; ++l) L += va[l * cs] * prior0;
-    if (ie < ne) out[(size_t)ie * ld_out + ic] = log(L);
+    if (ie < ne) out[(size_t)ie * ld_out + (size_t)ic * out_cs] = log(L);
 }
 
 // ---------------------------------------------------------------------------
@@ -1188,6 +1189,7 @@ struct mdp_engine {
     std::vector<MdpJitPlan> chunks;               // > 1: the series runs as chunks of years
     std::vector<std::vector<char>> chunk_code;    // their code objects
     bool qglobal = false;     // Q rows built by k_zrows + k_witems + k_wq (k_qrows' tables exceed the LDS)
+    int layout = MDP_LAYOUT_EC;  // mdp_engine_run's output layout (mdp_engine_set_layout)
     int fused_mode = -1;            // MDP_FUSED: -1 auto, 0, 1
     MdpJitPlan jit_plan;
     // direct path (jit): k_qrows computes Pc[j][b] for the needed (j, b)
@@ -1213,6 +1215,16 @@ struct mdp_engine {
 namespace {
 
 // record a launched kernel instantiation ("k_qrows<16,0,2>", ...)
+// the forward kernels' output strides for mdp_engine_run's ld: log L of
+// point (ie, ic) at out[ie * se + ic * sc] -- [e][c] rows (se = ld, sc = 1)
+// or [c][e] columns (se = 1, sc = ld); every forward kernel takes both
+inline void out_strides(const mdp_engine *eng, uint32_t ld, uint32_t &se, uint32_t &sc)
+{
+    const bool ce = eng->layout == MDP_LAYOUT_CE;
+    se = ce ? 1u : ld;
+    sc = ce ? ld : 1u;
+}
+
 void note_launch(const mdp_engine *eng, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 void note_launch(const mdp_engine *eng, const char *fmt, ...)
 {
@@ -1908,16 +1920,18 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
 template <int NP, int DEG, int EPL>
 void launch_fwd_epl(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
 {
+    uint32_t se, sc;
+    out_strides(eng, ld, se, sc);
     dim3 grid(d.nc, (d.ne + kBlock * EPL - 1) / (kBlock * EPL));
     const uint32_t nprog = (uint32_t)eng->prog.size() - 1;
     note_launch(eng, "%s<%d,%d,%d>", eng->fwd_lds ? "k_forward_lds" : "k_forward", NP, DEG, EPL);
     if (eng->fwd_lds)
         MDP_LAUNCH((k_forward_lds<NP, DEG, EPL>), grid, dim3(kBlock), eng->fwd_lds_bytes, s,
-                           d.R, ldR_of(eng), d.prog, nprog, eng->np[0], eng->prior0, d.e, d.ne, out, ld,
-                           d.stamps[2]);
+                           d.R, ldR_of(eng), d.prog, nprog, eng->np[0], eng->prior0, d.e, d.ne, out, se,
+                           sc, d.stamps[2]);
     else
         MDP_LAUNCH((k_forward<NP, DEG, EPL>), grid, dim3(kBlock), 0, s, d.R, ldR_of(eng),
-                           d.prog, nprog, eng->np[0], eng->prior0, d.e, d.ne, out, ld);
+                           d.prog, nprog, eng->np[0], eng->prior0, d.e, d.ne, out, se, sc);
 }
 
 template <int NP, int DEG>
@@ -1957,10 +1971,12 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
         double *vscr = d.vscr;
         uint32_t ldv = d.ldv;
         const uint32_t *qidx = nullptr;
+        uint32_t se, sc;
+        out_strides(eng, ld, se, sc);
         void *args[] = {(void *)&Qrow, (void *)&prior0, (void *)&ev,  (void *)&ne,   (void *)&nc,
-                        (void *)&out,  (void *)&ld,     (void *)&one, (void *)&st,   (void *)&cv,
+                        (void *)&out,  (void *)&se,     (void *)&one, (void *)&st,   (void *)&cv,
                         (void *)&ctab, (void *)&ctl,    (void *)&kmax, (void *)&vscr, (void *)&ldv,
-                        (void *)&qidx};
+                        (void *)&qidx, (void *)&sc};
         // threads per e block: kb (x 2 with the split state-vector kernel)
         const uint32_t kb = eng->jit_kblock, spl = eng->jit_plan.vlds && (eng->jit_plan.vsplit == 2 || eng->jit_plan.vsplit == 4)
                                                       ? (uint32_t)eng->jit_plan.vsplit : 1u;
@@ -2056,12 +2072,14 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, uint
         }
     } else {
         const uint32_t cb = d.wide_cb_fwd;
+        uint32_t se, sc;
+        out_strides(eng, ld, se, sc);
         for (uint32_t c0 = 0; c0 < d.nc; c0 += cb) {
             const uint32_t n = std::min(cb, d.nc - c0);
             const dim3 g((d.ne + kBlock - 1) / kBlock, n);
             note_launch(eng, "k_fwd_wide");
             hipLaunchKernelGGL(k_fwd_wide, g, dim3(kBlock), wide_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.udesc_w,
-                               d.np_d, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, d.V, eng->npmax, out, ld);
+                               d.np_d, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, d.V, eng->npmax, out, se, sc);
         }
     }
     HIP_TRY(hipGetLastError());
@@ -2518,13 +2536,23 @@ int mdp_engine_set_grid(mdp_engine *eng, const double *e, uint32_t ne, const dou
     return set_grid_dev(eng, eng->devs[0], e, ne, c, nc);
 }
 
+int mdp_engine_set_layout(mdp_engine *eng, int layout)
+{
+    if (!eng) return mdp_set_error(MDP_EINVAL, "null argument");
+    if (layout != MDP_LAYOUT_EC && layout != MDP_LAYOUT_CE) return mdp_set_error(MDP_EINVAL, "unknown layout %d", layout);
+    eng->layout = layout;
+    return MDP_OK;
+}
+
 int mdp_engine_run(mdp_engine *eng, double *d_out, uint32_t ld_out, void *stream)
 {
     if (!eng || !d_out) return mdp_set_error(MDP_EINVAL, "null argument");
     if (eng->devs.size() != 1)
         return mdp_set_error(MDP_EINVAL, "mdp_engine_run needs a single-device engine");
     DevCtx &d = eng->devs[0];
-    if (ld_out < d.nc) return mdp_set_error(MDP_EINVAL, "ld_out %u < nc %u", ld_out, d.nc);
+    if (eng->layout == MDP_LAYOUT_CE ? ld_out < d.ne : ld_out < d.nc)
+        return mdp_set_error(MDP_EINVAL, "ld_out %u < %s %u", ld_out, eng->layout == MDP_LAYOUT_CE ? "ne" : "nc",
+                             eng->layout == MDP_LAYOUT_CE ? d.ne : d.nc);
     // the caller's stream as given: NULL is HIP's null stream (torch's default
     // stream), never the engine's private non-blocking stream
     return run_dev(eng, d, d_out, ld_out, (hipStream_t)stream);
@@ -2671,7 +2699,9 @@ int mdp_engine_time_kernels(mdp_engine *eng, double *d_out, uint32_t ld_out, voi
     if (eng->devs.size() != 1)
         return mdp_set_error(MDP_EINVAL, "mdp_engine_time_kernels needs a single-device engine");
     DevCtx &d = eng->devs[0];
-    if (ld_out < d.nc) return mdp_set_error(MDP_EINVAL, "ld_out %u < nc %u", ld_out, d.nc);
+    if (eng->layout == MDP_LAYOUT_CE ? ld_out < d.ne : ld_out < d.nc)
+        return mdp_set_error(MDP_EINVAL, "ld_out %u < %s %u", ld_out, eng->layout == MDP_LAYOUT_CE ? "ne" : "nc",
+                             eng->layout == MDP_LAYOUT_CE ? d.ne : d.nc);
     double t[3];
     const int saved = eng->profiling;
     eng->profiling = 0;

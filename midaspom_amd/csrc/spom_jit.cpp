@@ -211,7 +211,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    const double *__restrict__ Qrow, double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
          "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps,\n"
          "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax,\n"
-         "    double *__restrict__ vscr, u32 ldv, const u32 *__restrict__ qidx)\n{\n"
+         "    double *__restrict__ vscr, u32 ldv, const u32 *__restrict__ qidx, u32 out_cs)\n{\n"
          "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ + 2];\n"
       << stamp(6) << stamp(0) <<
          // XCD-aware order: the dispatcher deals blocks round-robin over the 8
@@ -672,9 +672,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        double L = 0.0;\n"
              "#pragma unroll\n"
              "        for (int l = 0; l < NPLAST; ++l) L += VREF(l) * prior0;\n"
-          << (pl.hack == 1 ? "        if (L == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = log(L);\n"
+          << (pl.hack == 1 ? "        if (L == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = log(L);\n"
                            : "        const double lg_ = LOGF(L);\n"
-                             "        if (lg_ == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = lg_;\n")
+                             "        if (lg_ == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = lg_;\n")
           << "    }\n";
     else if (pl.last)
         o << "    if (SPL == 1 || half == 0) {\n"
@@ -683,7 +683,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        double L = 0.0;\n"
              "#pragma unroll\n"
              "        for (int l = 0; l < NPLAST; ++l) L += VREF(l) * prior0;\n"
-             "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + ic] = LOGF(L);\n"
+             "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = LOGF(L);\n"
              "    }\n"
              "    }\n";
     else  // hand the end vector to the next chunk
