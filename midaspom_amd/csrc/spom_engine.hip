@@ -1181,8 +1181,15 @@ struct mdp_engine {
     bool wide = false;        // wide path (k_witems + k_wq + k_fwd_wide): npmax > 16 or MDP_WIDE=1
     bool qrows_xcd = true;    // k_qrows deals c ranges XCD-aware (MDP_QROWS_XCD=0: blockIdx order)
     double wide_flops_pt = 0; // its FP64 flops per grid point
-    int jit_epl = 1;          // its grid points per lane
+    int jit_epl = 1;          // its grid points per lane (Q-row reading variant and chunks)
     uint32_t jit_kblock = kBlock;  // its threads per column
+    // the fused variant's: 512 threads x 1 point per column by default (the
+    // same 512 e rows per block as 256 x 2, so the grid shape is shared): with
+    // one point per lane its 1 024-thread blocks fit 4 waves per SIMD, and the
+    // per-column prologue runs over twice the threads (config 2: -2 to -3 %)
+    int jit_epl_fused = 1;
+    uint32_t jit_kblock_fused = kBlock;
+    bool jit_shape_env = false;  // MDP_EPL / MDP_JIT_KBLOCK set: one shape for both variants
     double jit_flops_pt = 0;  // its FP64 flops per grid point (counted by the generator)
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
     std::vector<char> jit_code[2];  // forward kernel code objects [fused], compiled on demand
@@ -1612,9 +1619,21 @@ int jit_build(mdp_engine *eng, bool fused)
     if (!eng->jit_code[fused].empty()) return MDP_OK;
     MdpJitPlan plan = eng->jit_plan;
     plan.fused = fused;
+    // the reading variant's shape (e rows per block = kblock x epl, which
+    // set_grid_dev's block count uses before it picks the variant)
+    const int epl_r = plan.epl > 0 ? plan.epl : mdp_jit_default_epl(plan.udesc);
+    const int kb_r = plan.kblock > 0 ? plan.kblock : kBlock;
+    eng->jit_epl = epl_r;
+    eng->jit_kblock = (uint32_t)kb_r;
+    if (fused && !eng->jit_shape_env) {  // the same e rows per block, one point per lane
+        plan.kblock = kb_r * epl_r;
+        plan.epl = 1;
+    }
     const std::string src = mdp_jit_forward_source(plan);
-    eng->jit_epl = plan.epl;
-    eng->jit_kblock = (uint32_t)plan.kblock;
+    if (fused) {
+        eng->jit_epl_fused = plan.epl;
+        eng->jit_kblock_fused = (uint32_t)plan.kblock;
+    }
     eng->jit_flops_pt = plan.flops_pt;
     if (const char *dump = getenv("MDP_JIT_DUMP")) {  // <path>.hip (reading) / <path>.fused.hip
         if (FILE *f = fopen((std::string(dump) + (fused ? ".fused.hip" : ".hip")).c_str(), "w")) {
@@ -1978,9 +1997,11 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
                         (void *)&ctab, (void *)&ctl,    (void *)&kmax, (void *)&vscr, (void *)&ldv,
                         (void *)&qidx, (void *)&sc};
         // threads per e block: kb (x 2 with the split state-vector kernel)
-        const uint32_t kb = eng->jit_kblock, spl = eng->jit_plan.vlds && (eng->jit_plan.vsplit == 2 || eng->jit_plan.vsplit == 4)
-                                                      ? (uint32_t)eng->jit_plan.vsplit : 1u;
-        const uint64_t gy = (d.ne + kb * eng->jit_epl - 1) / (kb * eng->jit_epl);
+        const uint32_t kb = d.fused ? eng->jit_kblock_fused : eng->jit_kblock;
+        const uint32_t epl = d.fused ? (uint32_t)eng->jit_epl_fused : (uint32_t)eng->jit_epl;
+        const uint32_t spl = eng->jit_plan.vlds && (eng->jit_plan.vsplit == 2 || eng->jit_plan.vsplit == 4)
+                                 ? (uint32_t)eng->jit_plan.vsplit : 1u;
+        const uint64_t gy = (d.ne + kb * epl - 1) / (kb * epl);
         const uint32_t fc = d.fused ? (uint32_t)eng->jit_plan.fused_cols : 1u;
         const uint64_t nb = gy * ((d.nc + fc - 1) / fc);  // e blocks x column groups
         if (nb * kb * fc * spl > 0xffffffffull)
@@ -2405,7 +2426,10 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
             if (const char *fv2 = getenv("MDP_JIT_EFAST")) plan.efast = atoi(fv2) != 0;
             if (const char *qx = getenv("MDP_QROWS_XCD")) eng->qrows_xcd = atoi(qx) != 0;
-            if (const char *ev = getenv("MDP_EPL")) plan.epl = atoi(ev);
+            if (const char *ev = getenv("MDP_EPL")) {
+                plan.epl = atoi(ev);
+                eng->jit_shape_env = true;
+            }
             if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
             // compile the variant a small grid uses now (the other on demand)
             if (const char *fv = getenv("MDP_FUSED")) eng->fused_mode = atoi(fv) != 0;
@@ -2413,7 +2437,10 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (const char *cv = getenv("MDP_JIT_HACK")) plan.hack = atoi(cv);
             if (const char *cv = getenv("MDP_FAST_LOG")) plan.fast_log = atoi(cv) != 0;
             if (const char *cv = getenv("MDP_JIT_SQ")) plan.sq = atoi(cv) != 0;
-            if (const char *cv = getenv("MDP_JIT_KBLOCK"); cv && !vlds) plan.kblock = atoi(cv) == 512 ? 512 : 256;
+            if (const char *cv = getenv("MDP_JIT_KBLOCK"); cv && !vlds) {
+                plan.kblock = atoi(cv) == 512 ? 512 : 256;
+                eng->jit_shape_env = true;
+            }
             plan.nj = eng->nj;
             plan.nvar = eng->nvar;
             plan.nitems = eng->nitems;
