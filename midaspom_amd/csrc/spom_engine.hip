@@ -2411,8 +2411,11 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             MdpJitPlan &plan = eng->jit_plan;
             if (vlds) {  // the wide years' states in LDS: one point per lane, never fused
                 plan.vlds = true;
-                plan.epl = 1;
-                plan.kblock = (int)vkb;
+                // points per lane: 1, or 2 (MDP_VLDS_EPL=2: 128 lanes per wave
+                // group, each Q read shared by two points)
+                const char *ve = getenv("MDP_VLDS_EPL");
+                plan.epl = ve && atoi(ve) == 2 ? 2 : 1;
+                plan.kblock = (int)vkb / plan.epl;
                 plan.window = 16;
                 eng->fused_mode = 0;
                 if (const char *sv = getenv("MDP_VSPLIT")) plan.vsplit = atoi(sv) == 1 ? 1 : atoi(sv) == 2 ? 2 : 4;

@@ -163,7 +163,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     std::map<std::pair<uint32_t, uint32_t>, int> widx;
     uint32_t dmax = 0;
     const int nw = weight_index(pl.udesc, widx, dmax);
-    const int EPL = pl.vlds ? 1 : pl.epl > 0 ? pl.epl : (nw <= 64 ? 2 : 1);
+    const int EPL = pl.vlds ? (pl.epl == 2 ? 2 : 1) : pl.epl > 0 ? pl.epl : (nw <= 64 ? 2 : 1);
     pl.epl = EPL;
     const uint32_t np0 = pl.np[0];
     uint32_t npmax = 1;
@@ -251,7 +251,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         for (auto &kv : widx)
             w << "        W[i][" << kv.second << "] = xp[" << (kv.first.first - kv.first.second) << "] * yp["
               << kv.first.second << "];\n";
-        const char *vdst = pl.vlds ? "Vl[k * KBLOCK + tid]" : "v[i][k]";
+        const char *vdst = pl.vlds ? "Vl[(k * EPL + i) * KBLOCK + tid]" : "v[i][k]";
         // (split: the state k set by wave group k % SPL)
         const char *kloop = SPL > 1 ? "#pragma unroll\n        for (int k = half; k < NPMAX; k += SPL) "
                                     : "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) ";
@@ -263,11 +263,11 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         wblock = w.str();
     }
     o << "    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][(NPMAX + SPL - 1) / SPL];\n";
-    if (pl.vlds)  // wide years: the states of lane tid at Vl[k][tid] (EPL 1)
-        o << "    __shared__ double Vl[NPMAX * KBLOCK];\n";
+    if (pl.vlds)  // wide years: state k of point i of lane tid at Vl[k][i][tid]
+        o << "    __shared__ double Vl[NPMAX * EPL * KBLOCK];\n";
     // the state k of point i, as an expression
     auto vref = [&](uint32_t k) {
-        return pl.vlds ? "Vl[" + std::to_string(k) + " * KBLOCK + tid]" : "v[i][" + std::to_string(k) + "]";
+        return pl.vlds ? "Vl[(" + std::to_string(k) + " * EPL + i) * KBLOCK + tid]" : "v[i][" + std::to_string(k) + "]";
     };
     // stage n (compile-time, even) doubles from src (16-byte aligned) into the
     // LDS array dst, which has a double2 of scratch past n: every load is
@@ -665,7 +665,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         o << "    }\n";
     }
     o << "    }}\n" << stamp(3) << "#define NPLAST " << pl.np.back() << "\n"
-      << (pl.vlds ? "#define VREF(l) Vl[(l) * KBLOCK + tid]\n" : "#define VREF(l) v[i][l]\n");
+      << (pl.vlds ? "#define VREF(l) Vl[((l) * EPL + i) * KBLOCK + tid]\n" : "#define VREF(l) v[i][l]\n");
     if (pl.last && (pl.hack == 1 || pl.hack == 2))  // measurement only: the result is never stored
         o << "#pragma unroll\n"
              "    for (int i = 0; i < EPL; ++i) {\n"
