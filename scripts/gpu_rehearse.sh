@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/reh
-for cfg in "2" "3" "5" "4 --grid4 32"; do
+for cfg in "2" "3" "5" "6" "4 --grid4 32"; do
   tag=$(echo $cfg | cut -d' ' -f1)
   timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 --backend gloo --config $cfg > gpurun_out/reh/n2_cfg$tag.json 2> gpurun_out/reh/n2_cfg$tag.err || { echo "rehearsal cfg$tag failed"; tail -20 gpurun_out/reh/n2_cfg$tag.err; exit 1; }
   echo "cfg$tag:"; cat gpurun_out/reh/n2_cfg$tag.json | cut -c1-400

@@ -35,6 +35,7 @@ ap.add_argument("--steps", type=int, default=30)
 ap.add_argument("--configs", default="2,3")
 ap.add_argument("--variants", default=DEFAULT_VARIANTS)
 ap.add_argument("--diag", action="store_true")
+ap.add_argument("--layout", default="ce", choices=["ce", "ec"], help="device layout of log L (bench.py's default: ce)")
 args = ap.parse_args()
 torch.cuda.set_device(0)
 tmp = Path(tempfile.mkdtemp())
@@ -57,6 +58,7 @@ for cfgid in [int(x) for x in args.configs.split(",")]:
         eng = mdp.Engine(model, devices=[0])
         t_create = time.perf_counter() - t0
         eng.set_grid(g, g)
+        eng.set_layout(args.layout)
         out = torch.empty((s, s), dtype=torch.float64, device="cuda")
         st = torch.cuda.current_stream().cuda_stream
         for _ in range(3):
