@@ -410,7 +410,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        qb[k] = q0;\n"
              "        qn[k] = q1 - q0;\n"
              "#pragma unroll\n"
-             "        for (int u = 0; u < QUN; ++u) qx[k][u] = Qil[q0 + u < NQI ? q0 + u : NQI - 1];\n"
+             // only the entry's own items: lanes past their count stay masked
+             // off, so the gathers below touch no other entry's banks
+             "        for (int u = 0; u < QUN; ++u) qx[k][u] = (u32)u < qn[k] ? Qil[q0 + u] : 0u;\n"
              "    }\n"
              // Z per (column, row): the row's KZ (compile-time bound) values
              // all in flight; rows past kmax contribute fma(-c, 0, 1) = 1 (with
@@ -477,7 +479,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "            double a = 0.0;\n"
              "#pragma unroll\n"
              "            for (int u = 0; u < QUN; ++u) {\n"
-             "                const double pv = pl[qx[k][u]];\n"
+             "                const double pv = (u32)u < qn[k] ? pl[qx[k][u]] : 0.0;\n"
              "                a = (u32)u < qn[k] ? a + pv : a;\n"
              "            }\n"
              "#if QML > QUN\n"
