@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // kernel's XCD-aware order gives XCD x -- and the forward reads these Q
     // rows from its own L2
     const uint32_t nb = gridDim.x, full = nb & ~7u;
-    const uint32_t lb = (xcd & 1u) && blockIdx.x < full ? (blockIdx.x & 7u) * (full >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const uint32_t lb = xcd && blockIdx.x < full ? (blockIdx.x & 7u) * (full >> 3) + (blockIdx.x >> 3) : blockIdx.x;
     const uint32_t c0 = lb * CB, ncb = min((uint32_t)CB, nc - c0);
     // per-c values in planes of two c values ([CB/2][n][2] for CB = 4): a
     // lane's 16-byte access then sits 16 bytes after its neighbour's, not 32,
@@ -368,109 +368,12 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     double cv[CB];  // this workgroup's c values (the last one again past the grid: never stored)
 #pragma unroll
     for (int i = 0; i < CB; ++i) cv[i] = cvals[c0 + min((uint32_t)i, ncb - 1)];  // no load in a branch
-    // staged stores past an array's end go to this scratch slot (no branch)
-    uint2 *const dummy = (uint2 *)((double *)(It + nitems) + (ncoef + 2 + nqi) / 2);
-    // phase 1, per row and c value: Z_r(c) = the row's explicit columns in
-    // k_zrows' four chains and order, the clamp test against the row maximum
-    // (stored first), the small columns' series; then the row's pressures
-    // min(1, c S) (the columns of j, where sv holds -1, and padded slots
-    // select a factor of exactly 1.0 in phase 2 whatever is stored here)
-    if (!(xcd & 2u) || NV > 16) {
-        // threads over (row, c) (MDP_QROWS_ZROW=0, and NV = 24, whose row
-        // threads would spill): every thread loads its row, so each row is
-        // read CB times
-        // items, the Q CSR and the var-column S: every thread's loads in flight
-        // before its stores (one global round trip instead of one per pass)
-        {
-            constexpr uint32_t kSt = 4;
-            const uint32_t nmax = max(max(nitems, ncoef + 1), nqi);
-            for (uint32_t i0 = threadIdx.x; i0 < nmax; i0 += kSt * kQrowsBlock) {
-                uint2 ti[kSt];
-                uint32_t ts[kSt], tq[kSt];
-#pragma unroll
-                for (uint32_t u = 0; u < kSt; ++u) {
-                    const uint32_t i = i0 + u * kQrowsBlock;
-                    ti[u] = i < nitems ? items[i] : make_uint2(0u, 0u);
-                    ts[u] = i <= ncoef ? qstart[i] : 0u;
-                    tq[u] = i < nqi ? qitem[i] : 0u;
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < kSt; ++u) {
-                    const uint32_t i = i0 + u * kQrowsBlock;
-                    if (i < nitems) It[i] = ti[u];
-                    if (i <= ncoef) Qs[i] = ts[u];
-                    if (i < nqi) Qi[i] = tq[u];
-                }
-            }
-        }
-        MDP_STAMP(stamps, 4);
-        // 1. Z per (row, c)
-        for (uint32_t w = threadIdx.x; w < nrows * CB; w += kQrowsBlock) {
-            const uint32_t cl = w % CB, r = w / CB;
-            double c = cv[0];
-#pragma unroll
-            for (int i = 1; i < CB; ++i) c = cl == (uint32_t)i ? cv[i] : c;
-            const double2 *zr = (const double2 *)(zsT + (size_t)r * kmax);
-            double za = 1.0, zb = 1.0, zcc = 1.0, zd = 1.0;
-            auto chunk = [&](const double *sk) {
-                za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
-                zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);
-                zcc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);
-                zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
-            };
-            double first = 0.0;
-            uint32_t k = 0;
-            for (; k + 16 <= kmax; k += 16) {
-                double sk[16];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const double2 t2 = zr[k / 2 + u];
-                    sk[2 * u] = t2.x;
-                    sk[2 * u + 1] = t2.y;
-                }
-                if (k == 0) first = sk[0];
-                chunk(sk);
-                chunk(sk + 8);
-            }
-            if (k < kmax) {  // kmax is a multiple of 8
-                double sk[8];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const double2 t2 = zr[k / 2 + u];
-                    sk[2 * u] = t2.x;
-                    sk[2 * u + 1] = t2.y;
-                }
-                if (k == 0) first = sk[0];
-                chunk(sk);
-            }
-            double zz = (za * zb) * (zcc * zd);
-            if (kmax && !(fma(-c, first, 1.0) > 0.0)) zz = 0.0;
-            double zq[kZTermsDev];
-#pragma unroll
-            for (int i = 0; i < kZTermsDev; ++i) zq[i] = zc[(size_t)r * kZTermsDev + i];
-            zz *= zseries(zq, c);
-            Zl[pix(nrows, r, cl)] = zz;
-            // the row's pressures for this c: min(1, c S) (the columns of j, where
-            // sv holds -1, and padded slots select a factor of exactly 1.0 in
-            // phase 2 whatever is stored here)
-            double pr[NV];
-#pragma unroll
-            for (int b = 0; b < NV; ++b) {
-                // min(1, c S) as the reference clamps it (:355-357): NaN stays NaN
-                const double t = (EXACT || (uint32_t)b < nvar) ? c * sv[(size_t)r * nvar + b] : 0.0;
-                pr[b] = t > 1.0 ? 1.0 : t;
-            }
-            double2 *pd = (double2 *)(Prl + (size_t)r * PRS + cl * NV);
-#pragma unroll
-            for (int b = 0; b < NV / 2; ++b) pd[b] = make_double2(pr[2 * b], pr[2 * b + 1]);
-        }
-    } else {
-        // threads over rows, all CB c values each (default): the row's
-        // explicit columns, series coefficients and var-column S are read
-        // once per workgroup instead of CB times (the (row, c) threads' loads
-        // were most of phase 1's vector-memory issue), the next 8 columns in
-        // flight during this 8's products.  The items, the Q CSR: every load
-        // of a pass in flight before its (branch-free) stores.
+    // items and the Q CSR: every thread's loads of a pass in flight before
+    // its stores.  (Clamped indices and branch-free stores to a scratch slot
+    // shortened the staging, 2.3 k -> 1.8 k cycles on config 3, but phase 1
+    // as a whole went 8.7 k -> 9.3 k: its loads then queue behind the
+    // staging's.  Not kept.)
+    {
         constexpr uint32_t kSt = 4;
         const uint32_t nmax = max(max(nitems, ncoef + 1), nqi);
         for (uint32_t i0 = threadIdx.x; i0 < nmax; i0 += kSt * kQrowsBlock) {
@@ -479,74 +382,87 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
 #pragma unroll
             for (uint32_t u = 0; u < kSt; ++u) {
                 const uint32_t i = i0 + u * kQrowsBlock;
-                ti[u] = items[nitems ? min(i, nitems - 1) : 0u];
-                ts[u] = qstart[min(i, ncoef)];
-                tq[u] = qitem[nqi ? min(i, nqi - 1) : 0u];
+                ti[u] = i < nitems ? items[i] : make_uint2(0u, 0u);
+                ts[u] = i <= ncoef ? qstart[i] : 0u;
+                tq[u] = i < nqi ? qitem[i] : 0u;
             }
 #pragma unroll
             for (uint32_t u = 0; u < kSt; ++u) {
                 const uint32_t i = i0 + u * kQrowsBlock;
-                *(i < nitems ? It + i : dummy) = ti[u];
-                *(i <= ncoef ? Qs + i : (uint32_t *)dummy) = ts[u];
-                *(i < nqi ? Qi + i : (uint32_t *)dummy) = tq[u];
+                if (i < nitems) It[i] = ti[u];
+                if (i <= ncoef) Qs[i] = ts[u];
+                if (i < nqi) Qi[i] = tq[u];
             }
         }
-        MDP_STAMP(stamps, 4);
-        for (uint32_t r = threadIdx.x; r < nrows; r += kQrowsBlock) {
-            const double2 *zr = (const double2 *)(zsT + (size_t)r * kmax);
-            double2 u0, u1, u2, u3;
-            u0 = u1 = u2 = u3 = make_double2(0.0, 0.0);
-            if (kmax) {
-                u0 = zr[0];
-                u1 = zr[1];
-                u2 = zr[2];
-                u3 = zr[3];
+    }
+    MDP_STAMP(stamps, 4);
+    // 1. Z per (row, c): the row's explicit columns in k_zrows' four chains
+    // and order, the clamp test against the row maximum (stored first), the
+    // small columns' series; then the row's pressures min(1, c S) (the
+    // columns of j, where sv holds -1, and padded slots select a factor of
+    // exactly 1.0 in phase 2 whatever is stored here).  Measured slower and
+    // not kept (config 3, phase 1 8.7 k cycles): threads over rows with all
+    // CB c values each, so each row is read once, not CB times (9.3 k: the
+    // per-thread chains at one wave per SIMD); the series coefficients and S
+    // loaded with the first columns (9.8 k: the slowest wave later).
+    for (uint32_t w = threadIdx.x; w < nrows * CB; w += kQrowsBlock) {
+        const uint32_t cl = w % CB, r = w / CB;
+        double c = cv[0];
+#pragma unroll
+        for (int i = 1; i < CB; ++i) c = cl == (uint32_t)i ? cv[i] : c;
+        const double2 *zr = (const double2 *)(zsT + (size_t)r * kmax);
+        double za = 1.0, zb = 1.0, zcc = 1.0, zd = 1.0;
+        auto chunk = [&](const double *sk) {
+            za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
+            zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);
+            zcc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);
+            zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
+        };
+        double first = 0.0;
+        uint32_t k = 0;
+        for (; k + 16 <= kmax; k += 16) {
+            double sk[16];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const double2 t2 = zr[k / 2 + u];
+                sk[2 * u] = t2.x;
+                sk[2 * u + 1] = t2.y;
             }
-            double zq[kZTermsDev], svr[NV];
-#pragma unroll
-            for (int i = 0; i < kZTermsDev; ++i) zq[i] = zc[(size_t)r * kZTermsDev + i];
-#pragma unroll
-            for (int b = 0; b < NV; ++b) svr[b] = (EXACT || (uint32_t)b < nvar) ? sv[(size_t)r * nvar + b] : 0.0;
-            const double first = u0.x;
-            double za[CB], zb[CB], zcc[CB], zd[CB];
-#pragma unroll
-            for (int i = 0; i < CB; ++i) za[i] = zb[i] = zcc[i] = zd[i] = 1.0;
-            for (uint32_t k = 0; k < kmax; k += 8) {  // kmax is a multiple of 8
-                const bool more = k + 8 < kmax;
-                const double2 *zn = zr + (more ? (k + 8) / 2 : 0);
-                const double2 n0 = zn[0], n1 = zn[1], n2 = zn[2], n3 = zn[3];
-#pragma unroll
-                for (int i = 0; i < CB; ++i) {
-                    const double c = cv[i];
-                    za[i] *= fma(-c, u0.x, 1.0) * fma(-c, u2.x, 1.0);
-                    zb[i] *= fma(-c, u0.y, 1.0) * fma(-c, u2.y, 1.0);
-                    zcc[i] *= fma(-c, u1.x, 1.0) * fma(-c, u3.x, 1.0);
-                    zd[i] *= fma(-c, u1.y, 1.0) * fma(-c, u3.y, 1.0);
-                }
-                u0 = n0;
-                u1 = n1;
-                u2 = n2;
-                u3 = n3;
-            }
-#pragma unroll
-            for (int i = 0; i < CB; ++i) {
-                const double c = cv[i];
-                double zz = (za[i] * zb[i]) * (zcc[i] * zd[i]);
-                if (kmax && !(fma(-c, first, 1.0) > 0.0)) zz = 0.0;
-                zz *= zseries(zq, c);
-                Zl[pix(nrows, r, i)] = zz;
-                double pr[NV];
-#pragma unroll
-                for (int b = 0; b < NV; ++b) {
-                    // min(1, c S) as the reference clamps it (:355-357): NaN stays NaN
-                    const double t = (EXACT || (uint32_t)b < nvar) ? c * svr[b] : 0.0;
-                    pr[b] = t > 1.0 ? 1.0 : t;
-                }
-                double2 *pd = (double2 *)(Prl + (size_t)r * PRS + i * NV);
-#pragma unroll
-                for (int b = 0; b < NV / 2; ++b) pd[b] = make_double2(pr[2 * b], pr[2 * b + 1]);
-            }
+            if (k == 0) first = sk[0];
+            chunk(sk);
+            chunk(sk + 8);
         }
+        if (k < kmax) {  // kmax is a multiple of 8
+            double sk[8];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double2 t2 = zr[k / 2 + u];
+                sk[2 * u] = t2.x;
+                sk[2 * u + 1] = t2.y;
+            }
+            if (k == 0) first = sk[0];
+            chunk(sk);
+        }
+        double zz = (za * zb) * (zcc * zd);
+        if (kmax && !(fma(-c, first, 1.0) > 0.0)) zz = 0.0;
+        double zq[kZTermsDev];
+#pragma unroll
+        for (int i = 0; i < kZTermsDev; ++i) zq[i] = zc[(size_t)r * kZTermsDev + i];
+        zz *= zseries(zq, c);
+        Zl[pix(nrows, r, cl)] = zz;
+        // the row's pressures for this c: min(1, c S) (the columns of j, where
+        // sv holds -1, and padded slots select a factor of exactly 1.0 in
+        // phase 2 whatever is stored here)
+        double pr[NV];
+#pragma unroll
+        for (int b = 0; b < NV; ++b) {
+            // min(1, c S) as the reference clamps it (:355-357): NaN stays NaN
+            const double t = (EXACT || (uint32_t)b < nvar) ? c * sv[(size_t)r * nvar + b] : 0.0;
+            pr[b] = t > 1.0 ? 1.0 : t;
+        }
+        double2 *pd = (double2 *)(Prl + (size_t)r * PRS + cl * NV);
+#pragma unroll
+        for (int b = 0; b < NV / 2; ++b) pd[b] = make_double2(pr[2 * b], pr[2 * b + 1]);
     }
     MDP_STAMP(stamps, 5);
     __syncthreads();
@@ -1288,7 +1204,6 @@ struct mdp_engine {
     bool jit = false;         // forward kernel specialised with hipRTC (spom_jit.cpp)
     bool wide = false;        // wide path (k_witems + k_wq + k_fwd_wide): npmax > 16 or MDP_WIDE=1
     bool qrows_xcd = true;    // k_qrows deals c ranges XCD-aware (MDP_QROWS_XCD=0: blockIdx order)
-    bool qrows_zrow = true;   // k_qrows phase 1 threads over rows, all c values each (MDP_QROWS_ZROW=0: over (row, c))
     double wide_flops_pt = 0; // its FP64 flops per grid point
     int jit_epl = 1;          // its grid points per lane (Q-row reading variant and chunks)
     uint32_t jit_kblock = kBlock;  // its threads per column
@@ -1623,8 +1538,7 @@ size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
     const size_t nv = eng->nvar <= 8 ? 8 : eng->nvar <= 16 ? 16 : 24;  // k_qrows NV
     return ((((size_t)cb * eng->nj + 1) & ~(size_t)1) + (size_t)eng->nj * (cb * nv + 2) + (size_t)cb * eng->nitems) *
                sizeof(double) +
-           (size_t)eng->nitems * sizeof(uint2) + ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t) +
-           16;  // the staging's scratch slot
+           (size_t)eng->nitems * sizeof(uint2) + ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);
 }
 
 // Z rows for a grid whose |c| <= cmax.  Z_j(c) = prod over the always-zero
@@ -2252,7 +2166,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
     MDP_LAUNCH((k_qrows<NV, EX, CB>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, eng->nvar, eng->nj,         \
                d.zs_kmax, d.zs, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
                (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1],                 \
-               (uint32_t)(eng->qrows_xcd ? 1u : 0u) | (eng->qrows_zrow ? 2u : 0u)); } while (0)
+               (uint32_t)(eng->qrows_xcd ? 1u : 0u)); } while (0)
         // c values per workgroup: <= qrows_maxcb(nvar) (register budget at 1024 threads)
         if (eng->nvar == 8) {
             if (cb == 4) MDP_QROWS_CB(8, true, 4);
@@ -2539,7 +2453,6 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
             if (const char *fv2 = getenv("MDP_JIT_EFAST")) plan.efast = atoi(fv2) != 0;
             if (const char *qx = getenv("MDP_QROWS_XCD")) eng->qrows_xcd = atoi(qx) != 0;
-            if (const char *qz = getenv("MDP_QROWS_ZROW")) eng->qrows_zrow = atoi(qz) != 0;
             if (const char *ev = getenv("MDP_EPL")) {
                 plan.epl = atoi(ev);
                 eng->jit_shape_env = true;
