@@ -38,6 +38,7 @@ namespace {
 
 constexpr int kScnBlock = 1024;       // 16 waves: four per SIMD
 constexpr bool kPingPong = kScnBlock <= 768;  // register double-buffering (needs > 128 VGPRs)
+constexpr bool kDppFactors = true;  // hi factors by DPP row broadcast (fma_rowbcast) instead of LDS broadcasts
 constexpr int kE = 32;                 // e values per workgroup (lanes mod 32)
 constexpr int kWaves = kScnBlock / 64;
 constexpr uint32_t kMaxN = 8;          // k_scn: 2 x 2^8 x 32 state values + factor tables in LDS
@@ -94,6 +95,18 @@ __host__ __device__ constexpr int sup_rank(int NL, int jl, int bl)
     for (int b = NL - 1; b >= 0; --b)
         if (!((jl >> b) & 1)) r = 2 * r + ((bl >> b) & 1);
     return r;
+}
+
+// acc + (lane K of this lane's row of 16)'s f * x: v_fmac_f64 with a DPP
+// row_newbcast source (gfx950), so a wave-half-uniform factor reaches every
+// lane of its row without a broadcast LDS read or an extra move
+template <int K>
+__device__ __forceinline__ double fma_rowbcast(double f, double x, double acc)
+{
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc)
+        : "v"(f), "v"(x), "i"(K));
+    return acc;
 }
 
 // lanes 0-31: a[lane] + a[lane + 32]; lanes 32-63: b[lane - 32] + b[lane]
@@ -307,6 +320,34 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
                     acc[jl] = fma(bv[jl], in, acc[jl]);
                 }
             };
+            // the same sums with the hi factors spread over the lanes of each
+            // row of 16 (lane k holds factor k of its half's superset): one
+            // lane-distinct ds_read_b64 per superset instead of NLO / 2
+            // broadcast ds_read_b128 -- half the colonisation phase's LDS
+            // cycles -- and the same FMAs, so the same bits
+            auto accumulate_dpp = [&](const double (&yc)[NLO], double bvr) {
+                double in[NLO];
+#pragma unroll
+                for (int jl = 0; jl < NLO; ++jl) {
+                    in[jl] = 0.0;
+#pragma unroll
+                    for (int bl = 0; bl < NLO; ++bl)
+                        if ((bl & jl) == jl) in[jl] = fma(A[aoff(NL, jl) + sup_rank(NL, jl, bl)], yc[bl], in[jl]);
+                }
+                static_assert(NLO <= 8, "hi factors of a superset fit a row of 16 lanes");
+                acc[0] = fma_rowbcast<0>(bvr, in[0], acc[0]);
+                if constexpr (NLO > 1) acc[1] = fma_rowbcast<1>(bvr, in[1], acc[1]);
+                if constexpr (NLO > 2) {
+                    acc[2] = fma_rowbcast<2>(bvr, in[2], acc[2]);
+                    acc[3] = fma_rowbcast<3>(bvr, in[3], acc[3]);
+                }
+                if constexpr (NLO > 4) {
+                    acc[4] = fma_rowbcast<4>(bvr, in[4], acc[4]);
+                    acc[5] = fma_rowbcast<5>(bvr, in[5], acc[5]);
+                    acc[6] = fma_rowbcast<6>(bvr, in[6], acc[6]);
+                    acc[7] = fma_rowbcast<7>(bvr, in[7], acc[7]);
+                }
+            };
             uint32_t sub = 0;
             if (!kPingPong) {
                 // the next superset's states load under this one's FMAs (its
@@ -316,20 +357,25 @@ __global__ __launch_bounds__(kScnBlock) void k_scn(ScnArgs a, const double *__re
 #pragma unroll
                 for (int l = 0; l < NLO; ++l) yn[l] = yrow[l * LS];
                 for (uint32_t it = 0; it < units; ++it) {
-                    double ya[NLO], ba[NLO];
+                    double ya[NLO];
 #pragma unroll
                     for (int l = 0; l < NLO; ++l) ya[l] = yn[l];
                     const uint32_t sn = (sub - frp) & frp;  // wraps to 0 after the last
 #pragma unroll
                     for (int l = 0; l < NLO; ++l) yn[l] = yrow[l * LS + sn * kE];
-                    const double2 *bp = (const double2 *)(bt + it * NLO);
+                    if (kDppFactors) {
+                        accumulate_dpp(ya, bt[it * NLO + (tid & (NLO - 1))]);
+                    } else {
+                        double ba[NLO];
+                        const double2 *bp = (const double2 *)(bt + it * NLO);
 #pragma unroll
-                    for (int l = 0; l < NLO / 2; ++l) {
-                        const double2 t2 = bp[l];
-                        ba[2 * l] = t2.x;
-                        ba[2 * l + 1] = t2.y;
+                        for (int l = 0; l < NLO / 2; ++l) {
+                            const double2 t2 = bp[l];
+                            ba[2 * l] = t2.x;
+                            ba[2 * l + 1] = t2.y;
+                        }
+                        accumulate(ya, ba);
                     }
-                    accumulate(ya, ba);
                     sub = sn;
                 }
             } else {
