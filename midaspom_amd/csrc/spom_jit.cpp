@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <atomic>
 #include <mutex>
 #include <sstream>
@@ -172,8 +173,15 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     o << kPrelude;
     const bool gather = !pl.qidx.empty();
     const bool sq = pl.sq && !pl.fused;
+    const bool dppq = pl.dppq && !sq;
     const size_t ldq_local = gather ? ((pl.qidx.size() + 1) & ~(size_t)1) : pl.ldQ;
     o << "#define LOGF(x) " << (pl.fast_log ? "mdp_log(x)" : "log(x)") << "\n";
+    if (dppq)  // acc + Q[16 c + K] w, the coefficient broadcast from lane K of each row of 16
+        o << "template <int K>\n"
+             "__device__ __forceinline__ double qf(double qc, double w, double acc)\n{\n"
+             "    asm(\"v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf\"\n"
+             "        : \"+v\"(acc) : \"v\"(qc), \"v\"(w), \"i\"(K));\n"
+             "    return acc;\n}\n";
     o << "#define KBLOCK " << (pl.kblock > 0 ? pl.kblock : 256) << "\n";  // threads per column
     o << "#define EPL " << EPL << "\n#define LDQ " << ldq_local << "\n#define LDQG "
       << (gather ? pl.ldq_row : pl.ldQ) << "\n#define NQG " << pl.qidx.size() << "\n#define NPMAX " << npmax
@@ -212,7 +220,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps,\n"
          "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax,\n"
          "    double *__restrict__ vscr, u32 ldv, const u32 *__restrict__ qidx, u32 out_cs)\n{\n"
-         "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ + 2];\n"
+      << "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ + " << (dppq ? 16 : 2) << "];\n"
       << stamp(6) << stamp(0) <<
          // XCD-aware order: the dispatcher deals blocks round-robin over the 8
          // XCDs, so consecutive logical blocks (adjacent c columns of the
@@ -496,8 +504,30 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     // (scalar Q with gathered chunks: the chunk-local offset mapped back to
     // the Q row's own)
     auto qoff = [&](uint32_t i) { return std::to_string(sq && gather ? pl.qidx[i] : i); };
+    // dppq: the chunks a region has loaded (declared in its scope), and the
+    // declarations the next emitted line needs first
+    std::set<uint32_t> region_chunks;
+    std::string chunk_decls;
+    auto chunk = [&](uint32_t o) {
+        const uint32_t c = o / 16;
+        if (region_chunks.insert(c).second)
+            chunk_decls += "    const double QC" + std::to_string(c) + " = Qh[" + std::to_string(16 * c) +
+                           " + (threadIdx.x & 15u)];\n";
+        return "qf<" + std::to_string(o % 16) + ">(QC" + std::to_string(c);
+    };
+    auto flush_decls = [&]() {
+        std::string t;
+        t.swap(chunk_decls);
+        return t;
+    };
     auto pexpr = [&](uint32_t d) {
         const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u, nA = d >> 27;
+        if (dppq) {  // the same FMAs as below (the first as fma(Q, W, 0) = Q W)
+            std::string e = "0.0";
+            for (uint32_t m = 0; m <= nX; ++m)
+                e = chunk(off + m) + ", W[i][" + std::to_string(widx[std::make_pair(nA, m)]) + "], " + e + ")";
+            return e;
+        }
         std::string e = "Qh[" + qoff(off) + "] * W[i][" +
                         std::to_string(widx[std::make_pair(nA, 0u)]) + "]";
         for (uint32_t m = 1; m <= nX; ++m)
@@ -522,6 +552,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     auto fence = [&]() {
         if (++since >= window) {
             o << "    }}\n" << guard;
+            region_chunks.clear();
             since = 0;
         }
     };
@@ -598,7 +629,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         if (npp == 1 && npc == 1 && !pl.vlds) {
             std::string pre;
             const std::string e = use_expr(u++, pre);
-            o << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
+            o << flush_decls() << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
             flops += 1.0;
             fence();
             continue;
@@ -617,6 +648,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                           : h + 1 < SPL ? "    } else if (half == " + std::to_string(h) + ") {\n"
                                         : std::string("    } else {\n"))
                       << guard;
+                    region_chunks.clear();
                     since = 0;
                 }
                 for (uint32_t k = 0; k < npp; ++k)
@@ -624,7 +656,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                         std::string pre;
                         const std::string e = use_expr(ubase + (size_t)l * npp + k, pre);
                         const std::string acc = "n[i][" + std::to_string(l / SPL) + "]";
-                        o << "    for (int i = 0; i < EPL; ++i) { " << pre << acc << " = fma(" << vref(k) << ", " << e
+                        o << flush_decls() << "    for (int i = 0; i < EPL; ++i) { " << pre << acc << " = fma(" << vref(k) << ", " << e
                           << ", " << (k ? acc : std::string("0.0")) << "); }\n";
                         flops += k ? 2.0 : 1.0;
                         fence();
@@ -644,6 +676,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             o << (split ? "        }\n    }\n    __syncthreads();\n" : "    }\n");
             if (split) {
                 o << guard;
+                region_chunks.clear();
                 since = 0;
             }
             u = ubase + (size_t)npp * npc;
@@ -654,7 +687,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             for (uint32_t k = 0; k < npp; ++k) {
                 std::string pre;
                 const std::string e = use_expr(u++, pre);
-                o << "    for (int i = 0; i < EPL; ++i) { " << pre << "n[i][" << l << "] = fma(" << vref(k) << ", "
+                o << flush_decls() << "    for (int i = 0; i < EPL; ++i) { " << pre << "n[i][" << l << "] = fma(" << vref(k) << ", "
                   << e << ", " << (k ? "n[i][" + std::to_string(l) + "]" : std::string("0.0")) << "); }\n";
                 flops += k ? 2.0 : 1.0;
                 fence();

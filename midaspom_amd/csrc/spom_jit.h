@@ -46,6 +46,11 @@ struct MdpJitPlan {
     // into SGPRs, FMA operands) instead of staged in LDS (MDP_JIT_SQ)
     bool sq = false;
     int slots = 8;                // registers caching transitions that recur (0: none)
+    // Q coefficients as 16-value chunks (lane k of each row of 16 holds Q[16 c
+    // + k], one lane-distinct ds_read_b64 per chunk) fed to the FMAs through
+    // v_fmac_f64_dpp row_newbcast instead of broadcast LDS pair reads
+    // (MDP_JIT_DPPQ; not with sq)
+    bool dppq = false;
     int wpe = 0;                  // minimum waves per SIMD asked of the compiler (0: its default)
     double flops_pt = 0;          // out: FP64 flops per grid point of the generated code
     // a chunk of a long series (main_MIDASPOM.c:371-384 has no length limit):
