@@ -99,7 +99,11 @@ __host__ __device__ constexpr int sup_rank(int NL, int jl, int bl)
 
 // acc + (lane K of this lane's row of 16)'s f * x: v_fmac_f64 with a DPP
 // row_newbcast source (gfx950), so a wave-half-uniform factor reaches every
-// lane of its row without a broadcast LDS read or an extra move
+// lane of its row without a broadcast LDS read or an extra move.  A DPP
+// source must not be written by a VALU instruction in the two before it; f is
+// always a value just loaded from LDS (no VALU write), and the compiled k_scn
+// was checked for such a pair (none).  All lanes are active
+// where it is used (wave-uniform loops).
 template <int K>
 __device__ __forceinline__ double fma_rowbcast(double f, double x, double acc)
 {
