@@ -2449,7 +2449,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             plan.ldQ = eng->ldQ;
             plan.diag = eng->diag;
             if (const char *cv = getenv("MDP_JIT_SLOTS")) plan.slots = atoi(cv);
-            if (const char *cv = getenv("MDP_JIT_DPPQ")) plan.dppq = atoi(cv) != 0;
+            if (const char *cv = getenv("MDP_JIT_DPPQ")) plan.dppq = std::max(0, std::min(2, atoi(cv)));
             if (const char *wv = getenv("MDP_JIT_WPE")) plan.wpe = atoi(wv);
             if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
             if (const char *fv2 = getenv("MDP_JIT_EFAST")) plan.efast = atoi(fv2) != 0;

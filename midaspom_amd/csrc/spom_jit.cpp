@@ -173,7 +173,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     o << kPrelude;
     const bool gather = !pl.qidx.empty();
     const bool sq = pl.sq && !pl.fused;
-    const bool dppq = pl.dppq && !sq;
+    const int dppq = sq ? 0 : pl.dppq;
     const size_t ldq_local = gather ? ((pl.qidx.size() + 1) & ~(size_t)1) : pl.ldQ;
     o << "#define LOGF(x) " << (pl.fast_log ? "mdp_log(x)" : "log(x)") << "\n";
     if (dppq)  // acc + Q[16 c + K] w, the coefficient broadcast from lane K of each row of 16
@@ -522,9 +522,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     };
     auto pexpr = [&](uint32_t d) {
         const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u, nA = d >> 27;
-        if (dppq) {  // the same FMAs as below (the first as fma(Q, W, 0) = Q W)
-            std::string e = "0.0";
-            for (uint32_t m = 0; m <= nX; ++m)
+        if (dppq) {  // the same FMAs as below (dppq 1: the first as fma(Q, W, 0) = Q W)
+            std::string e = dppq == 1 ? std::string("0.0")
+                                      : "Qh[" + qoff(off) + "] * W[i][" + std::to_string(widx[std::make_pair(nA, 0u)]) + "]";
+            for (uint32_t m = dppq == 1 ? 0 : 1; m <= nX; ++m)
                 e = chunk(off + m) + ", W[i][" + std::to_string(widx[std::make_pair(nA, m)]) + "], " + e + ")";
             return e;
         }

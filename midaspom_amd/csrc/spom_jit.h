@@ -49,8 +49,10 @@ struct MdpJitPlan {
     // Q coefficients as 16-value chunks (lane k of each row of 16 holds Q[16 c
     // + k], one lane-distinct ds_read_b64 per chunk) fed to the FMAs through
     // v_fmac_f64_dpp row_newbcast instead of broadcast LDS pair reads
-    // (MDP_JIT_DPPQ; not with sq)
-    bool dppq = false;
+    // (MDP_JIT_DPPQ; not with sq): 1 every coefficient (each dot product
+    // from a zeroed accumulator), 2 all but the first (its product a plain
+    // multiply with the coefficient read as before)
+    int dppq = 0;
     int wpe = 0;                  // minimum waves per SIMD asked of the compiler (0: its default)
     double flops_pt = 0;          // out: FP64 flops per grid point of the generated code
     // a chunk of a long series (main_MIDASPOM.c:371-384 has no length limit):
