@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // kernel's XCD-aware order gives XCD x -- and the forward reads these Q
     // rows from its own L2
     const uint32_t nb = gridDim.x, full = nb & ~7u;
-    const uint32_t lb = (xcd & 1u) && blockIdx.x < full ? (blockIdx.x & 7u) * (full >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const uint32_t lb = xcd && blockIdx.x < full ? (blockIdx.x & 7u) * (full >> 3) + (blockIdx.x >> 3) : blockIdx.x;
     const uint32_t c0 = lb * CB, ncb = min((uint32_t)CB, nc - c0);
     // per-c values in planes of two c values ([CB/2][n][2] for CB = 4): a
     // lane's 16-byte access then sits 16 bytes after its neighbour's, not 32,
@@ -405,29 +405,12 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // CB c values each, so each row is read once, not CB times (9.3 k: the
     // per-thread chains at one wave per SIMD); the series coefficients and S
     // loaded with the first columns (9.8 k: the slowest wave later).
-    // The rows' explicit columns are staged once into the Pc area (unused
-    // until phase 2) when they fit, so the CB threads of a row read them from
-    // LDS instead of each loading the row from L2 (MDP_QROWS_ZLDS=1).
-    const bool zlds = (xcd & 2u) && kmax && (size_t)nrows * kmax <= (size_t)nitems * CB;  // uniform
-    if (zlds) {
-        const double2 *src = (const double2 *)zsT;
-        double2 *dst = (double2 *)Pl;
-        const uint32_t n2 = nrows * kmax / 2;  // kmax is a multiple of 8
-        for (uint32_t i0 = threadIdx.x; i0 < n2; i0 += 4 * kQrowsBlock) {
-            double2 t[4];
-#pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) t[u] = src[min(i0 + u * kQrowsBlock, n2 - 1)];
-#pragma unroll
-            for (uint32_t u = 0; u < 4; ++u)
-                if (i0 + u * kQrowsBlock < n2) dst[i0 + u * kQrowsBlock] = t[u];
-        }
-        __syncthreads();
-    }
     for (uint32_t w = threadIdx.x; w < nrows * CB; w += kQrowsBlock) {
         const uint32_t cl = w % CB, r = w / CB;
         double c = cv[0];
 #pragma unroll
         for (int i = 1; i < CB; ++i) c = cl == (uint32_t)i ? cv[i] : c;
+        const double2 *zr = (const double2 *)(zsT + (size_t)r * kmax);
         double za = 1.0, zb = 1.0, zcc = 1.0, zd = 1.0;
         auto chunk = [&](const double *sk) {
             za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
@@ -436,37 +419,30 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
             zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
         };
         double first = 0.0;
-        // the row's products from either copy (LDS or global), same order
-        auto row = [&](const double2 *zr) {
-            uint32_t k = 0;
-            for (; k + 16 <= kmax; k += 16) {
-                double sk[16];
+        uint32_t k = 0;
+        for (; k + 16 <= kmax; k += 16) {
+            double sk[16];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const double2 t2 = zr[k / 2 + u];
-                    sk[2 * u] = t2.x;
-                    sk[2 * u + 1] = t2.y;
-                }
-                if (k == 0) first = sk[0];
-                chunk(sk);
-                chunk(sk + 8);
+            for (int u = 0; u < 8; ++u) {
+                const double2 t2 = zr[k / 2 + u];
+                sk[2 * u] = t2.x;
+                sk[2 * u + 1] = t2.y;
             }
-            if (k < kmax) {  // kmax is a multiple of 8
-                double sk[8];
+            if (k == 0) first = sk[0];
+            chunk(sk);
+            chunk(sk + 8);
+        }
+        if (k < kmax) {  // kmax is a multiple of 8
+            double sk[8];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const double2 t2 = zr[k / 2 + u];
-                    sk[2 * u] = t2.x;
-                    sk[2 * u + 1] = t2.y;
-                }
-                if (k == 0) first = sk[0];
-                chunk(sk);
+            for (int u = 0; u < 4; ++u) {
+                const double2 t2 = zr[k / 2 + u];
+                sk[2 * u] = t2.x;
+                sk[2 * u + 1] = t2.y;
             }
-        };
-        if (zlds)
-            row((const double2 *)(Pl + (size_t)r * kmax));
-        else
-            row((const double2 *)(zsT + (size_t)r * kmax));
+            if (k == 0) first = sk[0];
+            chunk(sk);
+        }
         double zz = (za * zb) * (zcc * zd);
         if (kmax && !(fma(-c, first, 1.0) > 0.0)) zz = 0.0;
         double zq[kZTermsDev];
@@ -1228,7 +1204,6 @@ struct mdp_engine {
     bool jit = false;         // forward kernel specialised with hipRTC (spom_jit.cpp)
     bool wide = false;        // wide path (k_witems + k_wq + k_fwd_wide): npmax > 16 or MDP_WIDE=1
     bool qrows_xcd = true;    // k_qrows deals c ranges XCD-aware (MDP_QROWS_XCD=0: blockIdx order)
-    bool qrows_zlds = false;  // k_qrows stages the rows' explicit columns in LDS (MDP_QROWS_ZLDS=1; default: read from L2)
     double wide_flops_pt = 0; // its FP64 flops per grid point
     int jit_epl = 1;          // its grid points per lane (Q-row reading variant and chunks)
     uint32_t jit_kblock = kBlock;  // its threads per column
@@ -2191,7 +2166,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
     MDP_LAUNCH((k_qrows<NV, EX, CB>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, eng->nvar, eng->nj,         \
                d.zs_kmax, d.zs, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
                (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1],                 \
-               (uint32_t)(eng->qrows_xcd ? 1u : 0u) | (eng->qrows_zlds ? 2u : 0u)); } while (0)
+               (uint32_t)(eng->qrows_xcd ? 1u : 0u)); } while (0)
         // c values per workgroup: <= qrows_maxcb(nvar) (register budget at 1024 threads)
         if (eng->nvar == 8) {
             if (cb == 4) MDP_QROWS_CB(8, true, 4);
@@ -2479,7 +2454,6 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
             if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
             if (const char *fv2 = getenv("MDP_JIT_EFAST")) plan.efast = atoi(fv2) != 0;
             if (const char *qx = getenv("MDP_QROWS_XCD")) eng->qrows_xcd = atoi(qx) != 0;
-            if (const char *qz = getenv("MDP_QROWS_ZLDS")) eng->qrows_zlds = atoi(qz) != 0;
             if (const char *ev = getenv("MDP_EPL")) {
                 plan.epl = atoi(ev);
                 eng->jit_shape_env = true;
