@@ -36,7 +36,7 @@ extern "C" {
 #define MDP_ENODEV (-5)       /* no usable GPU                             */
 #define MDP_EUNSUPPORTED (-6) /* problem outside the engine's limits       */
 
-#define MDP_ABI_VERSION 6
+#define MDP_ABI_VERSION 7
 
 /* ------------------------------------------------------------------ */
 /* Host model: parse + state enumeration (the reference's L2 layer)    */
@@ -87,6 +87,11 @@ double mdp_grid(uint32_t s, double lo, double hi, double *g);
 /* Ltot = 2 log(win) + log(sum_k sum_l w_k w_l exp(loglik[k][l])), trapezoid
  * weights 1/2 at the grid ends.  Replaces main_MIDASPOM.c:413-425. */
 double mdp_log_total(const double *loglik, uint32_t s, double win);
+/* Same on any s x s view: log L of (e row k, c column l) at loglik[k*se +
+ * l*sc] -- (s, 1) is the reference's lik[k][l], (1, s) the [c][e] layout the
+ * device engine writes fastest (MDP_LAYOUT_CE).  Same summation order, so the
+ * same bits (ABI 7). */
+double mdp_log_total_view(const double *loglik, uint32_t s, size_t se, size_t sc, double win);
 
 /* Posterior text file: "%.20lf\t" of exp(loglik-ltot) per cell, "\n" per row
  * (rows = e, columns = c).  Replaces main_MIDASPOM.c:427-436.  raw != 0
@@ -94,6 +99,11 @@ double mdp_log_total(const double *loglik, uint32_t s, double win);
  * main_MIDASPOM_MPI.c:527). */
 int mdp_write_posterior(const char *path, const double *loglik, uint32_t s, double ltot,
                         int raw);
+/* Same on the view loglik[i*se + j*sc] (row i = e, column j = c); the bytes
+ * written are the same as for the row-major matrix (ABI 7).  Memory held
+ * while writing is bounded (a few MB per host thread) whatever s is. */
+int mdp_write_posterior_view(const char *path, const double *loglik, uint32_t s, size_t se, size_t sc, double ltot,
+                             int raw);
 
 /* ------------------------------------------------------------------ */
 /* GPU likelihood engine (the reference's hot loop, L3 + L4 + L6)      */
@@ -108,6 +118,17 @@ typedef struct mdp_engine mdp_engine;
  * (per-point recomputation of S = piall*M moves here, once). */
 int mdp_engine_create(const mdp_problem *problem, const int *devices, int n_devices,
                       mdp_engine **out);
+
+/* Same with engine options (ABI 7): "NAME=VALUE" pairs separated by ';', ','
+ * or white space, selecting among the engine's parity-tested kernel variants
+ * (MDP_FUSED=0|1, MDP_WIDE=1, MDP_JIT_CHUNK=<uses>, ...).
+ * The library reads no tuning knob from the environment; mdp_engine_create
+ * is this call with options == NULL (the measured defaults).  Measurement-only
+ * options (MDP_DIAG, MDP_JIT_HACK, MDP_JIT_WPE) exist only in the diag build
+ * (libmidaspom_diag.so, -DMDP_DIAG_BUILD); elsewhere they, like any unknown
+ * name, return MDP_EINVAL. */
+int mdp_engine_create_opts(const mdp_problem *problem, const int *devices, int n_devices,
+                           const char *options, mdp_engine **out);
 
 void mdp_engine_destroy(mdp_engine *engine);
 
@@ -153,7 +174,7 @@ const char *mdp_engine_kernel_name(const mdp_engine *engine, int k);
 int mdp_engine_time_kernels(mdp_engine *engine, double *d_out, uint32_t ld_out, void *stream, int reps,
                             double *ms, int max_k);
 
-/* Diagnostics (MDP_DIAG=1 in the environment at engine creation): text
+/* Diagnostics (diag build, option MDP_DIAG=1 at engine creation): text
  * report of per-workgroup s_memtime phase durations (shader cycles) of the
  * last run's kernels; returns the report length (0 when disabled). */
 int mdp_engine_diag_report(mdp_engine *engine, char *buf, size_t len);
@@ -233,6 +254,10 @@ typedef struct mdp_scenario mdp_scenario;
  * Pc tables in LDS), larger n a kernel whose state vectors live in HBM. */
 int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, double d, int kind, int device,
                         mdp_scenario **out);
+/* Same with options (ABI 7): "MDP_SCN_BIG=1" / "MDP_SCN_ROW=1" force the
+ * HBM-state / row-parallel kernel for any n they support (tests). */
+int mdp_scenario_create_opts(const int32_t *row, uint32_t n, double m, float p, double d, int kind, int device,
+                             const char *options, mdp_scenario **out);
 void mdp_scenario_destroy(mdp_scenario *scenario);
 
 /* out[((ie*nc + ic)*nK + iK)*nd + id] = L(e, c, K[, dsrc]) =

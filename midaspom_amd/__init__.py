@@ -129,15 +129,19 @@ class Model:
 class Engine:
     """GPU likelihood engine (``mdp_engine``) over one or more devices."""
 
-    def __init__(self, model: Model, devices=None, n_devices: int | None = None):
+    def __init__(self, model: Model, devices=None, n_devices: int | None = None, options=None):
+        """options: engine options (dict or "K=V;..." string,
+        ``mdp_engine_create_opts``); None forwards the MDP_* variables set in
+        the environment (``_lib.options_string``)."""
         self.model = model  # keep the host tables alive
         h = ctypes.c_void_p()
+        opts = _lib.options_string(options)
         if devices is not None:
             arr = (ctypes.c_int * len(devices))(*devices)
-            rc = lib().mdp_engine_create(ctypes.byref(model.problem), arr, len(devices), ctypes.byref(h))
+            rc = lib().mdp_engine_create_opts(ctypes.byref(model.problem), arr, len(devices), opts, ctypes.byref(h))
         else:
-            rc = lib().mdp_engine_create(ctypes.byref(model.problem), None, int(n_devices or 0),
-                                         ctypes.byref(h))
+            rc = lib().mdp_engine_create_opts(ctypes.byref(model.problem), None, int(n_devices or 0), opts,
+                                              ctypes.byref(h))
         check(rc)
         self._h = h
 
@@ -203,7 +207,7 @@ class Engine:
         return {nm: buf[i] for i, nm in enumerate(names) if nm}
 
     def diag_report(self) -> str:
-        """Phase-stamp report of the last run (engine created with MDP_DIAG=1)."""
+        """Phase-stamp report of the last run (diag library, engine option MDP_DIAG=1)."""
         buf = ctypes.create_string_buffer(8192)
         check(lib().mdp_engine_diag_report(self._h, buf, len(buf)))
         return buf.value.decode()
@@ -247,18 +251,31 @@ def grid(s: int, lo: float = 0.0, hi: float = 1.0):
     return g, win
 
 
-def log_total(lik: np.ndarray, win: float) -> float:
-    """Trapezoid log normaliser (:413-425)."""
-    a = np.ascontiguousarray(lik, dtype=np.float64)
+def _view(lik: np.ndarray):
+    """(base array, se, sc) of an s x s float64 [e][c] matrix given as is or
+    as the transpose of a C-contiguous [c][e] array (lik = ce.T): the host
+    functions read either in place through mdp_*_view, no copy."""
+    a = np.asarray(lik)
     if a.ndim != 2 or a.shape[0] != a.shape[1]:
-        raise ValueError("log_total needs a square s x s grid")
-    return float(lib().mdp_log_total(_dptr(a), a.shape[0], float(win)))
+        raise ValueError("needs a square s x s grid")
+    if a.dtype == np.float64 and a.T.flags.c_contiguous and not a.flags.c_contiguous:
+        return a.T, 1, a.shape[0]
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.shape[0], 1
+
+
+def log_total(lik: np.ndarray, win: float) -> float:
+    """Trapezoid log normaliser (:413-425); lik may be an [e][c] array or the
+    transposed view of a [c][e] one."""
+    a, se, sc = _view(lik)
+    return float(lib().mdp_log_total_view(_dptr(a), a.shape[0], se, sc, float(win)))
 
 
 def write_posterior(path, lik: np.ndarray, ltot: float, raw: bool = False) -> None:
-    """Posterior text file, reference bit layout (:427-436)."""
-    a = np.ascontiguousarray(lik, dtype=np.float64)
-    check(lib().mdp_write_posterior(os.fsencode(str(path)), _dptr(a), a.shape[0], float(ltot), int(raw)))
+    """Posterior text file, reference bit layout (:427-436); lik as for log_total."""
+    a, se, sc = _view(lik)
+    check(lib().mdp_write_posterior_view(os.fsencode(str(path)), _dptr(a), a.shape[0], se, sc, float(ltot),
+                                         int(raw)))
 
 
 def posterior(lik: np.ndarray, ltot: float) -> np.ndarray:
@@ -310,14 +327,15 @@ class Scenario:
     main_MIDASPOM_loss.c) scenario."""
 
     def __init__(self, row, kind: str = "dieoff", m: float = 400.0, p: float = 0.5, d: float = 200.0,
-                 device: int = 0):
+                 device: int = 0, options=None):
         if kind not in ("dieoff", "loss"):
             raise ValueError("kind must be 'dieoff' or 'loss'")
         self.kind = kind
         row = np.ascontiguousarray(row, dtype=np.int32)
         h = ctypes.c_void_p()
-        check(lib().mdp_scenario_create(row.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row.size, m, p, d,
-                                        1 if kind == "loss" else 0, device, ctypes.byref(h)))
+        opts = _lib.options_string(options, _lib.SCENARIO_OPTION_NAMES)
+        check(lib().mdp_scenario_create_opts(row.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), row.size, m, p, d,
+                                             1 if kind == "loss" else 0, device, opts, ctypes.byref(h)))
         self._h = h
 
     def close(self):

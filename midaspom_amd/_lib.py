@@ -13,6 +13,10 @@ from pathlib import Path
 PKG_DIR = Path(__file__).resolve().parent
 BUILD_DIR = PKG_DIR / "_build"
 LIB_PATH = BUILD_DIR / "libmidaspom.so"
+# the measurement build (`make -C midaspom_amd/csrc diag`: phase stamps,
+# MDP_JIT_HACK); loaded instead of LIB_PATH only when MIDASPOM_DIAG_LIB=1,
+# which only scripts/ set -- the CLIs, tests and bench.py use LIB_PATH
+DIAG_LIB_PATH = BUILD_DIR / "libmidaspom_diag.so"
 CLI_PATH = BUILD_DIR / "midaspom"
 DIEOFF_CLI_PATH = BUILD_DIR / "midaspom_dieoff"
 LOSS_CLI_PATH = BUILD_DIR / "midaspom_loss"
@@ -93,8 +97,14 @@ SIGNATURES = [
     ("mdp_grid", ctypes.c_double, [c_u32, ctypes.c_double, ctypes.c_double, c_dbl_p]),
     ("mdp_log_total", ctypes.c_double, [c_dbl_p, c_u32, ctypes.c_double]),
     ("mdp_write_posterior", ctypes.c_int, [ctypes.c_char_p, c_dbl_p, c_u32, ctypes.c_double, ctypes.c_int]),
+    ("mdp_log_total_view", ctypes.c_double, [c_dbl_p, c_u32, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_double]),
+    ("mdp_write_posterior_view", ctypes.c_int,
+     [ctypes.c_char_p, c_dbl_p, c_u32, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_double, ctypes.c_int]),
     ("mdp_engine_create", ctypes.c_int,
      [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("mdp_engine_create_opts", ctypes.c_int,
+     [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_char_p,
+      ctypes.POINTER(ctypes.c_void_p)]),
     ("mdp_engine_destroy", None, [ctypes.c_void_p]),
     ("mdp_loglik_grid", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_u32, c_dbl_p, c_u32, c_dbl_p]),
     ("mdp_engine_set_grid", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_u32, c_dbl_p, c_u32]),
@@ -120,6 +130,9 @@ SIGNATURES = [
     ("mdp_scenario_create", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32, ctypes.c_double, ctypes.c_float, ctypes.c_double,
       ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("mdp_scenario_create_opts", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32, ctypes.c_double, ctypes.c_float, ctypes.c_double,
+      ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
     ("mdp_scenario_destroy", None, [ctypes.c_void_p]),
     ("mdp_scenario_lik", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, c_dbl_p, ctypes.c_uint32, c_dbl_p, ctypes.c_uint32, c_dbl_p,
@@ -160,11 +173,12 @@ def lib() -> ctypes.CDLL:
     """Load libmidaspom.so (once).  Raises if the HIP build is missing."""
     global _lib
     if _lib is None:
-        if not LIB_PATH.exists():
+        path = DIAG_LIB_PATH if os.environ.get("MIDASPOM_DIAG_LIB") == "1" else LIB_PATH
+        if not path.exists():
             raise RuntimeError(
-                f"{LIB_PATH} is missing: the HIP engine is not built "
+                f"{path} is missing: the HIP engine is not built "
                 "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
-        handle = ctypes.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | ctypes.RTLD_GLOBAL)
+        handle = ctypes.CDLL(str(path), mode=os.RTLD_NOW | ctypes.RTLD_GLOBAL)
         for name, res, args in SIGNATURES:
             fn = getattr(handle, name)
             fn.restype = res
@@ -178,3 +192,27 @@ def check(rc: int) -> int:
     if rc < 0:
         raise MidaspomError(rc, lib().mdp_last_error().decode(errors="replace"))
     return rc
+
+
+# Engine options (mdp_engine_create_opts).  The library reads
+# no environment; the Python layer forwards these variables, when set, as the
+# options of engines created without explicit ones -- the developer interface
+# the tests and scripts/ use to pin kernel variants against each other.
+ENGINE_OPTION_NAMES = (
+    "MDP_JIT", "MDP_FUSED", "MDP_FUSED_COLS", "MDP_EPL", "MDP_JIT_SLOTS", "MDP_JIT_WINDOW", "MDP_JIT_XCD",
+    "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
+    "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
+    "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE",
+    # measurement-only: accepted by the diag build alone
+    "MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE")
+SCENARIO_OPTION_NAMES = ("MDP_SCN_BIG", "MDP_SCN_ROW")
+
+
+def options_string(options=None, names=ENGINE_OPTION_NAMES) -> bytes | None:
+    """The options argument of mdp_*_create_opts: a dict or "K=V;..." string
+    as given, or (None) the MDP_* variables of `names` set in the environment."""
+    if options is None:
+        options = {k: os.environ[k] for k in names if k in os.environ}
+    if isinstance(options, dict):
+        options = ";".join(f"{k}={v}" for k, v in options.items())
+    return options.encode() if options else None

@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <new>
 #include <set>
 #include <string>
@@ -1190,6 +1191,71 @@ struct DevCtx {
 
 }  // namespace
 
+// Engine options (ABI 7, mdp_engine_create_opts): "NAME=VALUE" pairs
+// separated by ';', ',' or white space.  They select among the engine's
+// parity-tested kernel variants; the defaults are the
+// measured best.  The library reads no tuning knob from the environment:
+// mdp_engine_create is mdp_engine_create_opts with no options.  Names
+// marked measurement-only exist in the diag build alone (-DMDP_DIAG_BUILD,
+// libmidaspom_diag.so, used by scripts/): MDP_JIT_HACK's kernels do not
+// store correct results, and phase stamps / occupancy hints are profiling
+// aids.  An unknown name, or a measurement-only name in the default
+// build, is MDP_EINVAL.
+namespace {
+const char *const kEngineOptNames[] = {
+    "MDP_JIT", "MDP_FUSED", "MDP_FUSED_COLS", "MDP_EPL", "MDP_JIT_SLOTS", "MDP_JIT_WINDOW", "MDP_JIT_XCD",
+    "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
+    "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
+    "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE"};
+const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
+#ifdef MDP_DIAG_BUILD
+constexpr bool kDiagBuild = true;
+#else
+constexpr bool kDiagBuild = false;
+#endif
+}  // namespace
+
+struct EngineOpts {
+    std::map<std::string, std::string> kv;
+    const char *get(const char *name) const
+    {
+        auto it = kv.find(name);
+        return it == kv.end() ? nullptr : it->second.c_str();
+    }
+};
+
+static int parse_engine_opts(const char *s, EngineOpts &o)
+{
+    o.kv.clear();
+    if (!s) return MDP_OK;
+    std::string cur;
+    auto flush = [&]() -> int {
+        if (cur.empty()) return MDP_OK;
+        const size_t eq = cur.find('=');
+        const std::string k = cur.substr(0, eq), v = eq == std::string::npos ? std::string("1") : cur.substr(eq + 1);
+        cur.clear();
+        bool known = false, diag = false;
+        for (const char *n : kEngineOptNames) known |= k == n;
+        for (const char *n : kDiagOptNames) diag |= k == n;
+        if (diag && !kDiagBuild)
+            return mdp_set_error(MDP_EINVAL, "option %s is measurement-only (libmidaspom_diag.so, -DMDP_DIAG_BUILD)",
+                                 k.c_str());
+        if (!known && !diag) return mdp_set_error(MDP_EINVAL, "unknown engine option '%s'", k.c_str());
+        o.kv[k] = v;
+        return MDP_OK;
+    };
+    for (const char *c = s;; ++c) {
+        if (*c == 0 || *c == ';' || *c == ',' || *c == ' ' || *c == '\t' || *c == '\n') {
+            const int rc = flush();
+            if (rc) return rc;
+            if (*c == 0) break;
+        } else {
+            cur += *c;
+        }
+    }
+    return MDP_OK;
+}
+
 struct mdp_engine {
     uint32_t n = 0, tmax = 0, nvar = 0, nstates = 0, nextid = 0;
     uint32_t npairs = 0, nuses = 0, ncoef = 0, npmax = 1, variant = 0;
@@ -1217,6 +1283,8 @@ struct mdp_engine {
     double jit_flops_pt = 0;  // its FP64 flops per grid point (counted by the generator)
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
     std::vector<char> jit_code[2];  // forward kernel code objects [fused], compiled on demand
+    std::string jit_src[2];         // their sources (a cached object the runtime refuses is rebuilt)
+    std::vector<std::string> chunk_src;
     std::vector<MdpJitPlan> chunks;               // > 1: the series runs as chunks of years
     std::vector<std::vector<char>> chunk_code;    // their code objects
     bool qglobal = false;     // Q rows built by k_zrows + k_witems + k_wq (k_qrows' tables exceed the LDS)
@@ -1236,7 +1304,9 @@ struct mdp_engine {
     double prior0 = 1.0;
     std::vector<uint32_t> np, pairA, pairB, pairOff, use_pair, prog, udesc, pairPart0, partP, partK0;
     std::vector<DevCtx> devs;
-    mutable std::set<std::string> launched;  // kernel instantiations launched so far (mdp_engine_launched)
+    EngineOpts opts;          // mdp_engine_create_opts (variant selection; no environment reads)
+    mutable std::set<std::string, std::less<>> launched;  // kernel instantiations launched so far (mdp_engine_launched)
+    mutable std::mutex launched_mu;                         // engines may be driven from several host threads
     int profiling = 0;
     double last_ms[3] = {0, 0, 0};  // mean per run over the last collected runs
     int nlast = 0;
@@ -1245,17 +1315,21 @@ struct mdp_engine {
 
 namespace {
 
-// record a launched kernel instantiation ("k_qrows<16,0,2>", ...)
-// the forward kernels' output strides for mdp_engine_run's ld: log L of
-// point (ie, ic) at out[ie * se + ic * sc] -- [e][c] rows (se = ld, sc = 1)
-// or [c][e] columns (se = 1, sc = ld); every forward kernel takes both
-inline void out_strides(const mdp_engine *eng, uint32_t ld, uint32_t &se, uint32_t &sc)
+// The forward kernels' output strides: log L of point (ie, ic) at
+// out[ie * se + ic * sc] -- [e][c] rows (se = ld, sc = 1) or [c][e] columns
+// (se = 1, sc = ld); every forward kernel takes both.  Passed explicitly down
+// every launch path: only mdp_engine_run / mdp_engine_time_kernels honour the
+// engine's layout (mdp_engine_set_layout); mdp_loglik_grid always fills its
+// device slab in [e][c] (its host contract).
+struct OutStrides {
+    uint32_t se, sc;
+};
+inline OutStrides layout_strides(int layout, uint32_t ld)
 {
-    const bool ce = eng->layout == MDP_LAYOUT_CE;
-    se = ce ? 1u : ld;
-    sc = ce ? ld : 1u;
+    return layout == MDP_LAYOUT_CE ? OutStrides{1u, ld} : OutStrides{ld, 1u};
 }
 
+// record a launched kernel instantiation ("k_qrows<16,0,2>", ...)
 void note_launch(const mdp_engine *eng, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 void note_launch(const mdp_engine *eng, const char *fmt, ...)
 {
@@ -1264,7 +1338,10 @@ void note_launch(const mdp_engine *eng, const char *fmt, ...)
     va_start(ap, fmt);
     vsnprintf(b, sizeof b, fmt, ap);
     va_end(ap);
-    eng->launched.emplace(b);
+    // look up before inserting: the hot path re-launches the same kernels, so
+    // after the first launch of each this allocates nothing
+    std::lock_guard<std::mutex> lk(eng->launched_mu);
+    if (eng->launched.find(b) == eng->launched.end()) eng->launched.emplace(b);
 }
 
 constexpr int kDegBuckets[] = {4, 8, 16, 24};
@@ -1299,7 +1376,7 @@ int build_plan(mdp_engine *eng, const mdp_problem *p)
         return mdp_set_error(MDP_EUNSUPPORTED, "%u variable columns (engine limit 24)", p->nvar);
     eng->nstates = 1u << p->nvar;
     eng->prior0 = (double)p->prior[0];
-    if (const char *wv = getenv("MDP_WIDE")) eng->wide = atoi(wv) != 0;
+    if (const char *wv = eng->opts.get("MDP_WIDE")) eng->wide = atoi(wv) != 0;
     eng->np.resize(p->tmax);
     eng->npmax = 1;
     for (uint32_t t = 0; t < p->tmax; ++t) {
@@ -1659,7 +1736,7 @@ int jit_build(mdp_engine *eng, bool fused)
         eng->jit_kblock_fused = (uint32_t)plan.kblock;
     }
     eng->jit_flops_pt = plan.flops_pt;
-    if (const char *dump = getenv("MDP_JIT_DUMP")) {  // <path>.hip (reading) / <path>.fused.hip
+    if (const char *dump = eng->opts.get("MDP_JIT_DUMP")) {  // <path>.hip (reading) / <path>.fused.hip
         if (FILE *f = fopen((std::string(dump) + (fused ? ".fused.hip" : ".hip")).c_str(), "w")) {
             fputs(src.c_str(), f);
             fclose(f);
@@ -1668,6 +1745,7 @@ int jit_build(mdp_engine *eng, bool fused)
     if (mdp_jit_compile(src, eng->jit_code[fused], eng->jit_log) != 0)
         return mdp_set_error(MDP_EHIP, "hipRTC compilation of the forward kernel failed: %s",
                              eng->jit_log.c_str());
+    eng->jit_src[fused] = src;
     return MDP_OK;
 }
 
@@ -1685,7 +1763,7 @@ int jit_build_chunks(mdp_engine *eng)
     for (size_t i = 0; i < nch; ++i) {
         srcs[i] = mdp_jit_forward_source(eng->chunks[i]);
         flops += eng->chunks[i].flops_pt;
-        if (const char *dump = getenv("MDP_JIT_DUMP"))
+        if (const char *dump = eng->opts.get("MDP_JIT_DUMP"))
             if (FILE *f = fopen((std::string(dump) + ".chunk" + std::to_string(i) + ".hip").c_str(), "w")) {
                 fputs(srcs[i].c_str(), f);
                 fclose(f);
@@ -1694,8 +1772,8 @@ int jit_build_chunks(mdp_engine *eng)
     {
         std::vector<std::thread> th;
         size_t nt = std::min<size_t>(8, nch);
-        if (const char *tv = getenv("MDP_JIT_THREADS")) nt = std::max<size_t>(1, std::min<size_t>(nch, atoi(tv)));
-        const bool verbose = getenv("MDP_JIT_VERBOSE") != nullptr;
+        if (const char *tv = eng->opts.get("MDP_JIT_THREADS")) nt = std::max<size_t>(1, std::min<size_t>(nch, atoi(tv)));
+        const bool verbose = eng->opts.get("MDP_JIT_VERBOSE") != nullptr;
         for (size_t t = 0; t < nt; ++t)
             th.emplace_back([&, t]() {
                 for (size_t i = t; i < nch; i += nt) {
@@ -1714,39 +1792,83 @@ int jit_build_chunks(mdp_engine *eng)
             return mdp_set_error(MDP_EHIP, "hipRTC compilation of forward chunk %zu failed: %s", i, logs[i].c_str());
         }
     eng->chunk_code = std::move(code);
+    eng->chunk_src = std::move(srcs);
     eng->jit_epl = eng->chunks[0].epl;
     eng->jit_kblock = (uint32_t)eng->chunks[0].kblock;
     eng->jit_flops_pt = flops;
     return MDP_OK;
 }
 
+// Load a code object; if the runtime refuses it (a stale or foreign object
+// from the disk cache), rebuild it from its source once and retry.
+hipError_t load_module(std::vector<char> &code, const std::string &src, hipModule_t *m)
+{
+    hipError_t e = hipModuleLoadData(m, code.data());
+    if (e == hipSuccess || src.empty()) return e;
+    std::string log;
+    if (mdp_jit_compile(src, code, log, true) != 0) return e;
+    return hipModuleLoadData(m, code.data());
+}
+
 // Load a forward kernel variant into the device (compiling it if needed).
 int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 {
     if (!eng->chunks.empty()) {  // a long series: its chunk kernels (never fused)
-        if (!d.cfn.empty()) return MDP_OK;
+        const size_t nch = eng->chunks.size();
+        if (d.cfn.size() == nch) return MDP_OK;
         int rc = jit_build_chunks(eng);
         if (rc) return rc;
         HIP_TRY(hipSetDevice(d.device));
-        for (size_t i = 0; i < eng->chunks.size(); ++i) {
+        // every chunk loads into locals first and is committed to the device
+        // context only when all have: a failure part-way leaves nothing
+        // loaded, so a later call retries instead of running some chunks
+        std::vector<hipModule_t> mods;
+        std::vector<hipFunction_t> fns;
+        std::vector<uint32_t *> qidx;
+        auto unload = [&]() {
+            for (hipModule_t m : mods) (void)hipModuleUnload(m);
+            for (uint32_t *q : qidx)
+                if (q) (void)hipFree(q);
+        };
+        for (size_t i = 0; i < nch; ++i) {
             hipModule_t m;
             hipFunction_t f;
-            HIP_TRY(hipModuleLoadData(&m, eng->chunk_code[i].data()));
-            d.cmod.push_back(m);
-            HIP_TRY(hipModuleGetFunction(&f, m, "mdp_fwd_jit"));
-            d.cfn.push_back(f);
+            hipError_t e = load_module(eng->chunk_code[i], i < eng->chunk_src.size() ? eng->chunk_src[i] : std::string(), &m);
+            if (e == hipSuccess) {
+                mods.push_back(m);
+                e = hipModuleGetFunction(&f, m, "mdp_fwd_jit");
+            }
+            if (e != hipSuccess) {
+                unload();
+                return mdp_set_error(MDP_EHIP, "loading forward chunk %zu failed: %s", i, hipGetErrorString(e));
+            }
+            fns.push_back(f);
             uint32_t *qi = nullptr;
-            if (!eng->chunks[i].qidx.empty() && (rc = dev_upload(&qi, eng->chunks[i].qidx))) return rc;
-            d.cqidx.push_back(qi);
+            if (!eng->chunks[i].qidx.empty() && (rc = dev_upload(&qi, eng->chunks[i].qidx))) {
+                unload();
+                return rc;
+            }
+            qidx.push_back(qi);
         }
+        d.cmod = std::move(mods);
+        d.cfn = std::move(fns);
+        d.cqidx = std::move(qidx);
         return MDP_OK;
     }
     if (d.jit_fn[fused]) return MDP_OK;
     int rc = jit_build(eng, fused);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(d.device));
-    HIP_TRY(hipModuleLoadData(&d.jit_mod[fused], eng->jit_code[fused].data()));
-    HIP_TRY(hipModuleGetFunction(&d.jit_fn[fused], d.jit_mod[fused], "mdp_fwd_jit"));
+    hipModule_t m = nullptr;
+    hipFunction_t f = nullptr;
+    HIP_TRY(load_module(eng->jit_code[fused], eng->jit_src[fused], &m));
+    const hipError_t e = hipModuleGetFunction(&f, m, "mdp_fwd_jit");
+    if (e != hipSuccess) {
+        (void)hipModuleUnload(m);
+        return mdp_set_error(MDP_EHIP, "hipModuleGetFunction(mdp_fwd_jit) failed: %s", hipGetErrorString(e));
+    }
+    d.jit_mod[fused] = m;
+    d.jit_fn[fused] = f;
     return MDP_OK;
 }
 
@@ -1904,7 +2026,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         // c values per k_witems launch: item factors within kWidePgBytes
         const size_t cap_c = std::max<size_t>(1, std::min<size_t>(nc, 65535));
         d.wide_cb_items = (uint32_t)std::min(cap_c, std::max<size_t>(1, kWidePgBytes / 8 / std::max<size_t>(1, eng->nitems)));
-        if (const char *cv = getenv("MDP_WIDE_CB"))  // tests: force several launches per slot
+        if (const char *cv = eng->opts.get("MDP_WIDE_CB"))  // tests: force several launches per slot
             d.wide_cb_items = std::min(d.wide_cb_items, (uint32_t)std::max(1, atoi(cv)));
         if ((rc = dev_reserve(&d.Pg, &d.cap_pg, (size_t)d.wide_cb_items * eng->nitems + 1))) return rc;
     }
@@ -1914,7 +2036,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         const size_t ne_pad = (size_t)std::max<uint32_t>(1u, (ne + kBlock - 1) / kBlock) * kBlock;
         const size_t cap_c = std::max<size_t>(1, std::min<size_t>(nc, 65535));
         d.wide_cb_fwd = (uint32_t)std::min(cap_c, std::max<size_t>(1, kWideVBytes / 8 / (2 * (size_t)eng->npmax * ne_pad)));
-        if (const char *cv = getenv("MDP_WIDE_CB"))
+        if (const char *cv = eng->opts.get("MDP_WIDE_CB"))
             d.wide_cb_fwd = std::min(d.wide_cb_fwd, (uint32_t)std::max(1, atoi(cv)));
         if ((rc = dev_reserve(&d.V, &d.cap_v, 2 * (size_t)eng->npmax * d.wide_cb_fwd * ne_pad))) return rc;
     } else if (eng->jit) {
@@ -1961,10 +2083,9 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
 }
 
 template <int NP, int DEG, int EPL>
-void launch_fwd_epl(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
+void launch_fwd_epl(const mdp_engine *eng, const DevCtx &d, double *out, OutStrides os, hipStream_t s)
 {
-    uint32_t se, sc;
-    out_strides(eng, ld, se, sc);
+    uint32_t se = os.se, sc = os.sc;
     dim3 grid(d.nc, (d.ne + kBlock * EPL - 1) / (kBlock * EPL));
     const uint32_t nprog = (uint32_t)eng->prog.size() - 1;
     note_launch(eng, "%s<%d,%d,%d>", eng->fwd_lds ? "k_forward_lds" : "k_forward", NP, DEG, EPL);
@@ -1978,29 +2099,29 @@ void launch_fwd_epl(const mdp_engine *eng, const DevCtx &d, double *out, uint32_
 }
 
 template <int NP, int DEG>
-void launch_fwd(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
+void launch_fwd(const mdp_engine *eng, const DevCtx &d, double *out, OutStrides os, hipStream_t s)
 {
     if constexpr (NP <= 4 && DEG <= 8) {
-        if (eng->epl == 1) return launch_fwd_epl<NP, DEG, 1>(eng, d, out, ld, s);
-        if (eng->epl == 4) return launch_fwd_epl<NP, DEG, 4>(eng, d, out, ld, s);
+        if (eng->epl == 1) return launch_fwd_epl<NP, DEG, 1>(eng, d, out, os, s);
+        if (eng->epl == 4) return launch_fwd_epl<NP, DEG, 4>(eng, d, out, os, s);
     }
-    launch_fwd_epl<NP, DEG, kEPL>(eng, d, out, ld, s);
+    launch_fwd_epl<NP, DEG, kEPL>(eng, d, out, os, s);
 }
 
 template <int NP>
-int launch_fwd_deg(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
+int launch_fwd_deg(const mdp_engine *eng, const DevCtx &d, double *out, OutStrides os, hipStream_t s)
 {
     switch (eng->deg) {
-    case 4: launch_fwd<NP, 4>(eng, d, out, ld, s); break;
-    case 8: launch_fwd<NP, 8>(eng, d, out, ld, s); break;
-    case 16: launch_fwd<NP, 16>(eng, d, out, ld, s); break;
-    case 24: launch_fwd<NP, 24>(eng, d, out, ld, s); break;
+    case 4: launch_fwd<NP, 4>(eng, d, out, os, s); break;
+    case 8: launch_fwd<NP, 8>(eng, d, out, os, s); break;
+    case 16: launch_fwd<NP, 16>(eng, d, out, os, s); break;
+    case 24: launch_fwd<NP, 24>(eng, d, out, os, s); break;
     default: return mdp_set_error(MDP_EUNSUPPORTED, "no forward kernel for degree %u", eng->deg);
     }
     return MDP_OK;
 }
 
-int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t ld, hipStream_t s)
+int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, OutStrides os, hipStream_t s)
 {
     int rc;
     if (eng->jit) {
@@ -2014,8 +2135,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
         double *vscr = d.vscr;
         uint32_t ldv = d.ldv;
         const uint32_t *qidx = nullptr;
-        uint32_t se, sc;
-        out_strides(eng, ld, se, sc);
+        uint32_t se = os.se, sc = os.sc;
         void *args[] = {(void *)&Qrow, (void *)&prior0, (void *)&ev,  (void *)&ne,   (void *)&nc,
                         (void *)&out,  (void *)&se,     (void *)&one, (void *)&st,   (void *)&cv,
                         (void *)&ctab, (void *)&ctl,    (void *)&kmax, (void *)&vscr, (void *)&ldv,
@@ -2032,6 +2152,8 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
             return mdp_set_error(MDP_EUNSUPPORTED, "grid %u x %u too large", d.ne, d.nc);
         if (!eng->chunks.empty()) {  // a long series: its chunks in order on the stream
             const size_t nch = d.cfn.size();
+            if (nch != eng->chunks.size() || d.cqidx.size() != nch)
+                return mdp_set_error(MDP_EHIP, "forward chunks not loaded (%zu of %zu)", nch, eng->chunks.size());
             for (size_t i = 0; i < nch; ++i) {
                 qidx = d.cqidx[i];
                 HIP_TRY(hipExtModuleLaunchKernel(d.cfn[i], (uint32_t)(nb * kb * spl), 1, 1, kb * spl, 1, 1, 0, s, args,
@@ -2050,11 +2172,11 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, uint32_t
         return MDP_OK;
     }
     switch (eng->variant / 100) {
-    case 1: rc = launch_fwd_deg<1>(eng, d, out, ld, s); break;
-    case 2: rc = launch_fwd_deg<2>(eng, d, out, ld, s); break;
-    case 4: rc = launch_fwd_deg<4>(eng, d, out, ld, s); break;
-    case 8: rc = launch_fwd_deg<8>(eng, d, out, ld, s); break;
-    case 16: rc = launch_fwd_deg<16>(eng, d, out, ld, s); break;
+    case 1: rc = launch_fwd_deg<1>(eng, d, out, os, s); break;
+    case 2: rc = launch_fwd_deg<2>(eng, d, out, os, s); break;
+    case 4: rc = launch_fwd_deg<4>(eng, d, out, os, s); break;
+    case 8: rc = launch_fwd_deg<8>(eng, d, out, os, s); break;
+    case 16: rc = launch_fwd_deg<16>(eng, d, out, os, s); break;
     default: return mdp_set_error(MDP_EUNSUPPORTED, "no forward kernel variant %u", eng->variant);
     }
     if (rc) return rc;
@@ -2093,7 +2215,7 @@ int launch_coefs(const mdp_engine *eng, const DevCtx &d, hipStream_t s)
 // Wide path, slot 1 (k_witems + k_wq per chunk of c values) or slot 2
 // (k_fwd_wide per chunk).  A profiled run times the slot as a whole: events
 // recorded around its launches.
-int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, uint32_t ld, hipStream_t s)
+int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutStrides os, hipStream_t s)
 {
     const KernelEvents ev = t_kev;
     t_kev = KernelEvents{};
@@ -2117,8 +2239,7 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, uint
         }
     } else {
         const uint32_t cb = d.wide_cb_fwd;
-        uint32_t se, sc;
-        out_strides(eng, ld, se, sc);
+        uint32_t se = os.se, sc = os.sc;
         for (uint32_t c0 = 0; c0 < d.nc; c0 += cb) {
             const uint32_t n = std::min(cb, d.nc - c0);
             const dim3 g((d.ne + kBlock - 1) / kBlock, n);
@@ -2142,11 +2263,11 @@ bool slot_active(const mdp_engine *eng, const DevCtx &d, int k)
     return k != 1 || eng->nuses;
 }
 
-int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hipStream_t s)
+int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, OutStrides os, hipStream_t s)
 {
     if (!slot_active(eng, d, k)) return MDP_OK;
-    if ((eng->wide && k > 0) || (eng->jit && eng->qglobal && k == 1)) return launch_wide(eng, d, k, out, ld, s);
-    if (k == 2) return launch_forward(eng, d, out, ld, s);
+    if ((eng->wide && k > 0) || (eng->jit && eng->qglobal && k == 1)) return launch_wide(eng, d, k, out, os, s);
+    if (k == 2) return launch_forward(eng, d, out, os, s);
     if ((eng->jit || eng->wide) && k == 0) {  // Z rows
         const uint32_t kmax = d.zs_kmax;
         const dim3 grid((d.nc + 64 * kZC - 1) / (64 * kZC), (eng->nj + kZRows - 1) / kZRows);
@@ -2197,7 +2318,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, uint32_t ld, hip
     return launch_coefs(eng, d, s);
 }
 
-int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
+int run_dev(mdp_engine *eng, DevCtx &d, double *out, OutStrides os, hipStream_t s)
 {
     HIP_TRY(hipSetDevice(d.device));
     if (d.ne == 0 || d.nc == 0) return MDP_OK;
@@ -2226,7 +2347,7 @@ int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
         // only launched kernels carry events (no marker packets between kernels)
         t_kev = prof ? KernelEvents{ev[2 * k], ev[2 * k + 1]} : KernelEvents{};
         if (prof) d.ev_mask.back() |= (uint8_t)(1u << k);
-        int rc = launch_slot(eng, d, k, out, ld, s);
+        int rc = launch_slot(eng, d, k, out, os, s);
         if (rc) return rc;
     }
     return MDP_OK;
@@ -2235,9 +2356,9 @@ int run_dev(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s)
 // Mean duration of each kernel of the run: one full run, then every kernel
 // launched `reps` times back to back between two events on the stream (no
 // per-launch events, so the figure is the kernel's own, as rocprofv3 sees it).
-int time_kernels(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream_t s, int reps, double *ms)
+int time_kernels(mdp_engine *eng, DevCtx &d, double *out, OutStrides os, hipStream_t s, int reps, double *ms)
 {
-    int rc = run_dev(eng, d, out, ld, s);
+    int rc = run_dev(eng, d, out, os, s);
     if (rc) return rc;
     hipEvent_t a, b;
     HIP_TRY(hipEventCreate(&a));
@@ -2245,9 +2366,9 @@ int time_kernels(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream
     for (int k = 0; k < 3; ++k) {
         ms[k] = 0.0;
         if (!slot_active(eng, d, k)) continue;
-        if ((rc = launch_slot(eng, d, k, out, ld, s))) break;  // warm
+        if ((rc = launch_slot(eng, d, k, out, os, s))) break;  // warm
         (void)hipEventRecord(a, s);
-        for (int r = 0; r < reps && !rc; ++r) rc = launch_slot(eng, d, k, out, ld, s);
+        for (int r = 0; r < reps && !rc; ++r) rc = launch_slot(eng, d, k, out, os, s);
         (void)hipEventRecord(b, s);
         if (rc) break;
         float t = 0;
@@ -2256,7 +2377,7 @@ int time_kernels(mdp_engine *eng, DevCtx &d, double *out, uint32_t ld, hipStream
         ms[k] = t / reps;
     }
     // leave the output as a full run computes it
-    if (!rc) rc = run_dev(eng, d, out, ld, s);
+    if (!rc) rc = run_dev(eng, d, out, os, s);
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     return rc;
@@ -2364,8 +2485,16 @@ extern "C" {
 
 int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, mdp_engine **out)
 {
+    return mdp_engine_create_opts(p, devices, n_devices, nullptr, out);
+}
+
+int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devices, const char *options,
+                           mdp_engine **out)
+{
     if (!p || !out || n_devices < 0) return mdp_set_error(MDP_EINVAL, "null argument");
     *out = nullptr;
+    EngineOpts opts;
+    if (int orc = parse_engine_opts(options, opts)) return orc;
     if (p->n == 0 || p->tmax == 0 || !p->M || !p->year_off || !p->year_ids || !p->prior ||
         !p->short_state || (p->nvar && !p->var_cols))
         return mdp_set_error(MDP_EINVAL, "incomplete problem description");
@@ -2373,7 +2502,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
     // MDP_JIT_CHECK=1 without a device: plan and compile both forward
     // variants (hipRTC runs offline), then report MDP_ENODEV -- the CPU
     // test that the generated sources compile for gfx950
-    const char *jcheck = getenv("MDP_JIT_CHECK");
+    const char *jcheck = opts.get("MDP_JIT_CHECK");
     const bool jit_check = jcheck && atoi(jcheck) != 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         ndev = 0;
@@ -2381,6 +2510,7 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
     }
     mdp_engine *eng = new (std::nothrow) mdp_engine();
     if (!eng) return mdp_set_error(MDP_ENOMEM, "out of host memory");
+    eng->opts = std::move(opts);
     int rc = build_plan(eng, p);
     if (rc) {
         delete eng;
@@ -2388,24 +2518,24 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
     }
     eng->fwd_lds_bytes = ldR_of(eng) * sizeof(double) + (eng->prog.size() + 1) * sizeof(uint32_t);
     eng->fwd_lds = eng->fwd_lds_bytes <= kFwdLds;
-    if (const char *ev = getenv("MDP_FWD"))
+    if (const char *ev = eng->opts.get("MDP_FWD"))
         if (!strcmp(ev, "scalar")) eng->fwd_lds = false;
-    if (const char *ev = getenv("MDP_EPL")) {
+    if (const char *ev = eng->opts.get("MDP_EPL")) {
         const int v = atoi(ev);
         if (v == 1 || v == 2 || v == 4) eng->epl = v;
     }
-    if (const char *ev = getenv("MDP_DIAG")) eng->diag = atoi(ev) != 0;
+    if (const char *ev = eng->opts.get("MDP_DIAG")) eng->diag = atoi(ev) != 0;
     {
-        const char *jv = getenv("MDP_JIT");
+        const char *jv = eng->opts.get("MDP_JIT");
         const bool jit_off = jv && !strcmp(jv, "0");
         // years of 17-64 states: the specialised forward kernel with its
         // state vectors in LDS (plan.vlds), unless the series is so long that
         // hipRTC would take minutes; MDP_WIDE=1 forces the wide kernels
-        const char *wv0 = getenv("MDP_WIDE");
+        const char *wv0 = eng->opts.get("MDP_WIDE");
         const bool wide_forced = wv0 && atoi(wv0) != 0;
         bool vlds = false;
         uint32_t vlds_max_uses = kVldsMaxUses;
-        if (const char *mv = getenv("MDP_VLDS_MAXUSES")) vlds_max_uses = (uint32_t)std::max(0, atoi(mv));
+        if (const char *mv = eng->opts.get("MDP_VLDS_MAXUSES")) vlds_max_uses = (uint32_t)std::max(0, atoi(mv));
         const uint32_t vkb = kBlock;  // points per workgroup (their states: npmax x vkb doubles of LDS)
         if (eng->wide && !wide_forced && !jit_off && eng->npmax <= kVldsMaxStates && eng->nuses <= vlds_max_uses) {
             eng->wide = false;
@@ -2415,15 +2545,15 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
         bool want_jit = want && build_direct_plan(eng, p) == MDP_OK;
         // k_qrows keeps every table of its c values in LDS; larger problems
         // build their Q rows in HBM (k_zrows + k_witems + k_wq, the same bits)
-        const char *qg = getenv("MDP_QGLOBAL");
+        const char *qg = eng->opts.get("MDP_QGLOBAL");
         eng->qglobal = want_jit && (qrows_lds(eng, 1) > kQrowsLdsMax || (qg && atoi(qg) != 0));
         eng->ldQ = ((size_t)eng->ncoef_d + 1) & ~(size_t)1;
         // a series longer than kJitMaxUses uses (or a Q row past the LDS) runs
         // as chunks of years (MDP_JIT_CHUNK / MDP_JIT_GATHER force them)
         uint32_t chunk_uses = kJitChunkUses;
-        const char *cv = getenv("MDP_JIT_CHUNK");
+        const char *cv = eng->opts.get("MDP_JIT_CHUNK");
         if (cv) chunk_uses = (uint32_t)std::max(1, atoi(cv));
-        const char *gv = getenv("MDP_JIT_GATHER");
+        const char *gv = eng->opts.get("MDP_JIT_GATHER");
         // coefficients a forward kernel may stage: what the LDS leaves beside
         // the wide years' state vectors (npmax x 256 lanes) when they are there
         const size_t qlimit = vlds ? std::min(kJitChunkQ, (kQrowsLdsMax - (size_t)eng->npmax * vkb * sizeof(double) -
@@ -2437,35 +2567,33 @@ int mdp_engine_create(const mdp_problem *p, const int *devices, int n_devices, m
                 plan.vlds = true;
                 // points per lane: 1, or 2 (MDP_VLDS_EPL=2: 128 lanes per wave
                 // group, each Q read shared by two points)
-                const char *ve = getenv("MDP_VLDS_EPL");
+                const char *ve = eng->opts.get("MDP_VLDS_EPL");
                 plan.epl = ve && atoi(ve) == 2 ? 2 : 1;
                 plan.kblock = (int)vkb / plan.epl;
                 plan.window = 16;
                 eng->fused_mode = 0;
-                if (const char *sv = getenv("MDP_VSPLIT")) plan.vsplit = atoi(sv) == 1 ? 1 : atoi(sv) == 2 ? 2 : 4;
+                if (const char *sv = eng->opts.get("MDP_VSPLIT")) plan.vsplit = atoi(sv) == 1 ? 1 : atoi(sv) == 2 ? 2 : 4;
             }
             plan.np = eng->np;
             plan.udesc = eng->udesc_d;
             plan.ldQ = eng->ldQ;
             plan.diag = eng->diag;
-            if (const char *cv = getenv("MDP_JIT_SLOTS")) plan.slots = atoi(cv);
-            if (const char *cv = getenv("MDP_JIT_DPPQ")) plan.dppq = std::max(0, std::min(2, atoi(cv)));
-            if (const char *wv = getenv("MDP_JIT_WPE")) plan.wpe = atoi(wv);
-            if (const char *xv = getenv("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
-            if (const char *fv2 = getenv("MDP_JIT_EFAST")) plan.efast = atoi(fv2) != 0;
-            if (const char *qx = getenv("MDP_QROWS_XCD")) eng->qrows_xcd = atoi(qx) != 0;
-            if (const char *ev = getenv("MDP_EPL")) {
+            if (const char *cv = eng->opts.get("MDP_JIT_SLOTS")) plan.slots = atoi(cv);
+            if (const char *wv = eng->opts.get("MDP_JIT_WPE")) plan.wpe = atoi(wv);
+            if (const char *xv = eng->opts.get("MDP_JIT_XCD")) plan.xcd = atoi(xv) != 0;
+            if (const char *fv2 = eng->opts.get("MDP_JIT_EFAST")) plan.efast = atoi(fv2) != 0;
+            if (const char *qx = eng->opts.get("MDP_QROWS_XCD")) eng->qrows_xcd = atoi(qx) != 0;
+            if (const char *ev = eng->opts.get("MDP_EPL")) {
                 plan.epl = atoi(ev);
                 eng->jit_shape_env = true;
             }
-            if (const char *wv = getenv("MDP_JIT_WINDOW")) plan.window = atoi(wv);
+            if (const char *wv = eng->opts.get("MDP_JIT_WINDOW")) plan.window = atoi(wv);
             // compile the variant a small grid uses now (the other on demand)
-            if (const char *fv = getenv("MDP_FUSED")) eng->fused_mode = atoi(fv) != 0;
-            if (const char *cv = getenv("MDP_FUSED_COLS")) plan.fused_cols = std::max(1, std::min(4, atoi(cv)));
-            if (const char *cv = getenv("MDP_JIT_HACK")) plan.hack = atoi(cv);
-            if (const char *cv = getenv("MDP_FAST_LOG")) plan.fast_log = atoi(cv) != 0;
-            if (const char *cv = getenv("MDP_JIT_SQ")) plan.sq = atoi(cv) != 0;
-            if (const char *cv = getenv("MDP_JIT_KBLOCK"); cv && !vlds) {
+            if (const char *fv = eng->opts.get("MDP_FUSED")) eng->fused_mode = atoi(fv) != 0;
+            if (const char *cv = eng->opts.get("MDP_FUSED_COLS")) plan.fused_cols = std::max(1, std::min(4, atoi(cv)));
+            if (const char *cv = eng->opts.get("MDP_JIT_HACK")) plan.hack = atoi(cv);
+            if (const char *cv = eng->opts.get("MDP_FAST_LOG")) plan.fast_log = atoi(cv) != 0;
+            if (const char *cv = eng->opts.get("MDP_JIT_KBLOCK"); cv && !vlds) {
                 plan.kblock = atoi(cv) == 512 ? 512 : 256;
                 eng->jit_shape_env = true;
             }
@@ -2610,7 +2738,7 @@ int mdp_engine_run(mdp_engine *eng, double *d_out, uint32_t ld_out, void *stream
                              eng->layout == MDP_LAYOUT_CE ? d.ne : d.nc);
     // the caller's stream as given: NULL is HIP's null stream (torch's default
     // stream), never the engine's private non-blocking stream
-    return run_dev(eng, d, d_out, ld_out, (hipStream_t)stream);
+    return run_dev(eng, d, d_out, layout_strides(eng->layout, ld_out), (hipStream_t)stream);
 }
 
 int mdp_loglik_grid(mdp_engine *eng, const double *e, uint32_t ne, const double *c, uint32_t nc,
@@ -2628,7 +2756,8 @@ int mdp_loglik_grid(mdp_engine *eng, const double *e, uint32_t ne, const double 
         const uint32_t rows = r1[r] - r0[r];
         if ((rc = set_grid_dev(eng, d, e + r0[r], rows, c, nc))) return rc;
         if ((rc = dev_reserve(&d.out, &d.cap_out, (size_t)rows * nc))) return rc;
-        if ((rc = run_dev(eng, d, d.out, nc, d.stream))) return rc;
+        // [e][c] whatever the engine layout: the host contract of this call
+        if ((rc = run_dev(eng, d, d.out, OutStrides{nc, 1u}, d.stream))) return rc;
     }
     for (uint32_t r = 0; r < nd; ++r) {
         DevCtx &d = eng->devs[r];
@@ -2760,7 +2889,7 @@ int mdp_engine_time_kernels(mdp_engine *eng, double *d_out, uint32_t ld_out, voi
     double t[3];
     const int saved = eng->profiling;
     eng->profiling = 0;
-    int rc = time_kernels(eng, d, d_out, ld_out, (hipStream_t)stream, reps, t);
+    int rc = time_kernels(eng, d, d_out, layout_strides(eng->layout, ld_out), (hipStream_t)stream, reps, t);
     eng->profiling = saved;
     if (rc) return rc;
     const int k = std::min(max_k, 3);
@@ -2830,7 +2959,10 @@ int mdp_engine_launched(const mdp_engine *eng, char *buf, size_t len)
 {
     if (!eng || !buf || !len) return mdp_set_error(MDP_EINVAL, "null argument");
     std::string all;
-    for (const std::string &k : eng->launched) all += (all.empty() ? "" : " ") + k;
+    {
+        std::lock_guard<std::mutex> lk(eng->launched_mu);
+        for (const std::string &k : eng->launched) all += (all.empty() ? "" : " ") + k;
+    }
     snprintf(buf, len, "%s", all.c_str());
     return (int)all.size();
 }

@@ -320,25 +320,28 @@ static void host_parallel(unsigned nt, size_t n, void *arg, void (*fn)(void *, s
 
 typedef struct {
     const double *lik;
+    uint32_t s;
+    size_t se, sc;
     double *ex;
 } exp_arg;
 
 static void exp_range(void *p, size_t i0, size_t i1)
 {
     exp_arg *a = (exp_arg *)p;
-    for (size_t i = i0; i < i1; ++i) a->ex[i] = exp(a->lik[i]);
+    for (size_t i = i0; i < i1; ++i) a->ex[i] = exp(a->lik[(i / a->s) * a->se + (i % a->s) * a->sc]);
 }
 
-/* main_MIDASPOM.c:413-425.  The exps of a large grid are evaluated in
- * threads; the weighted sum runs in the reference's order (k outer, l
- * inner), so Ltot is bit-identical to the sequential form. */
-double mdp_log_total(const double *lik, uint32_t s, double win)
+/* main_MIDASPOM.c:413-425, on the s x s view lik[k*se + l*sc] (k = e row,
+ * l = c column).  The exps of a large grid are evaluated in threads; the
+ * weighted sum runs in the reference's order (k outer, l inner), so Ltot is
+ * bit-identical to the sequential form in either layout. */
+double mdp_log_total_view(const double *lik, uint32_t s, size_t se, size_t sc, double win)
 {
     const size_t cells = (size_t)s * s;
     const unsigned nt = host_threads(cells);
     double *ex = nt > 1 ? (double *)malloc(sizeof(double) * cells) : NULL;
     if (ex) {
-        exp_arg a = {lik, ex};
+        exp_arg a = {lik, s, se, sc, ex};
         host_parallel(nt, cells, &a, exp_range);
     }
     double acc = 0;
@@ -347,22 +350,29 @@ double mdp_log_total(const double *lik, uint32_t s, double win)
         for (uint32_t l = 0; l < s; l++) {
             double w = wk;
             if (l == 0 || l == s - 1) w *= 0.5;
-            const size_t i = (size_t)k * s + l;
-            acc += (ex ? ex[i] : exp(lik[i])) * w;
+            acc += (ex ? ex[(size_t)k * s + l] : exp(lik[(size_t)k * se + (size_t)l * sc])) * w;
         }
     }
     free(ex);
     return 2 * log(win) + log(acc);
 }
 
+double mdp_log_total(const double *lik, uint32_t s, double win)
+{
+    return mdp_log_total_view(lik, s, s, 1, win);
+}
+
 typedef struct {
     const double *lik;
     uint32_t s;
+    size_t se, sc;
     double ltot;
     int raw;
-    char **buf;     /* per row range: the formatted text */
+    uint32_t rows_per_part;
+    size_t part0;   /* first part of the current batch */
+    char **buf;     /* per part of the batch: the formatted text */
     size_t *len;
-    size_t nparts;  /* rows are split into nparts ranges */
+    size_t *cap;
     int fail;
 } fmt_arg;
 
@@ -370,63 +380,82 @@ static void fmt_range(void *p, size_t q0, size_t q1)
 {
     fmt_arg *a = (fmt_arg *)p;
     for (size_t q = q0; q < q1; ++q) {
-        const uint32_t r0 = (uint32_t)((size_t)a->s * q / a->nparts), r1 = (uint32_t)((size_t)a->s * (q + 1) / a->nparts);
-        size_t cap = (size_t)(r1 - r0) * (a->s * 26u + 1u) + 64, used = 0;
-        char *b = (char *)malloc(cap);
-        if (!b) {
-            a->fail = 1;
-            continue;
-        }
+        const size_t part = a->part0 + q;
+        const uint32_t r0 = (uint32_t)(part * a->rows_per_part);
+        uint32_t r1 = r0 + a->rows_per_part;
+        if (r1 > a->s) r1 = a->s;
+        size_t cap = a->cap[q], used = 0;
+        char *b = a->buf[q];
         for (uint32_t i = r0; i < r1; i++) {
             for (uint32_t j = 0; j <= a->s; j++) {
                 /* room for one cell: %.20lf of the largest double is 331 bytes */
                 if (cap - used < 400) {
-                    cap = cap * 2 + 1024;
-                    char *nb = (char *)realloc(b, cap);
+                    const size_t ncap = cap * 2 + 1024;
+                    char *nb = (char *)realloc(b, ncap);
                     if (!nb) {
-                        free(b);
                         a->fail = 1;
+                        a->buf[q] = b;
+                        a->cap[q] = cap;
+                        a->len[q] = 0;
                         return;
                     }
                     b = nb;
+                    cap = ncap;
                 }
                 if (j == a->s) {
                     b[used++] = '\n';
                     break;
                 }
-                const double v = a->lik[(size_t)i * a->s + j];
+                const double v = a->lik[(size_t)i * a->se + (size_t)j * a->sc];
                 used += (size_t)snprintf(b + used, cap - used, "%.20lf\t", a->raw ? v : exp(v - a->ltot));
             }
         }
         a->buf[q] = b;
+        a->cap[q] = cap;
         a->len[q] = used;
     }
 }
 
 /* main_MIDASPOM.c:427-436 (raw: the MPI build's Ltot == 0 branch,
- * main_MIDASPOM_MPI.c:527).  Rows of a large grid are formatted in threads
- * and written in order: the bytes are those of the sequential writer. */
-int mdp_write_posterior(const char *path, const double *lik, uint32_t s, double ltot, int raw)
+ * main_MIDASPOM_MPI.c:527) on the view lik[i*se + j*sc] (i = e row, j = c
+ * column).  Rows are cut into parts of about 256 KB of text; batches of a
+ * few parts per thread are formatted in threads and written in order, so the
+ * bytes are those of the sequential writer and the memory held at once is
+ * bounded (a few MB per thread) whatever s is. */
+int mdp_write_posterior_view(const char *path, const double *lik, uint32_t s, size_t se, size_t sc, double ltot,
+                             int raw)
 {
     FILE *f = fopen(path, "wb");
     if (!f) return mdp_set_error(MDP_EIO, "cannot open output file '%s'", path);
     const unsigned nt = host_threads((size_t)s * s);
-    const size_t nparts = nt > 1 ? (size_t)nt * 4 : 1;  /* a few ranges per thread */
-    fmt_arg a = {lik, s, ltot, raw, (char **)calloc(nparts, sizeof(char *)), (size_t *)calloc(nparts, sizeof(size_t)),
-                 nparts, 0};
+    const size_t row_bytes = (size_t)s * 26u + 1u;
+    uint32_t rpp = (uint32_t)((1u << 18) / row_bytes);
+    if (rpp < 1) rpp = 1;
+    if (rpp > s) rpp = s ? s : 1;
+    const size_t nparts_all = s ? ((size_t)s + rpp - 1) / rpp : 0;
+    const size_t batch = nt > 1 ? (size_t)nt * 4 : 1;  /* a few parts per thread */
+    fmt_arg a = {lik, s, se, sc, ltot, raw, rpp, 0, (char **)calloc(batch, sizeof(char *)),
+                 (size_t *)calloc(batch, sizeof(size_t)), (size_t *)calloc(batch, sizeof(size_t)), 0};
     int rc = MDP_OK;
-    if (!a.buf || !a.len) {
-        rc = mdp_set_error(MDP_ENOMEM, "out of host memory");
-    } else {
-        host_parallel(nt, nparts, &a, fmt_range);
+    if (!a.buf || !a.len || !a.cap) rc = mdp_set_error(MDP_ENOMEM, "out of host memory");
+    for (size_t p0 = 0; p0 < nparts_all && !rc; p0 += batch) {
+        const size_t nb = nparts_all - p0 < batch ? nparts_all - p0 : batch;
+        a.part0 = p0;
+        host_parallel(nt, nb, &a, fmt_range);
         if (a.fail) rc = mdp_set_error(MDP_ENOMEM, "out of host memory");
-        for (size_t q = 0; q < nparts && !rc; ++q)
+        for (size_t q = 0; q < nb && !rc; ++q)
             if (a.len[q] && fwrite(a.buf[q], 1, a.len[q], f) != a.len[q]) rc = mdp_set_error(MDP_EIO, "write to '%s' failed", path);
     }
     if (a.buf)
-        for (size_t q = 0; q < nparts; ++q) free(a.buf[q]);
+        for (size_t q = 0; q < batch; ++q) free(a.buf[q]);
     free(a.buf);
     free(a.len);
+    free(a.cap);
     if (fclose(f) != 0 && !rc) rc = mdp_set_error(MDP_EIO, "write to '%s' failed", path);
     return rc;
+}
+
+int mdp_write_posterior(const char *path, const double *lik, uint32_t s, double ltot, int raw)
+{
+    return mdp_write_posterior_view(path, lik, s, s, 1, ltot, raw);
 }

@@ -9,7 +9,9 @@
 // the LDS reads of later transitions under the arithmetic of earlier ones;
 // the runtime-shape kernels in spom_engine.hip serialise on every general
 // year instead.  Code objects are cached in memory and on disk, keyed by the
-// FNV-1a hash of the generated source.
+// FNV-1a hash of the generated source, the compile options and the hipRTC
+// version; a cached file that is not a gfx950 code object, or that the
+// runtime refuses to load (spom_engine.hip jit_load), is rebuilt.
 #include <hip/hiprtc.h>
 #include <unistd.h>
 
@@ -172,16 +174,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     std::ostringstream o;
     o << kPrelude;
     const bool gather = !pl.qidx.empty();
-    const bool sq = pl.sq && !pl.fused;
-    const int dppq = sq ? 0 : pl.dppq;
     const size_t ldq_local = gather ? ((pl.qidx.size() + 1) & ~(size_t)1) : pl.ldQ;
     o << "#define LOGF(x) " << (pl.fast_log ? "mdp_log(x)" : "log(x)") << "\n";
-    if (dppq)  // acc + Q[16 c + K] w, the coefficient broadcast from lane K of each row of 16
-        o << "template <int K>\n"
-             "__device__ __forceinline__ double qf(double qc, double w, double acc)\n{\n"
-             "    asm(\"v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf\"\n"
-             "        : \"+v\"(acc) : \"v\"(qc), \"v\"(w), \"i\"(K));\n"
-             "    return acc;\n}\n";
     o << "#define KBLOCK " << (pl.kblock > 0 ? pl.kblock : 256) << "\n";  // threads per column
     o << "#define EPL " << EPL << "\n#define LDQ " << ldq_local << "\n#define LDQG "
       << (gather ? pl.ldq_row : pl.ldQ) << "\n#define NQG " << pl.qidx.size() << "\n#define NPMAX " << npmax
@@ -220,7 +214,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps,\n"
          "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax,\n"
          "    double *__restrict__ vscr, u32 ldv, const u32 *__restrict__ qidx, u32 out_cs)\n{\n"
-      << "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ + " << (dppq ? 16 : 2) << "];\n"
+      << "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ + 2];\n"
       << stamp(6) << stamp(0) <<
          // XCD-aware order: the dispatcher deals blocks round-robin over the 8
          // XCDs, so consecutive logical blocks (adjacent c columns of the
@@ -234,8 +228,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
       << (pl.efast ? "    const u32 gy = (ne + KBLOCK * EPL - 1) / (KBLOCK * EPL), ic0 = lb / gy * FC, by = lb % gy;\n"
                    : "    const u32 ncb = (nc + FC - 1) / FC, ic0 = lb % ncb * FC, by = lb / ncb;\n")
       << (SPL > 1 || FC == 1 ? "    const u32 ic = ic0;\n" : "    const u32 ic = ic0 + half;\n")
-      << (sq ? "    const double *Qh = Qrow + (size_t)(ic < nc ? ic : 0) * LDQG;\n"
-             : SPL > 1 ? "    const double *Qh = Ql;\n" : "    const double *Qh = Ql + half * LDQ;\n") <<
+      << (SPL > 1 ? "    const double *Qh = Ql;\n" : "    const double *Qh = Ql + half * LDQ;\n") <<
          // this lane's e values: issued first, their latency hides under the prologue
          "    u32 ie[EPL];\n    double ev[EPL];\n"
          "#pragma unroll\n"
@@ -300,9 +293,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        }\n"
              "    }\n";
     };
-    if (sq) {
-        // (no staging: the coefficients are read where they are used)
-    } else if (!pl.fused && !gather) {
+    if (!pl.fused && !gather) {
         stage("Ql", "Qrow + (size_t)ic * LDQ", "LDQ");  // this column's Q row (k_qrows)
         o << stamp(1);
     } else if (!pl.fused) {
@@ -501,38 +492,12 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     o << "    __syncthreads();\n"
       << stamp(2);
     // P = sum_m Q[off+m] W[|A|][m] as an expression for point i
-    // (scalar Q with gathered chunks: the chunk-local offset mapped back to
-    // the Q row's own)
-    auto qoff = [&](uint32_t i) { return std::to_string(sq && gather ? pl.qidx[i] : i); };
-    // dppq: the chunks a region has loaded (declared in its scope), and the
-    // declarations the next emitted line needs first
-    std::set<uint32_t> region_chunks;
-    std::string chunk_decls;
-    auto chunk = [&](uint32_t o) {
-        const uint32_t c = o / 16;
-        if (region_chunks.insert(c).second)
-            chunk_decls += "    const double QC" + std::to_string(c) + " = Qh[" + std::to_string(16 * c) +
-                           " + (threadIdx.x & 15u)];\n";
-        return "qf<" + std::to_string(o % 16) + ">(QC" + std::to_string(c);
-    };
-    auto flush_decls = [&]() {
-        std::string t;
-        t.swap(chunk_decls);
-        return t;
-    };
     auto pexpr = [&](uint32_t d) {
         const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u, nA = d >> 27;
-        if (dppq) {  // the same FMAs as below (dppq 1: the first as fma(Q, W, 0) = Q W)
-            std::string e = dppq == 1 ? std::string("0.0")
-                                      : "Qh[" + qoff(off) + "] * W[i][" + std::to_string(widx[std::make_pair(nA, 0u)]) + "]";
-            for (uint32_t m = dppq == 1 ? 0 : 1; m <= nX; ++m)
-                e = chunk(off + m) + ", W[i][" + std::to_string(widx[std::make_pair(nA, m)]) + "], " + e + ")";
-            return e;
-        }
-        std::string e = "Qh[" + qoff(off) + "] * W[i][" +
+        std::string e = "Qh[" + std::to_string(off) + "] * W[i][" +
                         std::to_string(widx[std::make_pair(nA, 0u)]) + "]";
         for (uint32_t m = 1; m <= nX; ++m)
-            e = "fma(Qh[" + qoff(off + m) + "], W[i][" +
+            e = "fma(Qh[" + std::to_string(off + m) + "], W[i][" +
                 std::to_string(widx[std::make_pair(nA, m)]) + "], " + e + ")";
         return e;
     };
@@ -553,7 +518,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     auto fence = [&]() {
         if (++since >= window) {
             o << "    }}\n" << guard;
-            region_chunks.clear();
             since = 0;
         }
     };
@@ -630,7 +594,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         if (npp == 1 && npc == 1 && !pl.vlds) {
             std::string pre;
             const std::string e = use_expr(u++, pre);
-            o << flush_decls() << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
+            o << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
             flops += 1.0;
             fence();
             continue;
@@ -649,7 +613,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                           : h + 1 < SPL ? "    } else if (half == " + std::to_string(h) + ") {\n"
                                         : std::string("    } else {\n"))
                       << guard;
-                    region_chunks.clear();
                     since = 0;
                 }
                 for (uint32_t k = 0; k < npp; ++k)
@@ -657,7 +620,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                         std::string pre;
                         const std::string e = use_expr(ubase + (size_t)l * npp + k, pre);
                         const std::string acc = "n[i][" + std::to_string(l / SPL) + "]";
-                        o << flush_decls() << "    for (int i = 0; i < EPL; ++i) { " << pre << acc << " = fma(" << vref(k) << ", " << e
+                        o << "    for (int i = 0; i < EPL; ++i) { " << pre << acc << " = fma(" << vref(k) << ", " << e
                           << ", " << (k ? acc : std::string("0.0")) << "); }\n";
                         flops += k ? 2.0 : 1.0;
                         fence();
@@ -677,7 +640,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             o << (split ? "        }\n    }\n    __syncthreads();\n" : "    }\n");
             if (split) {
                 o << guard;
-                region_chunks.clear();
                 since = 0;
             }
             u = ubase + (size_t)npp * npc;
@@ -688,7 +650,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             for (uint32_t k = 0; k < npp; ++k) {
                 std::string pre;
                 const std::string e = use_expr(u++, pre);
-                o << flush_decls() << "    for (int i = 0; i < EPL; ++i) { " << pre << "n[i][" << l << "] = fma(" << vref(k) << ", "
+                o << "    for (int i = 0; i < EPL; ++i) { " << pre << "n[i][" << l << "] = fma(" << vref(k) << ", "
                   << e << ", " << (k ? "n[i][" + std::to_string(l) + "]" : std::string("0.0")) << "); }\n";
                 flops += k ? 2.0 : 1.0;
                 fence();
@@ -745,10 +707,70 @@ std::string mdp_jit_log_source()
            "    if (i < n) y[i] = mdp_log(x[i]);\n}\n";
 }
 
-int mdp_jit_compile(const std::string &src, std::vector<char> &code, std::string &log)
+namespace {
+
+const char *const kJitOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+constexpr int kJitNOpts = 3;
+constexpr int kJitCacheFormat = 2;  // bump when the cache key or file layout changes
+
+// Cache key: the generated source, the compile options, the hipRTC version
+// and the cache format.  A code object built by another toolchain or with
+// other options therefore lands under another name.
+uint64_t jit_key(const std::string &src)
 {
-    const uint64_t key = fnv1a(src);
-    {
+    int major = 0, minor = 0;
+    (void)hiprtcVersion(&major, &minor);
+    std::string k = src;
+    k += '\0';
+    for (const char *o : kJitOpts) (k += o) += ' ';
+    k += "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " format " + std::to_string(kJitCacheFormat);
+    return fnv1a(k);
+}
+
+// Cache files are the code object followed by a 16-byte trailer: "MDPJ", the
+// format, and the 64-bit key it was compiled for.  A file whose trailer does
+// not name this key (a foreign or planted object, another format) is a miss.
+constexpr char kTrailerMagic[4] = {'M', 'D', 'P', 'J'};
+
+void add_trailer(std::vector<char> &c, uint64_t key)
+{
+    const uint32_t fmt = kJitCacheFormat;
+    c.insert(c.end(), kTrailerMagic, kTrailerMagic + 4);
+    c.insert(c.end(), (const char *)&fmt, (const char *)&fmt + 4);
+    c.insert(c.end(), (const char *)&key, (const char *)&key + 8);
+}
+
+bool strip_trailer(std::vector<char> &c, uint64_t key)
+{
+    if (c.size() < 16) return false;
+    const char *t = c.data() + c.size() - 16;
+    uint32_t fmt;
+    uint64_t k;
+    memcpy(&fmt, t + 4, 4);
+    memcpy(&k, t + 8, 8);
+    if (memcmp(t, kTrailerMagic, 4) != 0 || fmt != (uint32_t)kJitCacheFormat || k != key) return false;
+    c.resize(c.size() - 16);
+    return true;
+}
+
+// ... and what precedes it must be an AMDGPU ELF code object for gfx950
+// (e_machine EM_AMDGPU = 224, EF_AMDGPU_MACH = 0x04f).
+bool plausible_code_object(const std::vector<char> &c)
+{
+    if (c.size() < 64 || memcmp(c.data(), "\x7f" "ELF", 4) != 0) return false;
+    uint16_t machine;
+    uint32_t flags;
+    memcpy(&machine, c.data() + 18, sizeof machine);
+    memcpy(&flags, c.data() + 48, sizeof flags);
+    return machine == 224 && (flags & 0xffu) == 0x4fu;
+}
+
+}  // namespace
+
+int mdp_jit_compile(const std::string &src, std::vector<char> &code, std::string &log, bool fresh)
+{
+    const uint64_t key = jit_key(src);
+    if (!fresh) {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_code.find(key);
         if (it != g_code.end()) {
@@ -760,7 +782,8 @@ int mdp_jit_compile(const std::string &src, std::vector<char> &code, std::string
     snprintf(name, sizeof name, "fwd_%016llx.co", (unsigned long long)key);
     const std::string dir = cache_dir();
     const std::string path = dir + "/" + name;
-    if (!getenv("MDP_JIT_NOCACHE") && read_file(path, code)) {
+    if (!fresh && !getenv("MDP_JIT_NOCACHE") && read_file(path, code) && strip_trailer(code, key) &&
+        plausible_code_object(code)) {
         std::lock_guard<std::mutex> lk(g_mu);
         g_code[key] = code;
         return 0;
@@ -770,8 +793,7 @@ int mdp_jit_compile(const std::string &src, std::vector<char> &code, std::string
         log = "hiprtcCreateProgram failed";
         return -1;
     }
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    const hiprtcResult r = hiprtcCompileProgram(prog, kJitNOpts, kJitOpts);
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
     if (ls > 1) {
@@ -793,6 +815,10 @@ int mdp_jit_compile(const std::string &src, std::vector<char> &code, std::string
         std::lock_guard<std::mutex> lk(g_mu);
         g_code[key] = code;
     }
-    if (!getenv("MDP_JIT_NOCACHE")) write_file(dir, path, code);
+    if (!getenv("MDP_JIT_NOCACHE")) {
+        std::vector<char> file = code;
+        add_trailer(file, key);
+        write_file(dir, path, file);
+    }
     return 0;
 }

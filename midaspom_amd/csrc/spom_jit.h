@@ -15,7 +15,7 @@ struct MdpJitPlan {
     bool fused = false;
     int fused_cols = 2;  // c columns per fused workgroup (KBLOCK threads each)
     bool fast_log = true;  // mdp_log (prelude) instead of the library log for log L
-    int hack = 0;  // measurement-only builds (MDP_JIT_HACK; results wrong): 1 = no log, no stores; 2 = no stores
+    int hack = 0;  // diag build only (MDP_JIT_HACK; results wrong): 1 = no log, no stores; 2 = no stores
     uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
     // items, qstart, qitem, the Z-row series coefficients [nj][8], then
@@ -41,19 +41,8 @@ struct MdpJitPlan {
     bool diag = false;            // record s_memtime phase stamps (MDP_DIAG)
     bool xcd = true;              // XCD-aware block order
     bool efast = true;            // e blocks of one column group dispatched back to back (same XCD)
-    // reading variant: the transitions' Q coefficients read straight from the
-    // column's Q row in global memory (wave-uniform addresses: scalar loads
-    // into SGPRs, FMA operands) instead of staged in LDS (MDP_JIT_SQ)
-    bool sq = false;
     int slots = 8;                // registers caching transitions that recur (0: none)
-    // Q coefficients as 16-value chunks (lane k of each row of 16 holds Q[16 c
-    // + k], one lane-distinct ds_read_b64 per chunk) fed to the FMAs through
-    // v_fmac_f64_dpp row_newbcast instead of broadcast LDS pair reads
-    // (MDP_JIT_DPPQ; not with sq): 1 every coefficient (each dot product
-    // from a zeroed accumulator), 2 all but the first (its product a plain
-    // multiply with the coefficient read as before)
-    int dppq = 0;
-    int wpe = 0;                  // minimum waves per SIMD asked of the compiler (0: its default)
+    int wpe = 0;                  // diag build only: minimum waves per SIMD asked of the compiler (0: its default)
     double flops_pt = 0;          // out: FP64 flops per grid point of the generated code
     // a chunk of a long series (main_MIDASPOM.c:371-384 has no length limit):
     // np / udesc cover years [t0, t1] of the series; a chunk that is not the
@@ -78,7 +67,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &plan);
 std::string mdp_jit_log_source();
 
 // Compile (or fetch from the memory / disk cache) a gfx950 code object.
+// `fresh`: skip both caches and recompile (the runtime refused a cached
+// object); the new object replaces the cached one.
 // Returns 0 on success; on failure `log` holds the compiler output.
-int mdp_jit_compile(const std::string &src, std::vector<char> &code, std::string &log);
+int mdp_jit_compile(const std::string &src, std::vector<char> &code, std::string &log, bool fresh = false);
 
 #endif

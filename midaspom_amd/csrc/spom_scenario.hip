@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "mdp_internal.h"
@@ -841,8 +842,37 @@ int mdp_device_count(void)
 int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, double d, int kind, int device,
                         mdp_scenario **out)
 {
+    return mdp_scenario_create_opts(row, n, m, p, d, kind, device, nullptr, out);
+}
+
+// options (ABI 7): "MDP_SCN_BIG=1" / "MDP_SCN_ROW=1" force the HBM-state or
+// the row-parallel kernel (tests pin the kernels against each other); the
+// library reads no environment
+int mdp_scenario_create_opts(const int32_t *row, uint32_t n, double m, float p, double d, int kind, int device,
+                             const char *options, mdp_scenario **out)
+{
     if (!row || !out || n == 0) return mdp_set_error(MDP_EINVAL, "null argument");
     *out = nullptr;
+    bool force_big = false, force_row = false;
+    if (options) {
+        std::string cur;
+        for (const char *c = options;; ++c) {
+            if (*c == 0 || *c == ';' || *c == ',' || *c == ' ' || *c == '\t' || *c == '\n') {
+                if (!cur.empty()) {
+                    const size_t eq = cur.find('=');
+                    const std::string k = cur.substr(0, eq);
+                    const bool on = eq == std::string::npos || atoi(cur.c_str() + eq + 1) != 0;
+                    if (k == "MDP_SCN_BIG") force_big = on;
+                    else if (k == "MDP_SCN_ROW") force_row = on;
+                    else return mdp_set_error(MDP_EINVAL, "unknown scenario option '%s'", k.c_str());
+                    cur.clear();
+                }
+                if (*c == 0) break;
+            } else {
+                cur += *c;
+            }
+        }
+    }
     if (n > kBigMaxN)
         return mdp_set_error(MDP_EUNSUPPORTED, "%u patches: the scenario engine takes n <= %u (2^n states)", n,
                              kBigMaxN);
@@ -859,11 +889,9 @@ int mdp_scenario_create(const int32_t *row, uint32_t n, double m, float p, doubl
     sc->m = m;
     sc->d = d;
     sc->device = device;
-    // n > 8: the LDS-resident k_scn does not fit; MDP_SCN_BIG=1 forces k_scn_big (tests)
-    // 8 < n <= 12: k_scn_row (MDP_SCN_ROW=1 forces it for any n <= 12); n > 12:
-    // k_scn_big (MDP_SCN_BIG=1 forces it for any n)
-    const char *bv = getenv("MDP_SCN_BIG"), *rv = getenv("MDP_SCN_ROW");
-    const bool force_big = bv && atoi(bv) != 0, force_row = rv && atoi(rv) != 0;
+    // n > 8: the LDS-resident k_scn does not fit; 8 < n <= 12: k_scn_row
+    // (option MDP_SCN_ROW=1 forces it for any n <= 12); n > 12: k_scn_big
+    // (MDP_SCN_BIG=1 forces it for any n)
     sc->row = !force_big && n <= kRowMaxN && (n > kMaxN || force_row);
     sc->big = !sc->row && (n > kMaxN || force_big);
     const uint32_t ns = sc->ns;

@@ -37,6 +37,9 @@ ap.add_argument("--variants", default=DEFAULT_VARIANTS)
 ap.add_argument("--diag", action="store_true")
 ap.add_argument("--layout", default="ce", choices=["ce", "ec"], help="device layout of log L (bench.py's default: ce)")
 args = ap.parse_args()
+# phase stamps and the measurement-only options need the diag library
+if args.diag or "MDP_JIT_HACK" in args.variants or "MDP_JIT_WPE" in args.variants:
+    os.environ["MIDASPOM_DIAG_LIB"] = "1"
 torch.cuda.set_device(0)
 tmp = Path(tempfile.mkdtemp())
 KEYS = ("MDP_JIT", "MDP_EPL", "MDP_QROWS_XCD", "MDP_JIT_EFAST", "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_JIT_WINDOW", "MDP_FWD", "MDP_DIAG", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED",

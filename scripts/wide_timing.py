@@ -24,11 +24,10 @@ from midaspom_amd import synth  # noqa: E402
 tmp = Path(tempfile.mkdtemp())
 PATHS = {  # path name -> engine knobs
     "default": {}, "nosplit": {"MDP_VSPLIT": "1"}, "split2": {"MDP_VSPLIT": "2"}, "split4": {"MDP_VSPLIT": "4"},
-    "sq": {"MDP_JIT_SQ": "1"}, "split2_sq": {"MDP_VSPLIT": "2", "MDP_JIT_SQ": "1"},
-    "split4_sq": {"MDP_VSPLIT": "4", "MDP_JIT_SQ": "1"}, "wide": {"MDP_WIDE": "1"},
+    "wide": {"MDP_WIDE": "1"},
     "epl2": {"MDP_VLDS_EPL": "2"},
 }
-CASES = [(0.45, 30, 512, p) for p in os.environ.get("WIDE_PATHS", "default,nosplit,sq,wide").split(",")]
+CASES = [(0.45, 30, 512, p) for p in os.environ.get("WIDE_PATHS", "default,nosplit,wide").split(",")]
 CASES.append((0.6, 50, 256, "default"))
 for pmiss, T, s, path in CASES:
     for k in [k for k in os.environ if k.startswith("MDP_")]:

@@ -1,0 +1,122 @@
+"""Engine options (ABI 7) and the hipRTC code-object cache, on a CPU host.
+
+* The library reads no tuning knob from the environment: kernel variants are
+  chosen by mdp_engine_create_opts' options string.  Unknown names and the
+  measurement-only names (MDP_DIAG, MDP_JIT_HACK, MDP_JIT_WPE) are refused by
+  the default library; the diag library (libmidaspom_diag.so) accepts them.
+* A cached code object is used only if its trailer names the cache key of
+  the source being compiled (source, compile options, hipRTC version): a
+  planted or foreign file under the key is rebuilt, not loaded.
+
+Each case runs in a subprocess (the library is loaded once per process)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+from conftest import gpu_available
+
+ROOT = Path(__file__).resolve().parents[1]
+BUILD = ROOT / "midaspom_amd" / "_build"
+
+PRELUDE = r"""
+import ctypes, sys
+sys.path.insert(0, {root!r})
+import midaspom_amd as mdp
+from midaspom_amd import _lib
+model = mdp.Model.load({root!r} + "/tests/golden/occupancies.txt")
+L = _lib.lib()
+def create(opts, c_plain=False):
+    h = ctypes.c_void_p()
+    if c_plain:
+        rc = L.mdp_engine_create(ctypes.byref(model.problem), None, 0, ctypes.byref(h))
+    else:
+        rc = L.mdp_engine_create_opts(ctypes.byref(model.problem), None, 0, opts, ctypes.byref(h))
+    return rc, L.mdp_last_error().decode()
+"""
+
+
+def run(code, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if not k.startswith("MDP_") and k != "MIDASPOM_DIAG_LIB"}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, "-c", PRELUDE.format(root=str(ROOT)) + code], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks option parsing up to the device probe (CPU hosts)")
+def test_options_parsed_and_environment_ignored():
+    out = run(r"""
+rc, msg = create(b"MDP_NO_SUCH=1")
+assert rc == -1 and "unknown engine option" in msg, (rc, msg)
+for bad in (b"MDP_JIT_HACK=1", b"MDP_DIAG=1", b"MDP_JIT_WPE=3"):
+    rc, msg = create(bad)
+    assert rc == -1 and "measurement-only" in msg, (bad, rc, msg)
+# variant options pass the parser (then: no device)
+rc, msg = create(b"MDP_FUSED=1;MDP_JIT_CHUNK=64, MDP_EPL=1")
+assert rc == -5, (rc, msg)
+# MDP_JIT_HACK in the environment is not read by the library
+rc, msg = create(None, c_plain=True)
+assert rc == -5, (rc, msg)
+# ... while the Python layer forwards it as an option, which the default
+# library refuses instead of building kernels with wrong results
+try:
+    mdp.Engine(model)
+except mdp.MidaspomError as ex:
+    assert "measurement-only" in str(ex), ex
+else:
+    raise SystemExit("accepted")
+print("ok")
+""", {"MDP_JIT_HACK": "1"})
+    assert "ok" in out
+
+
+@pytest.mark.skipif(gpu_available(), reason="CPU hosts")
+@pytest.mark.skipif(not (BUILD / "libmidaspom_diag.so").exists(), reason="diag library not built")
+def test_diag_library_accepts_measurement_options():
+    out = run(r"""
+assert "diag" in L._name
+rc, msg = create(b"MDP_JIT_HACK=1;MDP_DIAG=1")
+assert rc == -5, (rc, msg)
+print("ok")
+""", {"MIDASPOM_DIAG_LIB": "1"})
+    assert "ok" in out
+
+
+@pytest.mark.skipif(gpu_available(), reason="offline compile check runs on CPU-only hosts")
+def test_jit_cache_rejects_planted_and_foreign_objects(tmp_path):
+    """Compile config 1's forward kernels into an empty cache; then replace
+    every cached file by garbage, by a bare gfx950 ELF without our trailer,
+    and by another key's (valid) file: each time the engine recompiles, and
+    the cache again holds trailer-stamped objects."""
+    cache = tmp_path / "jit"
+    code = r"""
+import os
+os.environ.pop("MDP_JIT_NOCACHE", None)
+rc, msg = create(b"MDP_JIT_CHECK=1")
+assert rc == -5 and "forward kernels compiled" in msg, msg
+print("ok")
+"""
+    env = {"MDP_JIT_CACHE": str(cache)}
+    assert "ok" in run(code, env)
+    files = sorted(cache.glob("fwd_*.co"))
+    assert len(files) == 2, files  # fused + reading variants
+    good = {f: f.read_bytes() for f in files}
+    for f, b in good.items():
+        assert b[:4] == b"\x7fELF" and b[-16:-12] == b"MDPJ"
+    plants = [
+        lambda f: b"not a code object" * 10,
+        lambda f: good[f][:-16],                   # a bare ELF: no trailer naming the key
+        lambda f: good[files[1 - files.index(f)]],  # another key's stamped object
+    ]
+    for plant in plants:
+        for f in files:
+            f.write_bytes(plant(f))
+        assert "ok" in run(code, env)
+        for f in files:
+            assert f.read_bytes() == good[f], f.name

@@ -83,3 +83,33 @@ def test_layout_rejects_short_ld():
             eng.run(1 << 20, 39)  # ld < ne: refused before any launch
         with pytest.raises(KeyError):
             eng.set_layout("xy")
+
+
+@pytest.mark.parametrize("name", ["fused", "reading", "wide"])
+def test_loglik_grid_ignores_engine_layout(name, monkeypatch):
+    """mdp_loglik_grid's host result is [e][c] whatever mdp_engine_set_layout
+    chose for mdp_engine_run: after set_layout('ce') on a grid with nc > ne
+    (where a CE write through loglik_grid's [e][c] slab would also overrun
+    it), the result equals a fresh engine's, bit for bit."""
+    import torch
+
+    make, _, _, env, _ = CASES[name]
+    model = make()
+    for k in KNOBS:
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = np.sort(np.random.default_rng(1).uniform(0.05, 0.9, 23))
+    c = np.sort(np.random.default_rng(2).uniform(0.01, 0.6, 90))
+    with mdp.Engine(model, devices=[0]) as fresh:
+        ref = fresh.loglik_grid(e, c)
+    with mdp.Engine(model, devices=[0]) as eng:
+        eng.set_grid(e, c)
+        eng.set_layout("ce")
+        out = torch.empty((c.size, e.size), dtype=torch.float64, device="cuda")
+        eng.run(out.data_ptr(), e.size)
+        got = eng.loglik_grid(e, c)
+        torch.cuda.synchronize()
+        ce = out.cpu().numpy()
+    assert np.array_equal(got, ref, equal_nan=True)
+    assert np.array_equal(ce.T, ref, equal_nan=True)

@@ -143,3 +143,29 @@ def test_missing_last_newline_drops_row(tmp_path):
     f.write_text("0 1 1\n1 0 1\n1 1 1")
     pm = mdp.Model.load(f)
     assert (pm.n, pm.tmax) == (3, 2)
+
+
+@pytest.mark.parametrize("threads", ["1", "3"])
+def test_batched_writer_and_ce_view_bitexact(tmp_path, monkeypatch, threads):
+    """The writer formats parts of ~256 KB of text in bounded batches (a few
+    parts per thread, written in order): at s = 700 (14 rows a part, 50
+    parts, several batches with 3 threads) the file is byte-identical to the
+    oracle's sequential writer.  The [c][e] device layout is read in place
+    through the transposed view (mdp_*_view with se = 1, sc = s): the same
+    Ltot bits and the same bytes."""
+    monkeypatch.setenv("OMP_NUM_THREADS", threads)
+    rng = np.random.default_rng(11)
+    s = 700
+    lik = rng.normal(-30, 8, (s, s))
+    lik[3, :5] = -np.inf
+    g, win = mdp.grid(s)
+    lt = mdp.log_total(lik, win)
+    assert lt == oracle.ltot(lik, win)
+    ce = np.ascontiguousarray(lik.T)  # what MDP_LAYOUT_CE leaves in device memory
+    assert mdp.log_total(ce.T, win) == lt
+    mdp.write_posterior(tmp_path / "a.txt", lik, lt)
+    mdp.write_posterior(tmp_path / "c.txt", ce.T, lt)
+    oracle.write_posterior(tmp_path / "b.txt", lik, lt)
+    ref = (tmp_path / "b.txt").read_bytes()
+    assert (tmp_path / "a.txt").read_bytes() == ref
+    assert (tmp_path / "c.txt").read_bytes() == ref
