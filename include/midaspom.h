@@ -151,6 +151,12 @@ int mdp_loglik_grid(mdp_engine *engine, const double *e, uint32_t ne, const doub
 #define MDP_LAYOUT_EC 0
 #define MDP_LAYOUT_CE 1
 int mdp_engine_set_layout(mdp_engine *engine, int layout);
+/* mdp_loglik_grid with the host result in either layout (ABI 7): EC
+ * out[ie*nc + ic] (= mdp_loglik_grid), or CE out[ic*ne + ie] -- what every
+ * device slab holds natively; mdp_log_total_view / mdp_write_posterior_view
+ * read it in place (se = 1, sc = ne), so the drop-in CLIs never transpose. */
+int mdp_loglik_grid_layout(mdp_engine *engine, const double *e, uint32_t ne, const double *c, uint32_t nc,
+                           int layout, double *out);
 int mdp_engine_set_grid(mdp_engine *engine, const double *e, uint32_t ne, const double *c,
                         uint32_t nc);
 int mdp_engine_run(mdp_engine *engine, double *d_out, uint32_t ld_out, void *stream);

@@ -162,10 +162,17 @@ class Engine:
         except Exception:
             pass
 
-    def loglik_grid(self, e, c) -> np.ndarray:
-        """log L on the e x c grid (host arrays in, host [ne][nc] out)."""
+    def loglik_grid(self, e, c, layout: str = "ec") -> np.ndarray:
+        """log L on the e x c grid (host arrays in, host [ne][nc] out).
+        layout="ce" computes the devices' native [c][e] and returns its
+        transposed view (still indexed [ie][ic]; log_total / write_posterior
+        read it in place)."""
         e = np.ascontiguousarray(e, dtype=np.float64)
         c = np.ascontiguousarray(c, dtype=np.float64)
+        if layout == "ce":
+            out = np.empty((c.size, e.size), dtype=np.float64)
+            check(lib().mdp_loglik_grid_layout(self._h, _dptr(e), e.size, _dptr(c), c.size, 1, _dptr(out)))
+            return out.T
         out = np.empty((e.size, c.size), dtype=np.float64)
         check(lib().mdp_loglik_grid(self._h, _dptr(e), e.size, _dptr(c), c.size, _dptr(out)))
         return out
@@ -289,7 +296,7 @@ def run_file(input_path, output_path=None, m=400.0, p=0.5, d=100.0, s=101, lo=0.
     model = Model.load(input_path, m=m, p=p, d=d)
     g, win = grid(s, lo, hi)
     with Engine(model, devices=devices) as eng:
-        lik = eng.loglik_grid(g, g)
+        lik = eng.loglik_grid(g, g, layout="ce")  # the devices' native layout, read in place
     ltot = log_total(lik, win)
     if output_path is not None:
         write_posterior(output_path, lik, ltot)

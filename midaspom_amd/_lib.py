@@ -107,6 +107,7 @@ SIGNATURES = [
       ctypes.POINTER(ctypes.c_void_p)]),
     ("mdp_engine_destroy", None, [ctypes.c_void_p]),
     ("mdp_loglik_grid", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_u32, c_dbl_p, c_u32, c_dbl_p]),
+    ("mdp_loglik_grid_layout", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_u32, c_dbl_p, c_u32, ctypes.c_int, c_dbl_p]),
     ("mdp_engine_set_grid", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_u32, c_dbl_p, c_u32]),
     ("mdp_engine_run", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u32, ctypes.c_void_p]),
     ("mdp_engine_set_layout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

@@ -97,7 +97,7 @@ def main(argv=None) -> int:
         out("Starting parallel likelihood computation\n")
         ngpu = a.g if a.g is not None else int(os.environ.get("MIDASPOM_GPUS", "0"))
         with mdp.Engine(model, n_devices=max(0, ngpu)) as eng:  # 0: the current device
-            lik = eng.loglik_grid(g, g)
+            lik = eng.loglik_grid(g, g, layout="ce")  # [c][e] slabs, read in place
         for ie in range(a.s):  # ((float)ie+1)*100.0/nstep, exact in double (:394)
             out(f"{(ie + 1) * 100.0 / a.s:.2f}% done\n")
         out("end likelihood computation\n")
@@ -125,7 +125,7 @@ def main(argv=None) -> int:
             out(f"Sending data (proc {rank})... ", all_ranks=True)
         else:
             out(f"Gathering data from {world - 1} proc... ")
-        lik = mdist.gather_rows(local_lik, rank, world, a.s, a.s,
+        lik = mdist.gather_cols(local_lik, rank, world, a.s, a.s,
                                 device=None if backend == "nccl" else "cpu")
         out("done\n", all_ranks=True)
         compute.engine.close()

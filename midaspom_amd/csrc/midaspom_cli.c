@@ -139,7 +139,10 @@ int main(int argc, char **argv)
     const double t_hip = now_s();
     rc = mdp_engine_create(&pb, devs, ngpu > 0 ? ngpu : 0, &eng);
     const double t_setup = now_s();
-    if (!rc) rc = mdp_loglik_grid(eng, grid, nstep, grid, nstep, lik);
+    /* lik[c][e]: each GPU writes its slab's columns contiguously (the
+     * layout the kernels store fastest); Ltot and the writer read it in
+     * place through the transposed view, so the file is the same bytes */
+    if (!rc) rc = mdp_loglik_grid_layout(eng, grid, nstep, grid, nstep, MDP_LAYOUT_CE, lik);
     free(devs);
     if (rc) {
         fprintf(stderr, "midaspom: %s\n", mdp_last_error());
@@ -151,11 +154,11 @@ int main(int argc, char **argv)
     for (unsigned ie = 0; ie < nstep; ie++) printf("%.2f%% done\n", ((float)ie + 1) * 100.0 / nstep);
     printf("end likelihood computation\n");
 
-    const double ltot = mdp_log_total(lik, nstep, win);
+    const double ltot = mdp_log_total_view(lik, nstep, 1, nstep, win);
     const double t_ltot = now_s();
     printf("Total log-likelihood=%.5lf\n", ltot);
     printf("Writing output in file %s... ", fout);
-    rc = mdp_write_posterior(fout, lik, nstep, ltot, 0);
+    rc = mdp_write_posterior_view(fout, lik, nstep, 1, nstep, ltot, 0);
     if (rc) {
         fprintf(stderr, "midaspom: %s\n", mdp_last_error());
         return 2;

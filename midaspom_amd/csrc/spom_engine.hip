@@ -330,6 +330,20 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
 // [c][row][NV] array whose 64-byte row stride put a wave's reads on a quarter
 // of the LDS banks, and ran threads over (c, item): SQ_LDS_BANK_CONFLICT was
 // 3x SQ_ACTIVE_INST_LDS.)
+// Canonical Q-entry sum -- k_qrows, k_wq and the fused forward kernel
+// (spom_jit.cpp) all use it, so their Q rows agree bit for bit: the entry's
+// items in CSR order taken in groups of kQGroup, each group summed left to
+// right, and the group sums added as a pairwise tree padded with zeros to a
+// power of two.  Folding the group sums into a binary counter (level l
+// holds the sum of an aligned block of 2^l groups) and then folding the
+// occupied levels from the lowest up gives exactly that tree; so does a
+// butterfly of xor shuffles over an aligned power-of-two lane segment
+// holding the sums of aligned power-of-two blocks of groups (k_qrows).
+constexpr uint32_t kQGroup = 4;
+constexpr int kQLevels = 24;
+constexpr uint32_t kQLanesMax = 64;  // k_qrows: lanes per entry (a power of two, <= a wave)
+constexpr int kQLevelsRows = 16;     // k_qrows: groups per lane <= 2^(kQLevelsRows - 1)
+
 constexpr int kQrowsBlock = 1024;
 constexpr uint32_t kQrowsMaxC = 4;
 template <int NV, bool EXACT, int CB>  // EXACT: nvar == NV (no padded factor slots)
@@ -338,7 +352,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     uint32_t kmax, const double *__restrict__ zsT, const double *__restrict__ zc, const double *__restrict__ sv,
     uint32_t nitems, const uint2 *__restrict__ items, uint32_t ncoef, const uint32_t *__restrict__ qstart,
     uint32_t nqi, const uint32_t *__restrict__ qitem, double *__restrict__ Q, uint32_t ldQ,
-    unsigned long long *__restrict__ stamps, uint32_t xcd)
+    unsigned long long *__restrict__ stamps, uint32_t xcd, const uint2 *__restrict__ qslot, uint32_t nslot)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     MDP_RSTAMP(stamps, 6);
@@ -515,33 +529,82 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     }
     __syncthreads();
     MDP_STAMP(stamps, 2);
-    // 3. Q rows: per entry its items in CSR order (four in flight), CB sums
-    for (uint32_t q = threadIdx.x; q < ldQ; q += kQrowsBlock) {
+    // 3. Q rows in the canonical order.  Each entry owns an aligned
+    // power-of-two segment of L <= kQLanesMax lanes of one wave (host table
+    // qslot: {entry, lane in entry | log2 L << 8 | log2 G << 12}, nslot a
+    // multiple of 64); a lane sums its 2^G consecutive groups for the CB c
+    // values (binary counter), then the segment adds the lanes' sums by a
+    // butterfly of xor shuffles, and its first lane stores the entry.  The
+    // chain per lane is a few gathers and log2 L shuffles instead of the
+    // entry's whole item list (35 on config 3).
+    for (uint32_t s0 = 0; s0 < nslot; s0 += kQrowsBlock) {
+        const uint32_t sl = s0 + threadIdx.x;
+        const uint2 sd = sl < nslot ? qslot[sl] : make_uint2(0xffffffffu, 0u);
+        const uint32_t q = sd.x, le = sd.y & 0xffu, lgL = (sd.y >> 8) & 0xfu, lgG = (sd.y >> 12) & 0xfu;
         double a[CB];
 #pragma unroll
         for (int i = 0; i < CB; ++i) a[i] = 0.0;
         if (q < ncoef) {
             const uint32_t i0 = Qs[q], i1 = Qs[q + 1];
-            for (uint32_t k = i0; k < i1; k += 4) {
-                double pv[4][CB];
+            // this lane's group sums: one group (nvar <= 8: an entry has at
+            // most C(8,4) = 70 items, 18 groups, so its segment takes them
+            // one per lane), else 2^G consecutive groups in a binary counter
+            auto group = [&](uint32_t j0, double *sg) {
 #pragma unroll
-                for (uint32_t u = 0; u < 4; ++u) {
-                    // lanes past their entry's end re-read item k: masking
-                    // them off instead splits these loads into per-u branches
-                    // with a wait each (measured: phase 3 7.3 k -> 9.8 k cycles)
-                    const uint32_t itm = Qi[k + u < i1 ? k + u : k];
+                for (int i = 0; i < CB; ++i) sg[i] = 0.0;
+                if (j0 >= i1) return;
+                uint32_t itm[kQGroup];
 #pragma unroll
-                    for (int i = 0; i < CB; ++i) pv[u][i] = Pl[pix(nitems, itm, i)];
+                for (uint32_t u = 0; u < kQGroup; ++u) itm[u] = Qi[j0 + u < i1 ? j0 + u : j0];
+#pragma unroll
+                for (int i = 0; i < CB; ++i) {
+                    double x = Pl[pix(nitems, itm[0], i)];
+#pragma unroll
+                    for (uint32_t u = 1; u < kQGroup; ++u) {
+                        const double y = Pl[pix(nitems, itm[u], i)];
+                        x = j0 + u < i1 ? x + y : x;
+                    }
+                    sg[i] = x;
                 }
+            };
+            if constexpr (NV == 8) {
+                group(i0 + le * kQGroup, a);
+            } else {
+                double lev[CB][kQLevelsRows];
+                const uint32_t ng = 1u << lgG;
+                for (uint32_t g = 0; g < ng; ++g) {
+                    double sg[CB];
+                    group(i0 + ((le << lgG) + g) * kQGroup, sg);
 #pragma unroll
-                for (uint32_t u = 0; u < 4; ++u)
+                    for (int l = 0; l < kQLevelsRows; ++l) {
+                        if ((g >> l) & 1u) {
 #pragma unroll
-                    for (int i = 0; i < CB; ++i) a[i] = k + u < i1 ? a[i] + pv[u][i] : a[i];
+                            for (int i = 0; i < CB; ++i) sg[i] = lev[i][l] + sg[i];
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < CB; ++i) lev[i][l] = sg[i];
+                            break;
+                        }
+                    }
+                    if (g + 1 == ng)  // 2^G groups: the counter holds one block
+#pragma unroll
+                        for (int i = 0; i < CB; ++i) a[i] = sg[i];
+                }
             }
         }
+        // every lane of the wave takes part in every shuffle; a lane adds
+        // only the levels inside its entry's segment
 #pragma unroll
-        for (int i = 0; i < CB; ++i)
-            if ((uint32_t)i < ncb) Q[(size_t)(c0 + i) * ldQ + q] = a[i];
+        for (uint32_t lv = 0; (1u << lv) < kQLanesMax; ++lv)
+#pragma unroll
+            for (int i = 0; i < CB; ++i) {
+                const double o = __shfl_xor(a[i], 1 << lv);
+                if (lv < lgL) a[i] = a[i] + o;
+            }
+        if (q < ldQ && le == 0)
+#pragma unroll
+            for (int i = 0; i < CB; ++i)
+                if ((uint32_t)i < ncb) Q[(size_t)(c0 + i) * ldQ + q] = a[i];
     }
     MDP_STAMP(stamps, 3);
     MDP_RSTAMP(stamps, 7);
@@ -1014,10 +1077,31 @@ __global__ __launch_bounds__(kBlock) void k_wq(uint32_t c0, uint32_t nitems, con
     const uint32_t q = blockIdx.x * kBlock + threadIdx.x, cl = blockIdx.y;
     if (q >= ldQ) return;
     double a = 0.0;
-    if (q < ncoef) {
+    if (q < ncoef) {  // the canonical order (kQGroup): groups, binary counter, fold
         const double *pl = Pg + (size_t)cl * nitems;
-        const uint32_t i1 = qstart[q + 1];
-        for (uint32_t i = qstart[q]; i < i1; ++i) a = a + pl[qitem[i]];
+        const uint32_t i0 = qstart[q], i1 = qstart[q + 1];
+        double lev[kQLevels];
+        uint32_t g = 0;
+        for (uint32_t i = i0; i < i1; i += kQGroup, ++g) {
+            double sg = pl[qitem[i]];
+            for (uint32_t u = 1; u < kQGroup && i + u < i1; ++u) sg = sg + pl[qitem[i + u]];
+#pragma unroll
+            for (int l = 0; l < kQLevels; ++l) {
+                if ((g >> l) & 1u) {
+                    sg = lev[l] + sg;
+                } else {
+                    lev[l] = sg;
+                    break;
+                }
+            }
+        }
+        bool have = false;
+#pragma unroll
+        for (int l = 0; l < kQLevels; ++l)
+            if ((g >> l) & 1u) {
+                a = have ? lev[l] + a : lev[l];
+                have = true;
+            }
     }
     Q[(size_t)(c0 + cl) * ldQ + q] = a;
 }
@@ -1148,6 +1232,11 @@ struct DevCtx {
     double *e = nullptr, *c = nullptr;
     size_t cap_e = 0, cap_c = 0;
     uint32_t ne = 0, nc = 0;
+    // forward kernels with several points per lane: list positions -> e rows
+    // (bit 31: a duplicate that is computed, not stored), grouped by ratio form
+    uint32_t *plist = nullptr;
+    size_t cap_plist = 0;
+    uint32_t nlist = 0, nlist_epl = 0;  // list length (a multiple of nlist_epl, its points per lane)
     double *ZPV = nullptr, *R = nullptr, *out = nullptr, *gpart = nullptr;
     size_t cap_zpv = 0, cap_r = 0, cap_out = 0, cap_gpart = 0;
     unsigned long long *stamps[3] = {nullptr, nullptr, nullptr};  // k_zpv, k_coefs, k_forward
@@ -1159,6 +1248,7 @@ struct DevCtx {
     double *zc = nullptr;   // Z-row series coefficients [row][kZTerms]
     size_t cap_zc = 0;
     uint2 *items = nullptr;  // per item {B | row << 24, j | (row >> 8) << 24}
+    uint2 *qslot = nullptr;  // k_qrows phase-3 lane table
     uint32_t *itemB = nullptr, *qstart = nullptr, *qitem = nullptr;
     size_t cap_zs = 0, cap_qrow = 0, cap_zg = 0;
     uint32_t zs_len = 0;    // doubles in zs = zs_kmax * nj
@@ -1167,6 +1257,7 @@ struct DevCtx {
     uint32_t ct_len = 0;       // doubles
     uint32_t zs_kmax = 0;   // padded length of the longest pruned row
     uint32_t qrows_cb = 1;  // c values per k_qrows workgroup for this grid
+    bool qrows_attr_set = false;  // k_qrows' LDS limit raised on this device
     double zs_cmax = -1.0;  // c bound the uploaded zs was pruned for (-1: none yet)
     hipModule_t jit_mod[2] = {nullptr, nullptr};  // problem-specialised forward kernel [fused]
     hipFunction_t jit_fn[2] = {nullptr, nullptr};
@@ -1297,6 +1388,7 @@ struct mdp_engine {
     size_t ldP = 0;
     std::vector<uint32_t> cj_bits, cj_item0, itemB, qstart, qitem, udesc_d, var_cols;
     std::vector<uint32_t> itemRow;  // row (j slot) of each item
+    std::vector<uint2> qslot;       // k_qrows phase-3 lanes (build_direct_plan)
     std::vector<uint8_t> isvar;
     std::vector<double> Sj;  // [nj][n] colonisation sums of every column for each needed j
     std::string jit_log;
@@ -1562,6 +1654,33 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
             });
             eng->qstart.push_back((uint32_t)eng->qitem.size());
         }
+    }
+    // k_qrows' phase-3 lane table (the canonical Q-sum order, kQGroup): per
+    // entry q < ldQ an aligned segment of L = min(P, kQLanesMax) lanes, P =
+    // its group count rounded up to a power of two, each lane 2^G = P / L
+    // groups; segments packed largest first, so each is aligned and lies in
+    // one wave; padded to whole waves
+    {
+        const size_t ldq = ((size_t)off + 1) & ~(size_t)1;
+        struct Ent { uint32_t lgL, lgG, q; };
+        std::vector<Ent> ents;
+        for (uint32_t q = 0; q < ldq; ++q) {
+            const uint32_t n = q + 1 < eng->qstart.size() ? eng->qstart[q + 1] - eng->qstart[q] : 0u;
+            const uint32_t ng = std::max<uint32_t>(1u, (n + kQGroup - 1) / kQGroup);
+            uint32_t lgP = 0;
+            while ((1u << lgP) < ng) ++lgP;
+            uint32_t lgL = 0;
+            while ((1u << lgL) < kQLanesMax && lgL < lgP) ++lgL;
+            if (lgP - lgL >= (uint32_t)kQLevelsRows)
+                return mdp_set_error(MDP_EUNSUPPORTED, "a Q entry of %u items (k_qrows' lane table)", n);
+            ents.push_back({lgL, lgP - lgL, q});
+        }
+        std::stable_sort(ents.begin(), ents.end(), [](const Ent &x, const Ent &y) { return x.lgL > y.lgL; });
+        eng->qslot.clear();
+        for (const Ent &en : ents)
+            for (uint32_t le = 0; le < (1u << en.lgL); ++le)
+                eng->qslot.push_back(make_uint2(en.q, le | (en.lgL << 8) | (en.lgG << 12)));
+        while (eng->qslot.size() % 64) eng->qslot.push_back(make_uint2(0xffffffffu, 0u));
     }
     eng->udesc_d.clear();
     for (uint32_t pi : eng->use_pair) {
@@ -1877,7 +1996,7 @@ int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 size_t fused_lds(const mdp_engine *eng, size_t ct_len)
 {
     const size_t fc = (size_t)eng->jit_plan.fused_cols;
-    return (ct_len + 2 + fc * (eng->nj + eng->nitems + eng->ldQ)) * sizeof(double);  // + staging scratch
+    return (ct_len + 2 + fc * (eng->nj + eng->nitems + 2 * eng->ldQ)) * sizeof(double);  // + staging scratch
 }
 
 constexpr size_t kWidePgBytes = 256ull << 20;  // wide path: item-factor chunk
@@ -1897,10 +2016,10 @@ int upload_binomials()  // into the current device's constant bank
     return MDP_OK;
 }
 
-int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
+// The generic path's device tables: colonisation sums S of every state
+// (k_colsum), the binomial table, the pair plans, k_coefs' LDS limit.
+int init_generic(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
 {
-    HIP_TRY(hipSetDevice(d.device));
-    HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     int rc = upload_binomials();
     if (rc) return rc;
     std::vector<uint32_t> var(p->var_cols, p->var_cols + p->nvar), row_col;
@@ -1928,6 +2047,30 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(d.stream));
     (void)hipFree(dM);
+    if (eng->coef_lds > 64 * 1024) {
+        const void *fns[] = {
+            (const void *)k_coefs<true, true, 8>,   (const void *)k_coefs<true, true, 16>,
+            (const void *)k_coefs<true, true, 24>,  (const void *)k_coefs<false, true, 8>,
+            (const void *)k_coefs<false, true, 16>, (const void *)k_coefs<false, true, 24>,
+            (const void *)k_coefs<false, false, 8>, (const void *)k_coefs<false, false, 16>,
+            (const void *)k_coefs<false, false, 24>};
+        for (const void *fn : fns)
+            HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)eng->coef_lds));
+    }
+    return MDP_OK;
+}
+
+int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
+{
+    HIP_TRY(hipSetDevice(d.device));
+    HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    int rc = MDP_OK;
+    // the generic path's tables (k_zpv / k_coefs / k_forward: colonisation
+    // sums of every state, binomials, pair plans) only for an engine that
+    // runs it: the direct and wide paths never touch them, so their set-up
+    // does not load the library's precompiled kernels at all (CLI start-up)
+    if (!eng->jit && !eng->wide && (rc = init_generic(eng, d, p))) return rc;
     if (eng->jit || eng->wide) {
         std::vector<double> sv((size_t)eng->nj * eng->nvar + 1, 0.0);
         for (uint32_t js = 0; js < eng->nj; ++js)
@@ -1943,7 +2086,8 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
         std::vector<uint32_t> qitem = eng->qitem;
         qitem.push_back(0u);
         if ((rc = dev_upload(&d.sv, sv)) || (rc = dev_upload(&d.items, items)) ||
-            (rc = dev_upload(&d.qstart, eng->qstart)) || (rc = dev_upload(&d.qitem, qitem)))
+            (rc = dev_upload(&d.qstart, eng->qstart)) || (rc = dev_upload(&d.qitem, qitem)) ||
+            (rc = dev_upload(&d.qslot, eng->qslot)))
             return rc;
         if (eng->wide) {
             if ((rc = dev_upload(&d.np_d, eng->np)) || (rc = dev_upload(&d.udesc_w, eng->udesc_d))) return rc;
@@ -1951,28 +2095,27 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
                                         (int)wide_lds(eng)));
             return MDP_OK;
         }
-        const size_t lds_max = qrows_lds(eng, kQrowsMaxC);
-        if (lds_max > 64 * 1024)
-            for (const void *fn : {(const void *)k_qrows<8, true, 1>, (const void *)k_qrows<8, false, 1>,
-                                   (const void *)k_qrows<16, false, 1>, (const void *)k_qrows<24, false, 1>,
-                                   (const void *)k_qrows<8, true, 2>, (const void *)k_qrows<8, false, 2>,
-                                   (const void *)k_qrows<16, false, 2>, (const void *)k_qrows<8, true, 4>,
-                                   (const void *)k_qrows<8, false, 4>})
-                HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)std::min(lds_max, kQrowsLdsMax)));
-        if ((rc = jit_load(eng, d, eng->fused_mode == 1))) return rc;
+        // (k_qrows' LDS attribute is set before its first launch and the
+        // forward kernel loaded by set_grid_dev: nothing here loads a module)
     }
-    if (eng->coef_lds > 64 * 1024) {
-        const void *fns[] = {
-            (const void *)k_coefs<true, true, 8>,   (const void *)k_coefs<true, true, 16>,
-            (const void *)k_coefs<true, true, 24>,  (const void *)k_coefs<false, true, 8>,
-            (const void *)k_coefs<false, true, 16>, (const void *)k_coefs<false, true, 24>,
-            (const void *)k_coefs<false, false, 8>, (const void *)k_coefs<false, false, 16>,
-            (const void *)k_coefs<false, false, 24>};
-        for (const void *fn : fns)
+    return MDP_OK;
+}
+
+// k_qrows may take more than 64 KB of dynamic LDS: raise its limit once per
+// device, just before its first launch
+int qrows_attrs(const mdp_engine *eng, DevCtx &d)
+{
+    if (d.qrows_attr_set) return MDP_OK;
+    const size_t lds_max = qrows_lds(eng, kQrowsMaxC);
+    if (lds_max > 64 * 1024)
+        for (const void *fn : {(const void *)k_qrows<8, true, 1>, (const void *)k_qrows<8, false, 1>,
+                               (const void *)k_qrows<16, false, 1>, (const void *)k_qrows<24, false, 1>,
+                               (const void *)k_qrows<8, true, 2>, (const void *)k_qrows<8, false, 2>,
+                               (const void *)k_qrows<16, false, 2>, (const void *)k_qrows<8, true, 4>,
+                               (const void *)k_qrows<8, false, 4>})
             HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)eng->coef_lds));
-    }
+                                        (int)std::min(lds_max, kQrowsLdsMax)));
+    d.qrows_attr_set = true;
     return MDP_OK;
 }
 
@@ -1982,7 +2125,7 @@ void free_device(DevCtx &d)
     void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog,
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
                     d.zs, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
-                    d.Pg, d.V, d.np_d, d.udesc_w, d.zc,
+                    d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -2000,6 +2143,29 @@ void free_device(DevCtx &d)
 // an even count) plus two zero transitions of prefetch padding
 size_t rsp_of(const mdp_engine *eng) { return (eng->deg + 2) & ~1u; }
 size_t ldR_of(const mdp_engine *eng) { return ((size_t)eng->nuses + 2) * rsp_of(eng); }
+
+// The point list of forward kernels with `epl` points per lane: the e rows
+// whose ratio form is s (x < y, x = min(e, 1), y = 1 - x, as the kernel
+// computes them), then those of form t, each run padded to a multiple of epl
+// with duplicates of its last row (bit 31: computed, not stored), so every
+// lane's points share one form and so their coefficient reads.  A sorted
+// grid keeps its order (the kernels' stores stay coalesced).
+std::vector<uint32_t> point_list(const double *e, uint32_t ne, uint32_t epl)
+{
+    std::vector<uint32_t> s_rows, t_rows;
+    for (uint32_t i = 0; i < ne; ++i) {
+        const double x = e[i] > 1.0 ? 1.0 : e[i], y = 1.0 - x;
+        (x >= y ? t_rows : s_rows).push_back(i);
+    }
+    std::vector<uint32_t> pl;
+    pl.reserve(ne + 2 * epl);
+    for (const auto *rows : {&s_rows, &t_rows}) {
+        pl.insert(pl.end(), rows->begin(), rows->end());
+        while (!rows->empty() && pl.size() % epl) pl.push_back(rows->back() | 0x80000000u);
+    }
+    if (pl.empty()) pl.assign(epl, 0x80000000u);
+    return pl;
+}
 
 int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const double *c,
                  uint32_t nc)
@@ -2040,10 +2206,24 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
             d.wide_cb_fwd = std::min(d.wide_cb_fwd, (uint32_t)std::max(1, atoi(cv)));
         if ((rc = dev_reserve(&d.V, &d.cap_v, 2 * (size_t)eng->npmax * d.wide_cb_fwd * ne_pad))) return rc;
     } else if (eng->jit) {
+        // forward kernels with several points per lane read them from a list
+        // that puts only e rows of one ratio form in a lane (spom_jit.cpp)
+        const uint32_t epl_f = eng->jit_shape_env ? (uint32_t)eng->jit_epl : 1u;  // the fused variant's (jit_build)
+        const uint32_t epl_max = std::max<uint32_t>((uint32_t)eng->jit_epl, epl_f);
+        if (epl_max > 1) {
+            const std::vector<uint32_t> pl = point_list(e, ne, epl_max);
+            if ((rc = dev_reserve(&d.plist, &d.cap_plist, pl.size()))) return rc;
+            HIP_TRY(hipMemcpy(d.plist, pl.data(), pl.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            d.nlist = (uint32_t)pl.size();
+        } else {
+            d.nlist = ne;
+        }
+        d.nlist_epl = epl_max;
         // one e block per c column and a small per-c problem: the forward
         // kernel computes its column's Q itself (one launch); never for a
         // chunked series or Q rows built in HBM
-        const uint32_t gy = (ne + eng->jit_kblock * eng->jit_epl - 1) / (eng->jit_kblock * eng->jit_epl);
+        const uint32_t nl = eng->jit_epl > 1 ? d.nlist : ne;
+        const uint32_t gy = (nl + eng->jit_kblock * eng->jit_epl - 1) / (eng->jit_kblock * eng->jit_epl);
         d.fused = eng->chunks.empty() && !eng->qglobal && !eng->jit_plan.vlds && fused_lds(eng, d.ct_len) <= kFusedLdsMax &&
                   d.zs_kmax <= eng->jit_plan.kzmax && (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
         if ((rc = jit_load(eng, d, d.fused))) return rc;
@@ -2136,16 +2316,21 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, OutStrid
         uint32_t ldv = d.ldv;
         const uint32_t *qidx = nullptr;
         uint32_t se = os.se, sc = os.sc;
-        void *args[] = {(void *)&Qrow, (void *)&prior0, (void *)&ev,  (void *)&ne,   (void *)&nc,
-                        (void *)&out,  (void *)&se,     (void *)&one, (void *)&st,   (void *)&cv,
-                        (void *)&ctab, (void *)&ctl,    (void *)&kmax, (void *)&vscr, (void *)&ldv,
-                        (void *)&qidx, (void *)&sc};
         // threads per e block: kb (x 2 with the split state-vector kernel)
         const uint32_t kb = d.fused ? eng->jit_kblock_fused : eng->jit_kblock;
         const uint32_t epl = d.fused ? (uint32_t)eng->jit_epl_fused : (uint32_t)eng->jit_epl;
         const uint32_t spl = eng->jit_plan.vlds && (eng->jit_plan.vsplit == 2 || eng->jit_plan.vsplit == 4)
                                  ? (uint32_t)eng->jit_plan.vsplit : 1u;
-        const uint64_t gy = (d.ne + kb * epl - 1) / (kb * epl);
+        // several points per lane: the grid's point list (set_grid_dev)
+        const uint32_t *plist = epl > 1 ? d.plist : nullptr;
+        uint32_t nlist = epl > 1 ? d.nlist : d.ne;
+        if (epl > 1 && (!plist || d.nlist_epl % epl))
+            return mdp_set_error(MDP_EINVAL, "no point list for %u points per lane", epl);
+        void *args[] = {(void *)&Qrow, (void *)&prior0, (void *)&ev,  (void *)&ne,   (void *)&nc,
+                        (void *)&out,  (void *)&se,     (void *)&one, (void *)&st,   (void *)&cv,
+                        (void *)&ctab, (void *)&ctl,    (void *)&kmax, (void *)&vscr, (void *)&ldv,
+                        (void *)&qidx, (void *)&sc,     (void *)&plist, (void *)&nlist};
+        const uint64_t gy = (nlist + kb * epl - 1) / (kb * epl);
         const uint32_t fc = d.fused ? (uint32_t)eng->jit_plan.fused_cols : 1u;
         const uint64_t nb = gy * ((d.nc + fc - 1) / fc);  // e blocks x column groups
         if (nb * kb * fc * spl > 0xffffffffull)
@@ -2278,6 +2463,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, OutStrides os, h
         return MDP_OK;
     }
     if (eng->jit) {  // k == 1: Q rows
+        if (int rc = qrows_attrs(eng, d)) return rc;
         const uint32_t cb = d.qrows_cb;
         const dim3 grid((d.nc + cb - 1) / cb);
         const size_t lds = qrows_lds(eng, cb);
@@ -2287,7 +2473,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, OutStrides os, h
     MDP_LAUNCH((k_qrows<NV, EX, CB>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, eng->nvar, eng->nj,         \
                d.zs_kmax, d.zs, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
                (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1],                 \
-               (uint32_t)(eng->qrows_xcd ? 1u : 0u)); } while (0)
+               (uint32_t)(eng->qrows_xcd ? 1u : 0u), d.qslot, (uint32_t)eng->qslot.size()); } while (0)
         // c values per workgroup: <= qrows_maxcb(nvar) (register budget at 1024 threads)
         if (eng->nvar == 8) {
             if (cb == 4) MDP_QROWS_CB(8, true, 4);
@@ -2423,6 +2609,7 @@ int plan_chunks(mdp_engine *eng, uint32_t U, bool gather, size_t qlimit)
     eng->chunks.clear();
     uint32_t t0 = 0;
     size_t u0 = 0;
+    uint32_t e0 = 0;  // pending exponent of B at the chunk boundary (spom_jit.cpp)
     while (t0 + 1 < T) {
         size_t cur = 0, qloc = 0, u1 = u0, best_u1 = 0;
         uint32_t t1 = t0, best_t1 = 0;
@@ -2458,6 +2645,8 @@ int plan_chunks(mdp_engine *eng, uint32_t U, bool gather, size_t qlimit)
         c.udesc.assign(ud.begin() + u0, ud.begin() + u1);
         c.first = t0 == 0;
         c.last = t1 + 1 == T;
+        c.e0 = e0;
+        e0 = mdp_jit_end_exp(c);
         if (gather) {  // chunk-local Q layout, groups in first-use order
             std::map<uint32_t, uint32_t> lo;
             c.qidx.clear();
@@ -2556,9 +2745,11 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
         const char *gv = eng->opts.get("MDP_JIT_GATHER");
         // coefficients a forward kernel may stage: what the LDS leaves beside
         // the wide years' state vectors (npmax x 256 lanes) when they are there
-        const size_t qlimit = vlds ? std::min(kJitChunkQ, (kQrowsLdsMax - (size_t)eng->npmax * vkb * sizeof(double) -
-                                                         2048) / sizeof(double))
-                                   : kJitChunkQ;
+        // (halved: the forward kernel keeps each Q row twice, in stored and in
+        // reversed group order -- spom_jit.cpp, the ratio forms)
+        const size_t qlimit = (vlds ? std::min(kJitChunkQ, (kQrowsLdsMax - (size_t)eng->npmax * vkb * sizeof(double) -
+                                                          2048) / sizeof(double))
+                                    : kJitChunkQ) / 2;
         const bool gather = eng->ldQ > qlimit || (gv && atoi(gv) != 0);
         const bool chunked = eng->nuses > kJitMaxUses || gather || (cv && eng->nuses > chunk_uses);
         if (want_jit && eng->nuses > 0) {
@@ -2656,7 +2847,13 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
                 delete eng;
                 return r1 ? r1 : MDP_ENODEV;
             }
-            if ((chunked ? jit_build_chunks(eng) : jit_build(eng, eng->fused_mode == 1)) == MDP_OK) eng->jit = true;
+            // compile now the variant the first grid most likely runs (the
+            // fused kernel wherever its tables fit: every grid of at most one
+            // e block per column takes it), the other on demand (set_grid_dev)
+            const bool fused_first = eng->fused_mode == 1 ||
+                                     (eng->fused_mode == -1 && !vlds && !eng->qglobal &&
+                                      fused_lds(eng, plan.ct_max) <= kFusedLdsMax);
+            if ((chunked ? jit_build_chunks(eng) : jit_build(eng, fused_first)) == MDP_OK) eng->jit = true;
             else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the %s kernels:\n%s\n",
                          vlds ? "wide" : "generic", eng->jit_log.c_str());
         }
@@ -2744,7 +2941,15 @@ int mdp_engine_run(mdp_engine *eng, double *d_out, uint32_t ld_out, void *stream
 int mdp_loglik_grid(mdp_engine *eng, const double *e, uint32_t ne, const double *c, uint32_t nc,
                     double *out)
 {
+    return mdp_loglik_grid_layout(eng, e, ne, c, nc, MDP_LAYOUT_EC, out);
+}
+
+int mdp_loglik_grid_layout(mdp_engine *eng, const double *e, uint32_t ne, const double *c, uint32_t nc, int layout,
+                           double *out)
+{
     if (!eng || !out || (ne && !e) || (nc && !c)) return mdp_set_error(MDP_EINVAL, "null argument");
+    if (layout != MDP_LAYOUT_EC && layout != MDP_LAYOUT_CE) return mdp_set_error(MDP_EINVAL, "unknown layout %d", layout);
+    const bool ce = layout == MDP_LAYOUT_CE;
     const uint32_t nd = (uint32_t)eng->devs.size();
     const uint32_t avg = ne / nd, rem = ne % nd;
     std::vector<uint32_t> r0(nd), r1(nd);
@@ -2756,16 +2961,20 @@ int mdp_loglik_grid(mdp_engine *eng, const double *e, uint32_t ne, const double 
         const uint32_t rows = r1[r] - r0[r];
         if ((rc = set_grid_dev(eng, d, e + r0[r], rows, c, nc))) return rc;
         if ((rc = dev_reserve(&d.out, &d.cap_out, (size_t)rows * nc))) return rc;
-        // [e][c] whatever the engine layout: the host contract of this call
-        if ((rc = run_dev(eng, d, d.out, OutStrides{nc, 1u}, d.stream))) return rc;
+        // the layout asked of this call (not the engine's mdp_engine_run
+        // layout): the slab [e][c] (ld nc) or [c][e] (ld = the slab's rows)
+        if ((rc = run_dev(eng, d, d.out, ce ? OutStrides{1u, rows} : OutStrides{nc, 1u}, d.stream))) return rc;
     }
     for (uint32_t r = 0; r < nd; ++r) {
         DevCtx &d = eng->devs[r];
         const uint32_t rows = r1[r] - r0[r];
         HIP_TRY(hipSetDevice(d.device));
-        if (rows)
+        if (rows && !ce)
             HIP_TRY(hipMemcpyAsync(out + (size_t)r0[r] * nc, d.out, (size_t)rows * nc * sizeof(double),
                                    hipMemcpyDeviceToHost, d.stream));
+        else if (rows && nc)  // the slab's columns into out[c][e] at e offset r0
+            HIP_TRY(hipMemcpy2DAsync(out + r0[r], (size_t)ne * sizeof(double), d.out, (size_t)rows * sizeof(double),
+                                     (size_t)rows * sizeof(double), nc, hipMemcpyDeviceToHost, d.stream));
     }
     for (uint32_t r = 0; r < nd; ++r) {
         HIP_TRY(hipSetDevice(eng->devs[r].device));

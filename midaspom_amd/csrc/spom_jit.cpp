@@ -137,36 +137,150 @@ std::map<uint64_t, std::vector<char>> g_code;  // in-process code-object cache
 
 namespace {
 
-// weight table: every (|A|, m) a transition needs, W = x^{|A|-m} y^m
-int weight_index(const std::vector<uint32_t> &udesc, std::map<std::pair<uint32_t, uint32_t>, int> &widx,
-                 uint32_t &dmax)
+// The transition P[a][b](e, c) = sum_m Q_ab[m](c) x^(|A|-m) y^m (x = min(e, 1),
+// y = 1 - x) is evaluated per point without a weight table, in
+// one of two ratio forms chosen per lane:
+//   t-form (x >= y): P = x^|A| * H_t,              H_t = sum_m Q[m] t^m,      t = y / x <= 1
+//   s-form (x <  y): P = y^|A| * s^(|A|-nX) * H_s, H_s = sum_m Q[m] s^(nX-m), s = x / y <  1
+// Both are one Horner chain of nX FMAs over the group's coefficients -- the
+// s-form reads them in stored order, the t-form reversed (a second, reversed
+// copy of the Q row sits in LDS, so the choice is a per-lane base address).
+// Writing B = x (t) or y (s) and g = 1 (t) or s (s):  P = B^|A| g^(|A|-nX) H.
+// The factor g^d (d = |A| - nX = |A \ B|, the patches forced extinct) is a
+// multiply per transition when d > 0; B^|A| depends only on the source state,
+// so it is deferred: every state of a year carries the same pending exponent
+// E of B (sources of a year with |A| above the year's minimum are scaled by
+// B^(|A| - min) first), applied when E passes kFlushExp and at the end.
+// The deferred values are bounded: H <= sum_m Q[m] <= 2^nX <= 2^|A| with both
+// ratios <= 1 and B >= 1/2 for e in [0, 1] (B > 1 for e < 0, where nothing
+// grows), so a state is at most 2^E np0 times its true value and B^E >= 2^-E.
+constexpr uint32_t kFlushExp = 192;
+
+struct Schedule {
+    std::vector<uint32_t> amin;          // per year t >= 1: min |A| over the year's sources
+    std::vector<std::vector<uint32_t>> diff;  // per year: |A_k| - amin per source k
+    std::vector<uint32_t> flush;         // per year: pending exponent applied after it (0: none)
+    uint32_t final_exp = 0;              // pending exponent at the end of the program
+    uint32_t dp = 0, dg = 0;             // largest source pre-scale and g exponent used
+};
+
+Schedule schedule(const MdpJitPlan &pl)
 {
-    dmax = 0;
-    for (uint32_t d : udesc) {
-        const uint32_t nX = (d >> 22) & 31u, nA = d >> 27;
-        dmax = nA > dmax ? nA : dmax;
-        for (uint32_t m = 0; m <= nX; ++m) widx.emplace(std::make_pair(nA, m), 0);
+    Schedule sc;
+    sc.amin.assign(pl.np.size(), 0);
+    sc.diff.assign(pl.np.size(), {});
+    sc.flush.assign(pl.np.size(), 0);
+    uint32_t E = pl.e0;
+    size_t u = 0;
+    for (size_t t = 1; t < pl.np.size(); ++t) {
+        const uint32_t npp = pl.np[t - 1], npc = pl.np[t];
+        std::vector<uint32_t> a(npp, 0);
+        for (uint32_t l = 0; l < npc; ++l)
+            for (uint32_t k = 0; k < npp; ++k) {
+                const uint32_t d = pl.udesc[u + (size_t)l * npp + k];
+                const uint32_t nX = (d >> 22) & 31u, nA = d >> 27;
+                a[k] = nA;  // a use's |A| is its source's
+                if (nA > nX) sc.dg = std::max(sc.dg, nA - nX);
+            }
+        u += (size_t)npp * npc;
+        const uint32_t am = *std::min_element(a.begin(), a.end());
+        sc.amin[t] = am;
+        for (uint32_t k = 0; k < npp; ++k) {
+            sc.diff[t].push_back(a[k] - am);
+            sc.dp = std::max(sc.dp, a[k] - am);
+        }
+        E += am;
+        if (E >= kFlushExp) {
+            sc.flush[t] = E;
+            E = 0;
+        }
     }
-    int nw = 0;
-    for (auto &kv : widx) kv.second = nw++;
-    return nw;
+    sc.final_exp = E;
+    return sc;
+}
+
+// reversed-copy index of every coefficient slot: within each group (offset,
+// nX + 1 coefficients) slot off + k holds coefficient off + nX - k; slots of
+// no used group map to themselves
+std::vector<uint32_t> reversed_index(const std::vector<uint32_t> &udesc, size_t ldq)
+{
+    std::vector<uint32_t> rev(ldq);
+    for (size_t i = 0; i < ldq; ++i) rev[i] = (uint32_t)i;
+    for (uint32_t d : udesc) {
+        const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u;
+        for (uint32_t k = 0; k <= nX && off + k < ldq; ++k) rev[off + k] = off + nX - k;
+    }
+    return rev;
+}
+
+// B^E (or g^E) for point i as straight-line code: binary powers of `base`
+std::string power_expr(const std::string &base, uint32_t E, const std::string &tmp)
+{
+    if (E == 0) return "1.0";
+    std::ostringstream o;
+    o << "[&]() { double " << tmp << "_s = " << base << ", " << tmp << "_f = 1.0;";
+    bool first = true;
+    for (uint32_t b = E; b; b >>= 1) {
+        if (!first) o << " " << tmp << "_s *= " << tmp << "_s;";
+        if (b & 1u) o << " " << tmp << "_f = " << (first ? tmp + "_s;" : tmp + "_f * " + tmp + "_s;");
+        first = false;
+    }
+    o << " return " << tmp << "_f; }()";
+    return o.str();
 }
 
 }  // namespace
 
-int mdp_jit_default_epl(const std::vector<uint32_t> &udesc)
+// The fused kernel's Q-entry sum in the canonical order of spom_engine.hip
+// (kQGroup = 4: the items in groups of four summed left to right, the group
+// sums as a pairwise tree padded to a power of two, i.e. a binary counter
+// folded from its lowest occupied level up), unrolled for entries of at most
+// qml items; items u < qun come from the preloaded indices qx[k][u], the
+// rest from the CSR in LDS.  Sets `a`.
+std::string qsum_code(uint32_t qml, uint32_t qun)
 {
-    std::map<std::pair<uint32_t, uint32_t>, int> widx;
-    uint32_t dmax;
-    return weight_index(udesc, widx, dmax) <= 64 ? 2 : 1;
+    const uint32_t G = 4, ngm = (qml + G - 1) / G;
+    uint32_t nlev = 1;
+    while ((1u << nlev) <= ngm) ++nlev;
+    std::ostringstream o;
+    auto item = [&](uint32_t u) {
+        return u < qun ? "pl[qx[k][" + std::to_string(u) + "]]" : "pl[Qil[qb[k] + " + std::to_string(u) + "]]";
+    };
+    o << "            const u32 cnt_ = qn[k];\n"
+         "            double a = 0.0, lev_[" << nlev << "];\n";
+    for (uint32_t g = 0; g < ngm; ++g) {
+        o << "            if (" << G * g << "u < cnt_) {\n"
+          << "                double s_ = " << item(G * g) << ";\n";
+        for (uint32_t u = 1; u < G && G * g + u < qml; ++u)
+            o << "                if (" << G * g + u << "u < cnt_) s_ = s_ + " << item(G * g + u) << ";\n";
+        for (uint32_t l = 0; l < nlev; ++l) {
+            if ((g >> l) & 1u) {
+                o << "                s_ = lev_[" << l << "] + s_;\n";
+            } else {
+                o << "                lev_[" << l << "] = s_;\n";
+                break;
+            }
+        }
+        o << "            }\n";
+    }
+    o << "            {\n"
+         "                const u32 ng_ = (cnt_ + " << G - 1 << "u) / " << G << "u;\n"
+         "                bool hv_ = false;\n";
+    for (uint32_t l = 0; l < nlev; ++l)
+        o << "                if ((ng_ >> " << l << ") & 1u) { a = hv_ ? lev_[" << l << "] + a : lev_[" << l
+          << "]; hv_ = true; }\n";
+    o << "            }\n";
+    return o.str();
 }
+
+int mdp_jit_default_epl(const std::vector<uint32_t> &) { return 2; }
+
+uint32_t mdp_jit_end_exp(const MdpJitPlan &plan) { return schedule(plan).final_exp; }
 
 std::string mdp_jit_forward_source(MdpJitPlan &pl)
 {
-    std::map<std::pair<uint32_t, uint32_t>, int> widx;
-    uint32_t dmax = 0;
-    const int nw = weight_index(pl.udesc, widx, dmax);
-    const int EPL = pl.vlds ? (pl.epl == 2 ? 2 : 1) : pl.epl > 0 ? pl.epl : (nw <= 64 ? 2 : 1);
+    const Schedule sch = schedule(pl);
+    const int EPL = pl.vlds ? (pl.epl == 2 ? 2 : 1) : pl.epl > 0 ? pl.epl : 2;
     pl.epl = EPL;
     const uint32_t np0 = pl.np[0];
     uint32_t npmax = 1;
@@ -179,7 +293,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     o << "#define KBLOCK " << (pl.kblock > 0 ? pl.kblock : 256) << "\n";  // threads per column
     o << "#define EPL " << EPL << "\n#define LDQ " << ldq_local << "\n#define LDQG "
       << (gather ? pl.ldq_row : pl.ldQ) << "\n#define NQG " << pl.qidx.size() << "\n#define NPMAX " << npmax
-      << "\n#define DMAX " << dmax << "\n#define NW " << (nw ? nw : 1) << "\n";
+      << "\n#define DP " << sch.dp << "\n#define DG " << sch.dg << "\n";
     // diagnostic phase stamps: s_memtime (slots 0-3) and s_memrealtime (6, 7)
     auto stamp = [&](int slot) {
         if (!pl.diag) return std::string();
@@ -207,14 +321,27 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     // accumulating the new states l with l % SPL == half
     const int SPL = pl.vlds && (pl.vsplit == 2 || pl.vsplit == 4) ? pl.vsplit : 1;
     o << "#define FC " << FC << "\n#define SPL " << SPL << "\n#define NT (KBLOCK * FC * SPL)\n";
+    {   // slot of each coefficient in the reversed copy (see the ratio forms)
+        const std::vector<uint32_t> rev = reversed_index(pl.udesc, ldq_local);
+        o << "__constant__ const " << (ldq_local <= 65536 ? "unsigned short" : "unsigned int") << " REVQ[" << ldq_local + 2
+          << "] = {";
+        std::vector<uint32_t> all = rev;
+        all.push_back((uint32_t)ldq_local);
+        all.push_back((uint32_t)ldq_local + 1);
+        for (size_t q = 0; q < all.size(); ++q) o << (q ? (q % 32 ? "," : ",\n") : "") << all[q];
+        o << "};\n";
+    }
     o << "extern \"C\" __global__ __launch_bounds__(NT) "
       << (pl.wpe > 0 ? "__attribute__((amdgpu_waves_per_eu(" + std::to_string(pl.wpe) + "))) " : std::string())
       << "void mdp_fwd_jit(\n"
          "    const double *__restrict__ Qrow, double prior0, const double *__restrict__ evals, u32 ne, u32 nc,\n"
          "    double *__restrict__ out, u32 ld_out, u32 one, unsigned long long *__restrict__ stamps,\n"
          "    const double *__restrict__ cvals, const double *__restrict__ coltab, u32 ct_len, u32 kmax,\n"
-         "    double *__restrict__ vscr, u32 ldv, const u32 *__restrict__ qidx, u32 out_cs)\n{\n"
-      << "    __shared__ __attribute__((aligned(16))) double Ql[FC * LDQ + 2];\n"
+         "    double *__restrict__ vscr, u32 ldv, const u32 *__restrict__ qidx, u32 out_cs,\n"
+         "    const u32 *__restrict__ plist, u32 nlist)\n{\n"
+         // the Q rows in stored order, then the same rows with every group
+         // reversed (read by t-form lanes; see the ratio forms above)
+      << "    __shared__ __attribute__((aligned(16))) double Ql[2 * FC * LDQ + 2];\n"
       << stamp(6) << stamp(0) <<
          // XCD-aware order: the dispatcher deals blocks round-robin over the 8
          // XCDs, so consecutive logical blocks (adjacent c columns of the
@@ -225,77 +352,99 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          // FC columns per workgroup (fused variant): KBLOCK threads each
          "    const u32 half = threadIdx.x / KBLOCK, tid = threadIdx.x % KBLOCK;\n"
          // (column group, e block): FC columns x KBLOCK*EPL e values per workgroup
-      << (pl.efast ? "    const u32 gy = (ne + KBLOCK * EPL - 1) / (KBLOCK * EPL), ic0 = lb / gy * FC, by = lb % gy;\n"
+      << (pl.efast ? "    const u32 gy = (nlist + KBLOCK * EPL - 1) / (KBLOCK * EPL), ic0 = lb / gy * FC, by = lb % gy;\n"
                    : "    const u32 ncb = (nc + FC - 1) / FC, ic0 = lb % ncb * FC, by = lb / ncb;\n")
       << (SPL > 1 || FC == 1 ? "    const u32 ic = ic0;\n" : "    const u32 ic = ic0 + half;\n")
       << (SPL > 1 ? "    const double *Qh = Ql;\n" : "    const double *Qh = Ql + half * LDQ;\n") <<
-         // this lane's e values: issued first, their latency hides under the prologue
-         "    u32 ie[EPL];\n    double ev[EPL];\n"
+         // this lane's points: issued first, their latency hides under the
+         // prologue.  One point per lane: e row by * KBLOCK + tid.  Several:
+         // list positions pp = by * KBLOCK * EPL + tid * EPL + i, each naming
+         // an e row (plist; bit 31: a duplicate that computes but does not
+         // store), the host's list putting only points of one ratio form in a
+         // lane (set_grid_dev) so that they share their coefficient reads
+         "    u32 ie[EPL], pp[EPL];\n    bool st[EPL];\n    double ev[EPL];\n"
          "#pragma unroll\n"
          "    for (int i = 0; i < EPL; ++i) {\n"
-         "        ie[i] = by * (KBLOCK * EPL) + i * KBLOCK + tid;\n"
-         "        ev[i] = ie[i] < ne ? evals[ie[i]] : 0.0;\n"
+      << (EPL == 1 ? "        pp[i] = by * KBLOCK + tid;\n"
+                     "        ie[i] = pp[i];\n"
+                     "        st[i] = ie[i] < ne;\n"
+                   : "        pp[i] = by * (KBLOCK * EPL) + tid * EPL + i;\n"
+                     "        const u32 q_ = pp[i] < nlist ? plist[pp[i]] : 0x80000000u;\n"
+                     "        ie[i] = q_ & 0x7fffffffu;\n"
+                     "        st[i] = !(q_ >> 31) && ie[i] < ne;\n")
+      << "        ev[i] = ie[i] < ne ? evals[ie[i]] : 0.0;\n"
          "    }\n";
-    // per point: the weight table W[|A|][m] = x^(|A|-m) y^m and the state
-    // vector (emitted before the final prologue barrier; placing it between
-    // the table loads and stores made no difference: the compiler sinks it)
+    // per point: the ratio form (lane-uniform), the ratio z, the deferred
+    // base B, g, and the power tables bp[k] = B^k (source pre-scales, k <= DP)
+    // and gp[d] = g^d (d <= DG); then the state vector (emitted before the
+    // final prologue barrier)
     std::string wblock;
     {
         std::ostringstream w;
         w << "#pragma unroll\n"
              "    for (int i = 0; i < EPL; ++i) {\n"
              "        const double e = ev[i];\n"
-             "        const double x = e > 1.0 ? 1.0 : e;\n"
-             "        const double y = 1.0 - x;\n"
-             "        double xp[DMAX + 1], yp[DMAX + 1];\n        xp[0] = 1.0;\n        yp[0] = 1.0;\n"
-             "#pragma unroll\n        for (int r = 1; r <= DMAX; ++r) { xp[r] = xp[r - 1] * x; yp[r] = yp[r - 1] * y; }\n";
-        for (auto &kv : widx)
-            w << "        W[i][" << kv.second << "] = xp[" << (kv.first.first - kv.first.second) << "] * yp["
-              << kv.first.second << "];\n";
+             "        xx[i] = e > 1.0 ? 1.0 : e;\n"
+             "        yy[i] = 1.0 - xx[i];\n"
+             "    }\n"
+             // every point of a lane has one form (the host list), so point 0 decides
+             "    const bool tf = xx[0] >= yy[0];\n"
+             "    const double *Qp = Qh + (tf ? FC * LDQ : 0);\n"
+             "#pragma unroll\n"
+             "    for (int i = 0; i < EPL; ++i) {\n"
+             "        const double num = tf ? yy[i] : xx[i], den = tf ? xx[i] : yy[i];\n"
+             "        zz[i] = num / den;\n"
+             "        bb[i] = den;\n"
+             "        const double g = tf ? 1.0 : zz[i];\n"
+             "        bp[i][0] = 1.0;\n"
+             "        gp[i][0] = 1.0;\n"
+             "#pragma unroll\n        for (int r = 1; r <= DP; ++r) bp[i][r] = bp[i][r - 1] * den;\n"
+             "#pragma unroll\n        for (int r = 1; r <= DG; ++r) gp[i][r] = gp[i][r - 1] * g;\n";
         const char *vdst = pl.vlds ? "Vl[(k * EPL + i) * KBLOCK + tid]" : "v[i][k]";
         // (split: the state k set by wave group k % SPL)
         const char *kloop = SPL > 1 ? "#pragma unroll\n        for (int k = half; k < NPMAX; k += SPL) "
                                     : "#pragma unroll\n        for (int k = 0; k < NPMAX; ++k) ";
         if (pl.first)
             w << kloop << vdst << " = k < " << np0 << " ? 1.0 : 0.0;\n";
-        else  // the previous chunk's end vector (ldv covers every lane's e)
-            w << kloop << vdst << " = k < " << np0 << " ? vscr[((size_t)k * nc + ic) * ldv + ie[i]] : 0.0;\n";
+        else  // the previous chunk's end vector (ldv covers every lane's list position)
+            w << kloop << vdst << " = k < " << np0 << " ? vscr[((size_t)k * nc + ic) * ldv + pp[i]] : 0.0;\n";
         w << "    }\n";
         wblock = w.str();
     }
-    o << "    double W[EPL][NW];\n    double v[EPL][NPMAX];\n    double n[EPL][(NPMAX + SPL - 1) / SPL];\n";
+    o << "    double xx[EPL], yy[EPL], zz[EPL], bb[EPL], bp[EPL][DP + 1], gp[EPL][DG + 1];\n"
+         "    double v[EPL][NPMAX];\n    double n[EPL][(NPMAX + SPL - 1) / SPL];\n";
     if (pl.vlds)  // wide years: state k of point i of lane tid at Vl[k][i][tid]
         o << "    __shared__ double Vl[NPMAX * EPL * KBLOCK];\n";
     // the state k of point i, as an expression
     auto vref = [&](uint32_t k) {
         return pl.vlds ? "Vl[(" + std::to_string(k) + " * EPL + i) * KBLOCK + tid]" : "v[i][" + std::to_string(k) + "]";
     };
-    // stage n (compile-time, even) doubles from src (16-byte aligned) into the
-    // LDS array dst, which has a double2 of scratch past n: every load is
-    // issued before any store, and the stores are unconditional, so the
-    // compiler cannot sink each load into its own guarded store (that
-    // serialised the staging into one global round trip per load)
-    auto stage = [&](const char *dst, const char *src, const char *n) {
+    if (!pl.fused && !gather) {
+        // this column's Q row (k_qrows), in stored order and, through REVQ,
+        // with every group reversed: every load in flight before the
+        // (unconditional, past the end into a scratch slot) stores, as in stage()
         o << "    {\n"
-             "        const double2 *src_ = (const double2 *)(" << src << ");\n"
-             "        double2 *dst_ = (double2 *)" << dst << ";\n"
-             "        constexpr u32 N2 = (" << n << ") / 2, NK = (N2 + NT - 1) / NT;\n"
+             "        const double2 *src_ = (const double2 *)(Qrow + (size_t)ic * LDQ);\n"
+             "        double2 *dst_ = (double2 *)Ql;\n"
+             "        constexpr u32 N2 = LDQ / 2, NK = (N2 + NT - 1) / NT;\n"
              "        double2 t_[NK];\n"
+             "        u32 r0_[NK], r1_[NK];\n"
              "#pragma unroll\n"
              "        for (u32 k = 0; k < NK; ++k) {\n"
              "            const u32 i = threadIdx.x + k * NT;\n"
              "            t_[k] = src_[i < N2 ? i : 0];\n"
+             "            r0_[k] = i < N2 ? LDQ + REVQ[2 * i] : 2 * LDQ;\n"
+             "            r1_[k] = i < N2 ? LDQ + REVQ[2 * i + 1] : 2 * LDQ;\n"
              "        }\n"
              "#pragma unroll\n"
              "        for (u32 k = 0; k < NK; ++k) {\n"
              "            const u32 i = threadIdx.x + k * NT;\n"
-             "            dst_[i < N2 ? i : N2] = t_[k];\n"
+             "            dst_[i < N2 ? i : LDQ] = t_[k];\n"
+             "            Ql[r0_[k]] = t_[k].x;\n"
+             "            Ql[r1_[k]] = t_[k].y;\n"
              "        }\n"
-             "    }\n";
-    };
-    if (!pl.fused && !gather) {
-        stage("Ql", "Qrow + (size_t)ic * LDQ", "LDQ");  // this column's Q row (k_qrows)
-        o << stamp(1);
+             "    }\n"
+          << stamp(1);
     } else if (!pl.fused) {
         // this chunk's coefficients gathered from the column's Q row: every
         // load in flight before the (unconditional) stores, as in stage()
@@ -314,7 +463,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "#pragma unroll\n"
              "        for (u32 k = 0; k < NK; ++k) {\n"
              "            const u32 i = threadIdx.x + k * NT;\n"
-             "            Ql[i < NQG ? i : LDQ] = t_[k];\n"
+             "            Ql[i < NQG ? i : 2 * LDQ] = t_[k];\n"
+             "            Ql[i < NQG ? LDQ + REVQ[i] : 2 * LDQ] = t_[k];\n"
              "        }\n"
              "    }\n"
           << stamp(1);
@@ -475,31 +625,28 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        const u32 w = threadIdx.x + k * NT;\n"
              "        if (w < FC * LDQ) {\n"
              "            const double *pl = Pl + (w / LDQ) * NITEMS;\n"
-             "            double a = 0.0;\n"
-             "#pragma unroll\n"
-             "            for (int u = 0; u < QUN; ++u) {\n"
-             "                const double pv = (u32)u < qn[k] ? pl[qx[k][u]] : 0.0;\n"
-             "                a = (u32)u < qn[k] ? a + pv : a;\n"
-             "            }\n"
-             "#if QML > QUN\n"
-             "            for (u32 i = qb[k] + QUN; i < qb[k] + qn[k]; ++i) a += pl[Qil[i]];\n"
-             "#endif\n"
+          << qsum_code(std::max<uint32_t>(1u, pl.qmaxlen), std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)) <<
              "            Ql[w] = a;\n"
+             "            Ql[FC * LDQ + (w / LDQ) * LDQ + REVQ[w % LDQ]] = a;\n"
              "        }\n"
              "    }\n";
     }
     o << wblock;
     o << "    __syncthreads();\n"
       << stamp(2);
-    // P = sum_m Q[off+m] W[|A|][m] as an expression for point i
-    auto pexpr = [&](uint32_t d) {
-        const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u, nA = d >> 27;
-        std::string e = "Qh[" + std::to_string(off) + "] * W[i][" +
-                        std::to_string(widx[std::make_pair(nA, 0u)]) + "]";
-        for (uint32_t m = 1; m <= nX; ++m)
-            e = "fma(Qh[" + std::to_string(off + m) + "], W[i][" +
-                std::to_string(widx[std::make_pair(nA, m)]) + "], " + e + ")";
+    // H for point i: the Horner chain of a Q group (offset, nX) over the
+    // lane's copy of the coefficients (stored order for s-form lanes,
+    // reversed for t-form ones).  Transitions of one group (same A & B and B)
+    // from sources of different |A| share H and differ only in g^d.
+    auto hexpr = [&](uint32_t d) {
+        const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u;
+        std::string e = "Qp[" + std::to_string(off) + "]";
+        for (uint32_t m = 1; m <= nX; ++m) e = "fma(" + e + ", zz[i], Qp[" + std::to_string(off + m) + "])";
         return e;
+    };
+    auto gfac = [&](uint32_t d) {
+        const uint32_t nX = (d >> 22) & 31u, nA = d >> 27;
+        return nA > nX ? " * gp[i][" + std::to_string(nA - nX) + "]" : std::string();
     };
     // Regions are separate basic blocks: each guard value passes through an
     // opaque scalar move, so instruction selection can neither merge regions
@@ -541,52 +688,67 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             ub += (size_t)npp * npc;
         }
     }
-    // Transition cache: a use whose pair (same descriptor = same P) recurs
-    // within kHorizon of its group's uses keeps its P in one of pl.slots
-    // registers; later uses read it.  Slots are evicted farthest-next-use
-    // first.  The P values are computed exactly as inline, so results do not
-    // change.  Positions count within the use's wave group.
+    // Transition cache: a use whose Q group (same offset = same H) recurs
+    // within kHorizon of its wave group's uses keeps its H in one of
+    // pl.slots registers; later uses read it.  Slots are evicted
+    // farthest-next-use first.  H is computed exactly as inline, so results
+    // do not change.  Positions count within the use's wave group.
     const size_t kHorizon = 64;
+    const uint32_t kOffM = (1u << 22) - 1u;
     std::vector<int> grp(nu, 0);
     std::vector<size_t> pos(nu, 0), next_pos(nu, SIZE_MAX);
     for (int h = 0; h < SPL; ++h) {
         std::map<uint32_t, size_t> last;
         for (size_t p = seq[h].size(); p-- > 0;) {
             const size_t u = seq[h][p];
+            const uint32_t key = pl.udesc[u] & kOffM;
             grp[u] = h;
             pos[u] = p;
-            auto it = last.find(pl.udesc[u]);
+            auto it = last.find(key);
             if (it != last.end()) next_pos[u] = it->second;
-            last[pl.udesc[u]] = p;
+            last[key] = p;
         }
     }
-    // flops per point: weight table, transitions (below), prior sum
-    double flops = 2.0 * dmax + (double)nw + (pl.last ? 2.0 * npmax : 0.0);
+    // flops per point: the ratio and its power tables, transitions and
+    // scalings (below), the prior sum
+    double flops = 2.0 + (double)sch.dp + (double)sch.dg + (pl.last ? 2.0 * npmax : 0.0);
     std::vector<std::vector<uint32_t>> slot_key(SPL, std::vector<uint32_t>(nslot, 0));
     std::vector<std::vector<size_t>> slot_next(SPL, std::vector<size_t>(nslot, SIZE_MAX));  // SIZE_MAX: free / dead
-    // returns the expression for use u, emitting "pc[i][s] = P;" first when
-    // the use fills a slot (inside the caller's per-point loop)
+    // returns the expression for use u (H times its g^d), emitting
+    // "pc[i][s] = H;" first when the use fills a slot (inside the caller's
+    // per-point loop)
     auto use_expr = [&](size_t u, std::string &pre) -> std::string {
-        const uint32_t d = pl.udesc[u];
+        const uint32_t d = pl.udesc[u], key = d & kOffM;
         const size_t p = pos[u], np_ = next_pos[u];
         std::vector<uint32_t> &skey = slot_key[grp[u]];
         std::vector<size_t> &snext = slot_next[grp[u]];
+        const std::string g = gfac(d);
+        if (!g.empty()) flops += 1.0;
         for (int sl = 0; sl < nslot; ++sl)
-            if (snext[sl] == p && skey[sl] == d) {
+            if (snext[sl] == p && skey[sl] == key) {
                 snext[sl] = np_;
-                return "pc[i][" + std::to_string(sl) + "]";
+                return "(pc[i][" + std::to_string(sl) + "]" + g + ")";
             }
-        flops += 2.0 * ((d >> 22) & 31u) + 1.0;  // nX FMAs + 1 MUL
-        const std::string e = pexpr(d);
-        if (nslot == 0 || np_ == SIZE_MAX || np_ - p > kHorizon) return "(" + e + ")";
+        flops += 2.0 * ((d >> 22) & 31u);  // nX FMAs
+        const std::string e = hexpr(d);
+        if (nslot == 0 || np_ == SIZE_MAX || np_ - p > kHorizon) return "((" + e + ")" + g + ")";
         int best = 0;
         for (int sl = 1; sl < nslot; ++sl)
             if (snext[sl] > snext[best]) best = sl;
-        if (snext[best] != SIZE_MAX && snext[best] <= np_) return "(" + e + ")";
-        skey[best] = d;
+        if (snext[best] != SIZE_MAX && snext[best] <= np_) return "((" + e + ")" + g + ")";
+        skey[best] = key;
         snext[best] = np_;
         pre = "pc[i][" + std::to_string(best) + "] = " + e + "; ";
-        return "pc[i][" + std::to_string(best) + "]";
+        return "(pc[i][" + std::to_string(best) + "]" + g + ")";
+    };
+    // a year after which the pending exponent is applied: its new states
+    // times B^E (one factor per point)
+    auto flush_factor = [&](size_t t) { return power_expr("bb[i]", sch.flush[t], "fl"); };
+    // source k of year t, scaled by B^(|A_k| - the year's minimum) where that
+    // is not 0 (the register kernel scales in place before the year instead)
+    auto src = [&](size_t t, uint32_t k) {
+        const uint32_t df = sch.diff[t][k];
+        return pl.vlds && df ? "(" + vref(k) + " * bp[i][" + std::to_string(df) + "])" : vref(k);
     };
     size_t u = 0;
     for (size_t t = 1; t < pl.np.size(); ++t) {
@@ -596,9 +758,19 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             const std::string e = use_expr(u++, pre);
             o << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
             flops += 1.0;
+            if (sch.flush[t]) {
+                o << "    for (int i = 0; i < EPL; ++i) v[i][0] *= " << flush_factor(t) << ";\n";
+                flops += 1.0;
+            }
             fence();
             continue;
         }
+        if (!pl.vlds)
+            for (uint32_t k = 0; k < npp; ++k)
+                if (sch.diff[t][k]) {
+                    o << "    for (int i = 0; i < EPL; ++i) v[i][" << k << "] *= bp[i][" << sch.diff[t][k] << "];\n";
+                    flops += 1.0;
+                }
         if (pl.vlds) {
             // states in LDS: wave group h accumulates the new states l = h,
             // h + SPL, ... (a wave-uniform branch when split), source-major;
@@ -620,8 +792,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                         std::string pre;
                         const std::string e = use_expr(ubase + (size_t)l * npp + k, pre);
                         const std::string acc = "n[i][" + std::to_string(l / SPL) + "]";
-                        o << "    for (int i = 0; i < EPL; ++i) { " << pre << acc << " = fma(" << vref(k) << ", " << e
+                        o << "    for (int i = 0; i < EPL; ++i) { " << pre << acc << " = fma(" << src(t, k) << ", " << e
                           << ", " << (k ? acc : std::string("0.0")) << "); }\n";
+                        flops += sch.diff[t][k] ? 1.0 : 0.0;
                         flops += k ? 2.0 : 1.0;
                         fence();
                     }
@@ -629,13 +802,17 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             }
             if (split) o << "    }\n    __syncthreads();\n";
             o << "    for (int i = 0; i < EPL; ++i) {\n";
+            if (sch.flush[t]) {
+                o << "        const double fl_ = " << flush_factor(t) << ";\n";
+                flops += 1.0 + npc;
+            }
             for (int h = 0; h < SPL; ++h) {
                 if (split)
                     o << (h == 0 ? std::string("        if (half == 0) {\n")
                           : h + 1 < SPL ? "        } else if (half == " + std::to_string(h) + ") {\n"
                                         : std::string("        } else {\n"));
                 for (uint32_t l = h; l < npc; l += SPL)
-                    o << "            " << vref(l) << " = n[i][" << l / SPL << "];\n";
+                    o << "            " << vref(l) << " = n[i][" << l / SPL << "]" << (sch.flush[t] ? " * fl_" : "") << ";\n";
             }
             o << (split ? "        }\n    }\n    __syncthreads();\n" : "    }\n");
             if (split) {
@@ -659,9 +836,19 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         // the final sum runs over the last year's states), so they are not
         // zeroed: that was ~5 % of the forward's VALU issue on config 3
         o << "    for (int i = 0; i < EPL; ++i) {\n";
-        for (uint32_t l = 0; l < npc; ++l) o << "        " << vref(l) << " = n[i][" << l << "];\n";
+        if (sch.flush[t]) {
+            o << "        const double fl_ = " << flush_factor(t) << ";\n";
+            flops += 1.0 + npc;
+        }
+        for (uint32_t l = 0; l < npc; ++l)
+            o << "        " << vref(l) << " = n[i][" << l << "]" << (sch.flush[t] ? " * fl_" : "") << ";\n";
         o << "    }\n";
     }
+    // the pending exponent at the end: applied to L (last chunk); a chunk
+    // that is not the last hands its states over unscaled (the next one
+    // starts from this exponent, plan.e0)
+    const std::string fin = power_expr("bb[i]", sch.final_exp, "fe");
+    if (sch.final_exp && pl.last) flops += 1.0;
     o << "    }}\n" << stamp(3) << "#define NPLAST " << pl.np.back() << "\n"
       << (pl.vlds ? "#define VREF(l) Vl[((l) * EPL + i) * KBLOCK + tid]\n" : "#define VREF(l) v[i][l]\n");
     if (pl.last && (pl.hack == 1 || pl.hack == 2))  // measurement only: the result is never stored
@@ -670,9 +857,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        double L = 0.0;\n"
              "#pragma unroll\n"
              "        for (int l = 0; l < NPLAST; ++l) L += VREF(l) * prior0;\n"
-          << (pl.hack == 1 ? "        if (L == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = log(L);\n"
-                           : "        const double lg_ = LOGF(L);\n"
-                             "        if (lg_ == 1234.5678 && ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = lg_;\n")
+          << (pl.hack == 1 ? "        if (L == 1234.5678 && st[i] && ic < nc) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = log(L);\n"
+                           : "        const double lg_ = LOGF(L * " + fin + ");\n"
+                             "        if (lg_ == 1234.5678 && st[i] && ic < nc) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = lg_;\n")
           << "    }\n";
     else if (pl.last)
         o << "    if (SPL == 1 || half == 0) {\n"
@@ -681,16 +868,18 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        double L = 0.0;\n"
              "#pragma unroll\n"
              "        for (int l = 0; l < NPLAST; ++l) L += VREF(l) * prior0;\n"
-             "        if (ie[i] < ne && ic < nc) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = LOGF(L);\n"
+          << (sch.final_exp ? "        L *= " + fin + ";\n" : std::string()) <<
+             "        if (st[i] && ic < nc) out[(size_t)ie[i] * ld_out + (size_t)ic * out_cs] = LOGF(L);\n"
              "    }\n"
              "    }\n";
     else  // hand the end vector to the next chunk
         o << "    if (ic < nc) {\n"
              "#pragma unroll\n"
-             "        for (int i = 0; i < EPL; ++i)\n"
+             "        for (int i = 0; i < EPL; ++i) {\n"
              "#pragma unroll\n"
              "            for (int l = 0; l < NPLAST; ++l)\n"
-             "                if (SPL == 1 || l % SPL == (int)half) vscr[((size_t)l * nc + ic) * ldv + ie[i]] = VREF(l);\n"
+             "                if (SPL == 1 || l % SPL == (int)half) vscr[((size_t)l * nc + ic) * ldv + pp[i]] = VREF(l);\n"
+             "        }\n"
              "    }\n";
     o << stamp(7) << "}\n";
     pl.flops_pt = flops;

@@ -49,6 +49,10 @@ struct MdpJitPlan {
     // first reads its start vector from the scratch vscr[state][c][e], one
     // that is not the last stores its end vector there instead of the output
     bool first = true, last = true;
+    // the ratio forms' pending exponent of B at the chunk's start (the whole
+    // series' schedule, so a chunked run does the one-kernel run's arithmetic
+    // and hands over the same unscaled states: bit-identical results)
+    uint32_t e0 = 0;
     // gather staging: Ql[i] = Qrow[qidx[i]] (udesc offsets are then into
     // this chunk's own layout); empty: the whole Q row of ldQ doubles
     std::vector<uint32_t> qidx;
@@ -58,6 +62,10 @@ struct MdpJitPlan {
 // Grid points per lane for a program of these uses (2, or 1 when the weight
 // table is large); chunks of one series share it, as they share a scratch.
 int mdp_jit_default_epl(const std::vector<uint32_t> &udesc);
+
+// The pending exponent of B after the plan's years, starting from plan.e0
+// (the next chunk's e0).
+uint32_t mdp_jit_end_exp(const MdpJitPlan &plan);
 
 // HIP source of `mdp_fwd_jit` for this plan; sets plan.epl when it was 0.
 std::string mdp_jit_forward_source(MdpJitPlan &plan);

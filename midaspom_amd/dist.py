@@ -46,6 +46,31 @@ def gather_rows(local, rank: int, world: int, s: int, nc: int, device=None):
     return full
 
 
+def gather_cols(local, rank: int, world: int, s: int, nc: int, device=None):
+    """The same single gather for slabs in the devices' native [c][e] layout
+    (torch tensor [nc, rows], float64: rank r's e rows are its columns).
+    Returns on rank 0 the transposed view of the full [nc, s] array -- indexed
+    [ie][ic] like gather_rows' result; log_total / write_posterior read it in
+    place -- and None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    avg, rem = divmod(s, world)
+    cap = avg + rem
+    dev = local.device if device is None else device
+    buf = torch.zeros((nc, cap), dtype=torch.float64, device=dev)
+    buf[:, : local.shape[1]] = local
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, parts, dst=0)
+    if rank != 0:
+        return None
+    full = np.empty((nc, s), dtype=np.float64)
+    for r in range(world):
+        r0, r1 = row_slab(r, world, s)
+        full[:, r0:r1] = parts[r][:, : r1 - r0].cpu().numpy()
+    return full.T
+
+
 def distributed_loglik(e, c, rank: int, world: int,
                        compute: Callable[[np.ndarray, np.ndarray], object], device=None):
     """Each rank computes its slab with `compute(e_slab, c)` (a torch tensor
@@ -75,18 +100,20 @@ def under_launcher() -> bool:
 
 def gpu_slab_compute(model, device_index: int):
     """compute(e_slab, c) on this rank's GPU through the C ABI; the result
-    stays in HBM (a torch tensor) until the gather."""
+    stays in HBM (a torch tensor [nc, rows]: the [c][e] layout the kernels
+    store fastest, MDP_LAYOUT_CE) until the gather (gather_cols)."""
     import torch
 
     import midaspom_amd as mdp
 
     eng = mdp.Engine(model, devices=[device_index])
+    eng.set_layout("ce")
 
     def compute(e_slab, c):
-        out = torch.empty((len(e_slab), len(c)), dtype=torch.float64, device=f"cuda:{device_index}")
+        out = torch.empty((len(c), len(e_slab)), dtype=torch.float64, device=f"cuda:{device_index}")
         if len(e_slab):
             eng.set_grid(e_slab, c)
-            eng.run(out.data_ptr(), len(c), torch.cuda.current_stream(device_index).cuda_stream)
+            eng.run(out.data_ptr(), len(e_slab), torch.cuda.current_stream(device_index).cuda_stream)
         return out
 
     compute.engine = eng

@@ -67,6 +67,43 @@ def test_gloo_gather_matches_single_process(golden, tmp_path, world):
     assert np.array_equal(got, ref)
 
 
+def _ce_worker(rank, world, port, inp, s, outdir):
+    """The drop-in's device layout: each rank's slab as [c][e] columns
+    (gather_cols), exactly what gpu_slab_compute leaves in HBM."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(ROOT))
+    import oracle
+    from midaspom_amd import dist as md
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    om = oracle.OracleModel.load(inp, 400.0, 0.5, 100.0)
+    g, win = oracle.grid(s)
+    r0, r1 = md.row_slab(rank, world, s)
+    slab = om.loglik_grid(g[r0:r1], g, threads=1)              # [rows][c]
+    local = torch.from_numpy(np.ascontiguousarray(slab.T))   # [c][rows]
+    full = md.gather_cols(local, rank, world, s, s)
+    if rank == 0:
+        assert full.shape == (s, s) and full.T.flags.c_contiguous
+        np.save(os.path.join(outdir, "full.npy"), np.ascontiguousarray(full))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_gather_cols_matches_single_process(golden, tmp_path, world):
+    """[c][e] slabs gathered in one collective give the single-process grid
+    (as its transposed view), bit for bit."""
+    import oracle
+    s = 11
+    inp = str(golden / "config2_64x50.txt")
+    mp.spawn(_ce_worker, args=(world, _free_port(), inp, s, str(tmp_path)), nprocs=world, join=True)
+    got = np.load(tmp_path / "full.npy")
+    om = oracle.OracleModel.load(inp)
+    g, _ = oracle.grid(s)
+    assert np.array_equal(got, om.loglik_grid(g, g, threads=1))
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 @pytest.mark.parametrize("nsimul", [1, 7, 10000])
 def test_replicate_ranges_partition(world, nsimul):
