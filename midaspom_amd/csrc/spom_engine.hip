@@ -339,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
 // occupied levels from the lowest up gives exactly that tree; so does a
 // butterfly of xor shuffles over an aligned power-of-two lane segment
 // holding the sums of aligned power-of-two blocks of groups (k_qrows).
-constexpr uint32_t kQGroup = 4;
+constexpr uint32_t kQGroup = 8;  // config 3: 808 lanes, one pass of k_qrows, <= 3 shuffle levels
 constexpr int kQLevels = 24;
 constexpr uint32_t kQLanesMax = 64;  // k_qrows: lanes per entry (a power of two, <= a wave)
 constexpr int kQLevelsRows = 16;     // k_qrows: groups per lane <= 2^(kQLevelsRows - 1)
@@ -352,11 +352,15 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     uint32_t kmax, const double *__restrict__ zsT, const double *__restrict__ zc, const double *__restrict__ sv,
     uint32_t nitems, const uint2 *__restrict__ items, uint32_t ncoef, const uint32_t *__restrict__ qstart,
     uint32_t nqi, const uint32_t *__restrict__ qitem, double *__restrict__ Q, uint32_t ldQ,
-    unsigned long long *__restrict__ stamps, uint32_t xcd, const uint2 *__restrict__ qslot, uint32_t nslot)
+    unsigned long long *__restrict__ stamps, uint32_t xcd, const uint2 *__restrict__ qslot, uint32_t nslot,
+    uint32_t lglmax)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     MDP_RSTAMP(stamps, 6);
     MDP_STAMP(stamps, 0);
+    // phase 3's lane table does not depend on c: its first pass is loaded
+    // now, its latency hidden under phases 0-2
+    const uint2 sd0 = threadIdx.x < nslot ? qslot[threadIdx.x] : make_uint2(0xffffffffu, 0u);
     // XCD-aware: workgroups are dealt round-robin over the 8 XCDs, so XCD x
     // takes a contiguous eighth of the c range -- the columns the forward
     // kernel's XCD-aware order gives XCD x -- and the forward reads these Q
@@ -539,7 +543,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // entry's whole item list (35 on config 3).
     for (uint32_t s0 = 0; s0 < nslot; s0 += kQrowsBlock) {
         const uint32_t sl = s0 + threadIdx.x;
-        const uint2 sd = sl < nslot ? qslot[sl] : make_uint2(0xffffffffu, 0u);
+        const uint2 sd = s0 == 0 ? sd0 : sl < nslot ? qslot[sl] : make_uint2(0xffffffffu, 0u);
         const uint32_t q = sd.x, le = sd.y & 0xffu, lgL = (sd.y >> 8) & 0xfu, lgG = (sd.y >> 12) & 0xfu;
         double a[CB];
 #pragma unroll
@@ -594,8 +598,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         }
         // every lane of the wave takes part in every shuffle; a lane adds
         // only the levels inside its entry's segment
-#pragma unroll
-        for (uint32_t lv = 0; (1u << lv) < kQLanesMax; ++lv)
+        for (uint32_t lv = 0; lv < lglmax; ++lv)  // lglmax: the widest segment's levels (uniform)
 #pragma unroll
             for (int i = 0; i < CB; ++i) {
                 const double o = __shfl_xor(a[i], 1 << lv);
@@ -1237,6 +1240,7 @@ struct DevCtx {
     uint32_t *plist = nullptr;
     size_t cap_plist = 0;
     uint32_t nlist = 0, nlist_epl = 0;  // list length (a multiple of nlist_epl, its points per lane)
+    bool plist_identity = true;          // the list is 0, 1, ... (nothing uploaded; plist passed as null)
     double *ZPV = nullptr, *R = nullptr, *out = nullptr, *gpart = nullptr;
     size_t cap_zpv = 0, cap_r = 0, cap_out = 0, cap_gpart = 0;
     unsigned long long *stamps[3] = {nullptr, nullptr, nullptr};  // k_zpv, k_coefs, k_forward
@@ -1297,7 +1301,7 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT", "MDP_FUSED", "MDP_FUSED_COLS", "MDP_EPL", "MDP_JIT_SLOTS", "MDP_JIT_WINDOW", "MDP_JIT_XCD",
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
-    "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE"};
+    "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_FUSED_SBUILD"};
 const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
@@ -1368,8 +1372,9 @@ struct mdp_engine {
     // same 512 e rows per block as 256 x 2, so the grid shape is shared): with
     // one point per lane its 1 024-thread blocks fit 4 waves per SIMD, and the
     // per-column prologue runs over twice the threads (config 2: -2 to -3 %)
-    int jit_epl_fused = 1;
+    int jit_epl_fused = 2;
     uint32_t jit_kblock_fused = kBlock;
+    uint32_t jit_pro_fused = 2;
     bool jit_shape_env = false;  // MDP_EPL / MDP_JIT_KBLOCK set: one shape for both variants
     double jit_flops_pt = 0;  // its FP64 flops per grid point (counted by the generator)
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
@@ -1389,8 +1394,10 @@ struct mdp_engine {
     std::vector<uint32_t> cj_bits, cj_item0, itemB, qstart, qitem, udesc_d, var_cols;
     std::vector<uint32_t> itemRow;  // row (j slot) of each item
     std::vector<uint2> qslot;       // k_qrows phase-3 lanes (build_direct_plan)
+    uint32_t qslot_lglmax = 0;      // log2 of the widest lane segment
     std::vector<uint8_t> isvar;
     std::vector<double> Sj;  // [nj][n] colonisation sums of every column for each needed j
+    std::vector<double> Mv;  // [nvar][n] dispersal rows of the var columns
     std::string jit_log;
     size_t coef_lds = 0;      // k_coefs dynamic LDS bytes
     double prior0 = 1.0;
@@ -1677,6 +1684,7 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
         }
         std::stable_sort(ents.begin(), ents.end(), [](const Ent &x, const Ent &y) { return x.lgL > y.lgL; });
         eng->qslot.clear();
+        eng->qslot_lglmax = ents.empty() ? 0u : ents[0].lgL;
         for (const Ent &en : ents)
             for (uint32_t le = 0; le < (1u << en.lgL); ++le)
                 eng->qslot.push_back(make_uint2(en.q, le | (en.lgL << 8) | (en.lgG << 12)));
@@ -1695,6 +1703,9 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
     eng->var_cols.assign(p->var_cols, p->var_cols + nvar);
     eng->isvar.assign(n, 0);
     for (uint32_t b = 0; b < nvar; ++b) eng->isvar[p->var_cols[b]] = 1;
+    eng->Mv.assign((size_t)nvar * n, 0.0);  // the var columns' dispersal rows (the fused kernel's S-build)
+    for (uint32_t b = 0; b < nvar; ++b)
+        for (uint32_t k = 0; k < n; ++k) eng->Mv[(size_t)b * n + k] = p->M[(size_t)p->var_cols[b] * n + k];
     eng->Sj.assign((size_t)eng->nj * n, 0.0);
     for (uint32_t js = 0; js < eng->nj; ++js) {
         const uint32_t j = eng->cj_bits[js];
@@ -1755,10 +1766,12 @@ size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
 constexpr double kZTau = 0x1p-7;
 constexpr int kZTerms = kZTermsDev;
 
-void z_split(const mdp_engine *eng, uint32_t js, double cmax, std::vector<double> &large, double *coef)
+void z_split(const mdp_engine *eng, uint32_t js, double cmax, std::vector<double> &large, double *coef,
+             std::vector<uint32_t> *cols = nullptr)
 {
     const uint32_t n = eng->n;
     large.clear();
+    if (cols) cols->clear();
     size_t imax = 0;
     double pw[kZTerms] = {};
     for (uint32_t k = 0; k < n; ++k) {
@@ -1773,8 +1786,10 @@ void z_split(const mdp_engine *eng, uint32_t js, double cmax, std::vector<double
         }
         if (!large.empty() && sv > large[imax]) imax = large.size();
         large.push_back(sv);
+        if (cols) cols->push_back(k);
     }
     if (!large.empty()) std::swap(large[0], large[imax]);
+    if (cols && !cols->empty()) std::swap((*cols)[0], (*cols)[imax]);
     if (coef)
         for (int i = 0; i < kZTerms; ++i) coef[i] = pw[i] / (double)(i + 1);
 }
@@ -1810,6 +1825,39 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     // the fused kernel's column tables: one contiguous image it copies to LDS
     // (with zpad, all KZ zs rows, zero past kmax: the kernel reads them unmasked)
     const MdpJitPlan &pl = eng->jit_plan;
+    if (pl.sbuild) {  // S-build layout: Mv, items, CSR, series, column lists, row states
+        const size_t ct = pl.ct_max;
+        std::vector<double> img(ct, 0.0);
+        memcpy(img.data() + pl.off_mv, eng->Mv.data(), eng->Mv.size() * sizeof(double));
+        uint2 *it = (uint2 *)(img.data() + pl.off_it);
+        for (uint32_t i = 0; i < eng->nitems; ++i) {
+            const uint32_t r = eng->itemRow[i];
+            it[i] = make_uint2(eng->itemB[i] | ((r & 0xffu) << 24), eng->cj_bits[r] | ((r >> 8) << 24));
+        }
+        memcpy(img.data() + pl.off_qs, eng->qstart.data(), eng->qstart.size() * sizeof(uint32_t));
+        memcpy(img.data() + pl.off_zc, zc.data(), (size_t)nj * kZTerms * sizeof(double));
+        if (!eng->qitem.empty())
+            memcpy(img.data() + pl.off_qi, eng->qitem.data(), eng->qitem.size() * sizeof(uint32_t));
+        const bool small_n = n < 255;
+        unsigned char *zl8 = (unsigned char *)(img.data() + pl.off_zl);
+        uint16_t *zl16 = (uint16_t *)(img.data() + pl.off_zl);
+        std::vector<double> large;
+        std::vector<uint32_t> cols;
+        for (uint32_t js = 0; js < nj; ++js) {
+            z_split(eng, js, cmax, large, nullptr, &cols);
+            for (uint32_t k = 0; k < pl.kzmax; ++k) {
+                const uint32_t col = k < cols.size() ? cols[k] : (small_n ? 0xffu : 0xffffu);
+                if (small_n) zl8[(size_t)k * nj + js] = (unsigned char)col;
+                else zl16[(size_t)k * nj + js] = (uint16_t)col;
+            }
+        }
+        uint32_t *rj = (uint32_t *)(img.data() + pl.off_rj);
+        for (uint32_t js = 0; js < nj; ++js) rj[js] = eng->cj_bits[js];
+        if ((rc = dev_reserve(&d.coltab, &d.cap_coltab, ct))) return rc;
+        HIP_TRY(hipMemcpy(d.coltab, img.data(), ct * sizeof(double), hipMemcpyHostToDevice));
+        d.ct_len = (uint32_t)ct;
+        return MDP_OK;
+    }
     const size_t kimg = pl.zpad ? std::max<size_t>(kmax, std::max<uint32_t>(8u, pl.kzmax)) : kmax;
     const size_t ct = ((size_t)pl.off_zs + kimg * nj + 127) & ~(size_t)127;
     std::vector<double> img(ct, 0.0);
@@ -1845,14 +1893,21 @@ int jit_build(mdp_engine *eng, bool fused)
     const int kb_r = plan.kblock > 0 ? plan.kblock : kBlock;
     eng->jit_epl = epl_r;
     eng->jit_kblock = (uint32_t)kb_r;
-    if (fused && !eng->jit_shape_env) {  // the same e rows per block, one point per lane
-        plan.kblock = kb_r * epl_r;
-        plan.epl = 1;
+    if (fused && !eng->jit_shape_env) {
+        // the same e rows per block as the reading variant (kb_r x epl_r, the
+        // grid shape is shared), the forward at its points per lane, and
+        // twice the threads for the column-table prologue (pro 2): a
+        // forward at one point per lane was LDS-bound (each broadcast pair
+        // read feeds half the FMAs), while the prologue wants every thread
+        plan.kblock = kb_r;
+        plan.epl = epl_r;
+        plan.pro = 2;
     }
     const std::string src = mdp_jit_forward_source(plan);
     if (fused) {
         eng->jit_epl_fused = plan.epl;
         eng->jit_kblock_fused = (uint32_t)plan.kblock;
+        eng->jit_pro_fused = (uint32_t)std::max(1, plan.pro);
     }
     eng->jit_flops_pt = plan.flops_pt;
     if (const char *dump = eng->opts.get("MDP_JIT_DUMP")) {  // <path>.hip (reading) / <path>.fused.hip
@@ -1996,7 +2051,8 @@ int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 size_t fused_lds(const mdp_engine *eng, size_t ct_len)
 {
     const size_t fc = (size_t)eng->jit_plan.fused_cols;
-    return (ct_len + 2 + fc * (eng->nj + eng->nitems + 2 * eng->ldQ)) * sizeof(double);  // + staging scratch
+    const size_t sb = eng->jit_plan.sbuild ? (size_t)eng->jit_plan.kzmax * eng->nj + (size_t)eng->nj * eng->nvar + 1 : 0;
+    return (ct_len + 2 + sb + fc * (eng->nj + eng->nitems + 2 * eng->ldQ)) * sizeof(double);  // + staging scratch
 }
 
 constexpr size_t kWidePgBytes = 256ull << 20;  // wide path: item-factor chunk
@@ -2208,12 +2264,16 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     } else if (eng->jit) {
         // forward kernels with several points per lane read them from a list
         // that puts only e rows of one ratio form in a lane (spom_jit.cpp)
-        const uint32_t epl_f = eng->jit_shape_env ? (uint32_t)eng->jit_epl : 1u;  // the fused variant's (jit_build)
+        const uint32_t epl_f = (uint32_t)eng->jit_epl;  // the fused variant's (jit_build: the reading variant's)
         const uint32_t epl_max = std::max<uint32_t>((uint32_t)eng->jit_epl, epl_f);
+        d.plist_identity = true;
         if (epl_max > 1) {
             const std::vector<uint32_t> pl = point_list(e, ne, epl_max);
-            if ((rc = dev_reserve(&d.plist, &d.cap_plist, pl.size()))) return rc;
-            HIP_TRY(hipMemcpy(d.plist, pl.data(), pl.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            for (uint32_t i = 0; i < pl.size() && d.plist_identity; ++i) d.plist_identity = pl[i] == i;
+            if (!d.plist_identity) {  // an identity list is not uploaded: the kernels use the position
+                if ((rc = dev_reserve(&d.plist, &d.cap_plist, pl.size()))) return rc;
+                HIP_TRY(hipMemcpy(d.plist, pl.data(), pl.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            }
             d.nlist = (uint32_t)pl.size();
         } else {
             d.nlist = ne;
@@ -2318,13 +2378,14 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, OutStrid
         uint32_t se = os.se, sc = os.sc;
         // threads per e block: kb (x 2 with the split state-vector kernel)
         const uint32_t kb = d.fused ? eng->jit_kblock_fused : eng->jit_kblock;
+        const uint32_t pro = d.fused ? eng->jit_pro_fused : 1u;
         const uint32_t epl = d.fused ? (uint32_t)eng->jit_epl_fused : (uint32_t)eng->jit_epl;
         const uint32_t spl = eng->jit_plan.vlds && (eng->jit_plan.vsplit == 2 || eng->jit_plan.vsplit == 4)
                                  ? (uint32_t)eng->jit_plan.vsplit : 1u;
         // several points per lane: the grid's point list (set_grid_dev)
-        const uint32_t *plist = epl > 1 ? d.plist : nullptr;
+        const uint32_t *plist = epl > 1 && !d.plist_identity ? d.plist : nullptr;
         uint32_t nlist = epl > 1 ? d.nlist : d.ne;
-        if (epl > 1 && (!plist || d.nlist_epl % epl))
+        if (epl > 1 && ((!plist && !d.plist_identity) || d.nlist_epl % epl))
             return mdp_set_error(MDP_EINVAL, "no point list for %u points per lane", epl);
         void *args[] = {(void *)&Qrow, (void *)&prior0, (void *)&ev,  (void *)&ne,   (void *)&nc,
                         (void *)&out,  (void *)&se,     (void *)&one, (void *)&st,   (void *)&cv,
@@ -2350,7 +2411,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, OutStrid
             return MDP_OK;
         }
         const uint32_t dyn = d.fused ? (d.ct_len + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch
-        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kb * fc * spl), 1, 1, kb * fc * spl, 1, 1, dyn,
+        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kb * fc * spl * pro), 1, 1, kb * fc * spl * pro, 1, 1, dyn,
                                          s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));
         note_launch(eng, "mdp_fwd_jit<%s,maxA%u>", d.fused ? "fused" : "reading", eng->maxA);
@@ -2473,7 +2534,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, OutStrides os, h
     MDP_LAUNCH((k_qrows<NV, EX, CB>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, eng->nvar, eng->nj,         \
                d.zs_kmax, d.zs, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
                (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1],                 \
-               (uint32_t)(eng->qrows_xcd ? 1u : 0u), d.qslot, (uint32_t)eng->qslot.size()); } while (0)
+               (uint32_t)(eng->qrows_xcd ? 1u : 0u), d.qslot, (uint32_t)eng->qslot.size(), eng->qslot_lglmax); } while (0)
         // c values per workgroup: <= qrows_maxcb(nvar) (register budget at 1024 threads)
         if (eng->nvar == 8) {
             if (cb == 4) MDP_QROWS_CB(8, true, 4);
@@ -2808,15 +2869,31 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
             for (size_t q = 0; q + 1 < eng->qstart.size(); ++q)
                 plan.qmaxlen = std::max(plan.qmaxlen, eng->qstart[q + 1] - eng->qstart[q]);
             auto even = [](size_t v) { return (uint32_t)((v + 1) & ~(size_t)1); };
-            plan.off_it = even((size_t)eng->nj * eng->nvar);
-            plan.off_qs = even(plan.off_it + eng->nitems);
-            plan.off_qi = even(plan.off_qs + (eng->ncoef_d + 2) / 2);
-            plan.off_zc = even(plan.off_qi + (eng->qitem.size() + 1) / 2);
-            plan.off_zs = even(plan.off_zc + (size_t)eng->nj * kZTerms);
-            const size_t kmax_max = plan.kzmax;
-            plan.ct_max = (uint32_t)std::min<size_t>(((plan.off_zs + kmax_max * eng->nj) + 127) & ~(size_t)127,
-                                                     kFusedLdsMax / sizeof(double));
-            {   // zero-padded zs image when the largest one fits the fused kernel's LDS
+            plan.n = eng->n;
+            plan.var_cols = eng->var_cols;
+            if (const char *sv = eng->opts.get("MDP_FUSED_SBUILD")) plan.sbuild = atoi(sv) != 0;
+            if (plan.sbuild) {  // var-column rows, items, CSR, series, column lists, row states
+                plan.off_mv = 0;
+                plan.off_it = even((size_t)eng->nvar * eng->n);
+                plan.off_qs = even(plan.off_it + eng->nitems);
+                plan.off_qi = even(plan.off_qs + (eng->ncoef_d + 2) / 2);
+                plan.off_zc = even(plan.off_qi + (eng->qitem.size() + 1) / 2);
+                plan.off_zl = even(plan.off_zc + (size_t)eng->nj * kZTerms);
+                const size_t zlb = (size_t)plan.kzmax * eng->nj * (eng->n < 255 ? 1 : 2);
+                plan.off_rj = even(plan.off_zl + (zlb + 7) / 8);
+                plan.off_zs = even(plan.off_rj + (eng->nj + 1) / 2);  // (the end)
+                plan.ct_max = (uint32_t)((plan.off_zs + 127) & ~(size_t)127);
+                plan.zpad = true;  // the in-kernel image always holds KZ rows (zero past a row's list)
+            } else {
+                plan.off_it = even((size_t)eng->nj * eng->nvar);
+                plan.off_qs = even(plan.off_it + eng->nitems);
+                plan.off_qi = even(plan.off_qs + (eng->ncoef_d + 2) / 2);
+                plan.off_zc = even(plan.off_qi + (eng->qitem.size() + 1) / 2);
+                plan.off_zs = even(plan.off_zc + (size_t)eng->nj * kZTerms);
+                const size_t kmax_max = plan.kzmax;
+                plan.ct_max = (uint32_t)std::min<size_t>(((plan.off_zs + kmax_max * eng->nj) + 127) & ~(size_t)127,
+                                                         kFusedLdsMax / sizeof(double));
+                // zero-padded zs image when the largest one fits the fused kernel's LDS
                 const size_t kz = std::max<size_t>(8, kmax_max);
                 plan.zpad = fused_lds(eng, ((plan.off_zs + kz * eng->nj) + 127) & ~(size_t)127) <= kFusedLdsMax;
             }

@@ -232,14 +232,14 @@ std::string power_expr(const std::string &base, uint32_t E, const std::string &t
 }  // namespace
 
 // The fused kernel's Q-entry sum in the canonical order of spom_engine.hip
-// (kQGroup = 4: the items in groups of four summed left to right, the group
+// (kQGroup = 8: the items in groups of eight summed left to right, the group
 // sums as a pairwise tree padded to a power of two, i.e. a binary counter
 // folded from its lowest occupied level up), unrolled for entries of at most
 // qml items; items u < qun come from the preloaded indices qx[k][u], the
 // rest from the CSR in LDS.  Sets `a`.
 std::string qsum_code(uint32_t qml, uint32_t qun)
 {
-    const uint32_t G = 4, ngm = (qml + G - 1) / G;
+    const uint32_t G = 8, ngm = (qml + G - 1) / G;  // = kQGroup (spom_engine.hip)
     uint32_t nlev = 1;
     while ((1u << nlev) <= ngm) ++nlev;
     std::ostringstream o;
@@ -307,11 +307,14 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
           << pl.off_it << "\n#define OFF_QS " << pl.off_qs << "\n#define OFF_QI " << pl.off_qi << "\n#define OFF_ZC "
           << pl.off_zc << "\n#define OFF_ZS "
           << pl.off_zs << "\n#define KZ " << std::max<uint32_t>(8u, pl.kzmax) << "\n#define ZPAD " << (pl.zpad ? 1 : 0)
+          << "\n#define OFF_MV " << pl.off_mv << "\n#define OFF_ZL " << pl.off_zl << "\n#define OFF_RJ " << pl.off_rj
+          << "\n#define NN " << pl.n << "\n#define ZCT " << (pl.n < 255 ? "unsigned char" : "unsigned short")
+          << "\n#define ZNONE " << (pl.n < 255 ? "0xffu" : "0xffffu")
           << "\n#define QML "
           << std::max<uint32_t>(1u, pl.qmaxlen) << "\n#define QUN " << std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)
           << "\n#define NSTG "
-          << std::max<uint32_t>(1u, (pl.ct_max / 2 + (uint32_t)pl.kblock * pl.fused_cols - 1) /
-                                       ((uint32_t)pl.kblock * pl.fused_cols)) << "\n";
+          << std::max<uint32_t>(1u, (pl.ct_max / 2 + (uint32_t)(pl.kblock * pl.fused_cols * std::max(1, pl.pro)) - 1) /
+                                       ((uint32_t)(pl.kblock * pl.fused_cols * std::max(1, pl.pro)))) << "\n";
     // columns per workgroup (KBLOCK threads each; the fused variant).  Two
     // columns per reading workgroup (both Q rows staged, the pair's results
     // stored as one 16-byte store per row through LDS) was measured slower on
@@ -320,7 +323,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     // target split (vlds): SPL waves per 64 points, wave group `half`
     // accumulating the new states l with l % SPL == half
     const int SPL = pl.vlds && (pl.vsplit == 2 || pl.vsplit == 4) ? pl.vsplit : 1;
-    o << "#define FC " << FC << "\n#define SPL " << SPL << "\n#define NT (KBLOCK * FC * SPL)\n";
+    const int PRO = pl.fused && pl.pro > 1 ? pl.pro : 1;
+    o << "#define FC " << FC << "\n#define SPL " << SPL << "\n#define NTF (KBLOCK * FC * SPL)\n#define NT (NTF * "
+      << PRO << ")\n";
     {   // slot of each coefficient in the reversed copy (see the ratio forms)
         const std::vector<uint32_t> rev = reversed_index(pl.udesc, ldq_local);
         o << "__constant__ const " << (ldq_local <= 65536 ? "unsigned short" : "unsigned int") << " REVQ[" << ldq_local + 2
@@ -329,6 +334,12 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         all.push_back((uint32_t)ldq_local);
         all.push_back((uint32_t)ldq_local + 1);
         for (size_t q = 0; q < all.size(); ++q) o << (q ? (q % 32 ? "," : ",\n") : "") << all[q];
+        o << "};\n";
+    }
+    if (pl.fused && pl.sbuild) {  // the var columns (S-build)
+        o << "__constant__ const unsigned short VC[" << std::max<size_t>(1, pl.var_cols.size()) << "] = {";
+        for (size_t b = 0; b < pl.var_cols.size(); ++b) o << (b ? "," : "") << pl.var_cols[b];
+        if (pl.var_cols.empty()) o << "0";
         o << "};\n";
     }
     o << "extern \"C\" __global__ __launch_bounds__(NT) "
@@ -369,7 +380,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                      "        ie[i] = pp[i];\n"
                      "        st[i] = ie[i] < ne;\n"
                    : "        pp[i] = by * (KBLOCK * EPL) + tid * EPL + i;\n"
-                     "        const u32 q_ = pp[i] < nlist ? plist[pp[i]] : 0x80000000u;\n"
+                     // (no list: the identity, which a sorted grid with an even
+                     // number of s-form rows is -- no dependent load then)
+                     "        const u32 q_ = pp[i] < nlist ? (plist ? plist[pp[i]] : pp[i]) : 0x80000000u;\n"
                      "        ie[i] = q_ & 0x7fffffffu;\n"
                      "        st[i] = !(q_ >> 31) && ie[i] < ne;\n")
       << "        ev[i] = ie[i] < ne ? evals[ie[i]] : 0.0;\n"
@@ -477,12 +490,22 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         o << "    extern __shared__ __attribute__((aligned(16))) double ct[];\n"
              "    __shared__ double Zl[FC * NJ];\n"
              "    __shared__ double Pl[FC * NITEMS];\n"
-             "    const double *Svl = ct;\n"
              "    const uint2 *Itl = (const uint2 *)(ct + OFF_IT);\n"
              "    const u32 *Qsl = (const u32 *)(ct + OFF_QS);\n"
              "    const u32 *Qil = (const u32 *)(ct + OFF_QI);\n"
-             "    const double *zl = ct + OFF_ZS;\n"
              "    const double *zcl = ct + OFF_ZC;\n"
+          << (pl.sbuild
+                  // the colonisation sums are built here (S-build, below) from the
+                  // var columns' dispersal rows: half the bytes to stage
+                  ? "    __shared__ __attribute__((aligned(16))) double Zsb[KZ * NJ];\n"
+                    "    __shared__ double Svb[NJ * NVAR + 1];\n"
+                    "    const double *Svl = Svb;\n"
+                    "    const double *zl = Zsb;\n"
+                    "    const double *Mvl = ct + OFF_MV;\n"
+                    "    const ZCT *Zcl = (const ZCT *)(ct + OFF_ZL);\n"
+                    "    const u32 *Rjl = (const u32 *)(ct + OFF_RJ);\n"
+                  : "    const double *Svl = ct;\n"
+                    "    const double *zl = ct + OFF_ZS;\n") <<
              "    double cc[FC];\n"
              "#pragma unroll\n"
              "    for (int f = 0; f < FC; ++f) cc[f] = ic0 + f < nc ? cvals[ic0 + f] : 0.0;\n"
@@ -506,6 +529,33 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        }\n"
              "    }\n"
              "    __syncthreads();\n"
+          << (pl.sbuild
+                  // S-build: per row r (hidden state j) its explicit columns'
+                  // S[j][k] into the zs image (row pairs [k/2][r][k%2]) and its
+                  // var columns' into Svb, each the host's sum (spom_engine.hip
+                  // build_direct_plan): M[V_b][k] over the var columns b of j,
+                  // V_b != k, ascending b -- the same bits as the staged tables
+                  ? "    {\n"
+                    "        constexpr u32 NSB = NJ * (KZ + NVAR), KSB = (NSB + NT - 1) / NT;\n"
+                    "#pragma unroll\n"
+                    "        for (u32 k = 0; k < KSB; ++k) {\n"
+                    "            const u32 w = threadIdx.x + k * NT;\n"
+                    "            if (w < NSB) {\n"
+                    "                const u32 r = w % NJ, sl = w / NJ, j = Rjl[r];\n"
+                    "                const u32 col = sl < KZ ? (u32)Zcl[sl * NJ + r] : (u32)VC[sl - KZ];\n"
+                    "                double S = 0.0;\n"
+                    "                if (col != ZNONE) {\n"
+                    "#pragma unroll\n"
+                    "                    for (int b = 0; b < NVAR; ++b)\n"
+                    "                        if (((j >> (NVAR - 1 - b)) & 1u) && (u32)VC[b] != col) S += Mvl[b * NN + col];\n"
+                    "                }\n"
+                    "                if (sl < KZ) Zsb[((sl / 2) * NJ + r) * 2 + (sl & 1)] = S;\n"
+                    "                else Svb[r * NVAR + (sl - KZ)] = S;\n"
+                    "            }\n"
+                    "        }\n"
+                    "    }\n"
+                    "    __syncthreads();\n"
+                  : "")
           << stamp(4) <<
              // operands of the Pc and Q phases that do not depend on Z, read
              // and combined before the Z phase: per item its Z slot and the
@@ -633,7 +683,9 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     }
     o << wblock;
     o << "    __syncthreads();\n"
-      << stamp(2);
+      << stamp(2)
+      // the prologue's extra threads (PRO > 1) are done: the forward runs on NTF
+      << (PRO > 1 ? "    if (threadIdx.x >= NTF) return;\n" : "");
     // H for point i: the Horner chain of a Q group (offset, nX) over the
     // lane's copy of the coefficients (stored order for s-form lanes,
     // reversed for t-form ones).  Transitions of one group (same A & B and B)

@@ -14,6 +14,11 @@ struct MdpJitPlan {
     // three phases for one c value) instead of reading Q rows
     bool fused = false;
     int fused_cols = 2;  // c columns per fused workgroup (KBLOCK threads each)
+    // fused variant: the workgroup has PRO times the forward's threads; the
+    // extra ones share the column-table prologue and leave before the
+    // forward recursion (more threads for the latency-bound prologue, fewer
+    // LDS reads per FMA in the forward: its waves take EPL points a lane)
+    int pro = 1;
     bool fast_log = true;  // mdp_log (prelude) instead of the library log for log L
     int hack = 0;  // diag build only (MDP_JIT_HACK; results wrong): 1 = no log, no stores; 2 = no stores
     uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
@@ -21,6 +26,13 @@ struct MdpJitPlan {
     // items, qstart, qitem, the Z-row series coefficients [nj][8], then
     // zs[kmax][nj] (the explicit "large" columns)
     uint32_t off_it = 0, off_qs = 0, off_qi = 0, off_zc = 0, off_zs = 0;
+    // S-build layout (sbuild): instead of the var-column S and the zs image,
+    // the var columns' dispersal rows Mv[nvar][n] (off_mv), each row's
+    // explicit column list [kzmax][nj] (u8 for n < 255, else u16; off_zl)
+    // and each row's hidden state j (off_rj); the kernel builds S itself
+    bool sbuild = true;
+    uint32_t off_mv = 0, off_zl = 0, off_rj = 0, n = 0;
+    std::vector<uint32_t> var_cols;
     uint32_t kzmax = 0;    // zs rows compiled in (grids with |c| <= 1; larger ones use k_qrows)
     bool zpad = false;     // the fused image always holds kzmax zs rows (zero past kmax)
     uint32_t qmaxlen = 0;  // most items of one Q entry

@@ -17,4 +17,8 @@ done
 timeout -k 10 300 python scripts/sweep_forward.py --configs 2,3 --steps 50 --variants "${VARIANTS:-MDP_JIT=1;MDP_EPL=2;MDP_FUSED=0}" > $O/sweep.jsonl 2> $O/sweep.err || { echo "sweep failed"; tail $O/sweep.err; exit 1; }
 cut -c1-300 $O/sweep.jsonl
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 --config 3 --backend gloo > $O/bench_gloo2_cfg3.json 2> $O/bench_gloo2.err || { echo "gloo rehearsal failed"; tail $O/bench_gloo2.err; exit 1; }
-python -c "import json; d=json.load(open('$O/bench_gloo2_cfg3.json')); print('gloo2', d['value'], d['job'], d['strong'])"
+python -c "import json; d=json.loads([l for l in open('$O/bench_gloo2_cfg3.json') if l.startswith('{')][-1]); print('gloo2', d['value'], d['job'], d['strong'])"
+if [ -n "$DIAG" ]; then
+  timeout -k 10 300 python scripts/sweep_forward.py --configs 2,3 --steps 30 --variants "MDP_JIT=1" --diag > $O/diag.txt 2>&1 || { echo "diag failed"; tail $O/diag.txt; exit 1; }
+  grep -v amdgpu.ids $O/diag.txt | cut -c1-1500
+fi
