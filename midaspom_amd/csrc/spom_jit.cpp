@@ -690,15 +690,25 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     // lane's copy of the coefficients (stored order for s-form lanes,
     // reversed for t-form ones).  Transitions of one group (same A & B and B)
     // from sources of different |A| share H and differ only in g^d.
+    // Register kernels emit the forward twice (split_forms), once per ratio
+    // form behind a lane-uniform branch on tf: the t-form copy reads the
+    // reversed coefficients at a fixed base and drops every g^d factor (g = 1
+    // there, so the products it leaves out are exact: the same bits), 55 % of
+    // config 2's uses; waves of one form run only their copy.  The LDS-state
+    // kernels keep one copy (their wave groups already branch per year).
+    const bool split_forms = !pl.vlds;
+    const char *qbase = "Qp";  // the copy being emitted: "Qp", "Qs_" or "Qt_"
+    bool gmul = true;          // the copy being emitted multiplies by g^d
     auto hexpr = [&](uint32_t d) {
         const uint32_t off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u;
-        std::string e = "Qp[" + std::to_string(off) + "]";
-        for (uint32_t m = 1; m <= nX; ++m) e = "fma(" + e + ", zz[i], Qp[" + std::to_string(off + m) + "])";
+        std::string e = std::string(qbase) + "[" + std::to_string(off) + "]";
+        for (uint32_t m = 1; m <= nX; ++m)
+            e = "fma(" + e + ", zz[i], " + qbase + "[" + std::to_string(off + m) + "])";
         return e;
     };
     auto gfac = [&](uint32_t d) {
         const uint32_t nX = (d >> 22) & 31u, nA = d >> 27;
-        return nA > nX ? " * gp[i][" + std::to_string(nA - nX) + "]" : std::string();
+        return gmul && nA > nX ? " * gp[i][" + std::to_string(nA - nX) + "]" : std::string();
     };
     // Regions are separate basic blocks: each guard value passes through an
     // opaque scalar move, so instruction selection can neither merge regions
@@ -712,7 +722,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         : "    { u32 g_; asm volatile(\"s_mov_b32 %0, %1\" : \"=s\"(g_) : \"s\"(one)); if (g_) {\n";
     const int nslot = pl.slots > 0 ? pl.slots : 0;
     if (nslot > 0) o << "    double pc[EPL][" << nslot << "];\n";
-    o << guard;
     int since = 0;
     auto fence = [&]() {
         if (++since >= window) {
@@ -764,6 +773,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     // flops per point: the ratio and its power tables, transitions and
     // scalings (below), the prior sum
     double flops = 2.0 + (double)sch.dp + (double)sch.dg + (pl.last ? 2.0 * npmax : 0.0);
+    double fcount = 0.0;  // the copy's flops (the first copy's are kept: the s-form, an upper bound)
     std::vector<std::vector<uint32_t>> slot_key(SPL, std::vector<uint32_t>(nslot, 0));
     std::vector<std::vector<size_t>> slot_next(SPL, std::vector<size_t>(nslot, SIZE_MAX));  // SIZE_MAX: free / dead
     // returns the expression for use u (H times its g^d), emitting
@@ -775,13 +785,13 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         std::vector<uint32_t> &skey = slot_key[grp[u]];
         std::vector<size_t> &snext = slot_next[grp[u]];
         const std::string g = gfac(d);
-        if (!g.empty()) flops += 1.0;
+        if (!g.empty()) fcount += 1.0;
         for (int sl = 0; sl < nslot; ++sl)
             if (snext[sl] == p && skey[sl] == key) {
                 snext[sl] = np_;
                 return "(pc[i][" + std::to_string(sl) + "]" + g + ")";
             }
-        flops += 2.0 * ((d >> 22) & 31u);  // nX FMAs
+        fcount += 2.0 * ((d >> 22) & 31u);  // nX FMAs
         const std::string e = hexpr(d);
         if (nslot == 0 || np_ == SIZE_MAX || np_ - p > kHorizon) return "((" + e + ")" + g + ")";
         int best = 0;
@@ -802,6 +812,15 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         const uint32_t df = sch.diff[t][k];
         return pl.vlds && df ? "(" + vref(k) + " * bp[i][" + std::to_string(df) + "])" : vref(k);
     };
+    // one copy of the forward recursion (its own transition-cache state)
+    auto emit_body = [&]() {
+    for (int h = 0; h < SPL; ++h) {
+        std::fill(slot_key[h].begin(), slot_key[h].end(), 0u);
+        std::fill(slot_next[h].begin(), slot_next[h].end(), SIZE_MAX);
+    }
+    fcount = 0.0;
+    since = 0;
+    o << guard;
     size_t u = 0;
     for (size_t t = 1; t < pl.np.size(); ++t) {
         const uint32_t npp = pl.np[t - 1], npc = pl.np[t];
@@ -809,10 +828,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             std::string pre;
             const std::string e = use_expr(u++, pre);
             o << "    for (int i = 0; i < EPL; ++i) { " << pre << "v[i][0] = v[i][0] * " << e << "; }\n";
-            flops += 1.0;
+            fcount += 1.0;
             if (sch.flush[t]) {
                 o << "    for (int i = 0; i < EPL; ++i) v[i][0] *= " << flush_factor(t) << ";\n";
-                flops += 1.0;
+                fcount += 1.0;
             }
             fence();
             continue;
@@ -821,7 +840,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             for (uint32_t k = 0; k < npp; ++k)
                 if (sch.diff[t][k]) {
                     o << "    for (int i = 0; i < EPL; ++i) v[i][" << k << "] *= bp[i][" << sch.diff[t][k] << "];\n";
-                    flops += 1.0;
+                    fcount += 1.0;
                 }
         if (pl.vlds) {
             // states in LDS: wave group h accumulates the new states l = h,
@@ -846,8 +865,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                         const std::string acc = "n[i][" + std::to_string(l / SPL) + "]";
                         o << "    for (int i = 0; i < EPL; ++i) { " << pre << acc << " = fma(" << src(t, k) << ", " << e
                           << ", " << (k ? acc : std::string("0.0")) << "); }\n";
-                        flops += sch.diff[t][k] ? 1.0 : 0.0;
-                        flops += k ? 2.0 : 1.0;
+                        fcount += sch.diff[t][k] ? 1.0 : 0.0;
+                        fcount += k ? 2.0 : 1.0;
                         fence();
                     }
                 if (split) o << "    }}\n";
@@ -856,7 +875,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
             o << "    for (int i = 0; i < EPL; ++i) {\n";
             if (sch.flush[t]) {
                 o << "        const double fl_ = " << flush_factor(t) << ";\n";
-                flops += 1.0 + npc;
+                fcount += 1.0 + npc;
             }
             for (int h = 0; h < SPL; ++h) {
                 if (split)
@@ -881,7 +900,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                 const std::string e = use_expr(u++, pre);
                 o << "    for (int i = 0; i < EPL; ++i) { " << pre << "n[i][" << l << "] = fma(" << vref(k) << ", "
                   << e << ", " << (k ? "n[i][" + std::to_string(l) + "]" : std::string("0.0")) << "); }\n";
-                flops += k ? 2.0 : 1.0;
+                fcount += k ? 2.0 : 1.0;
                 fence();
             }
         // states past npc are never read again (a year reads k < npp, and
@@ -890,18 +909,36 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         o << "    for (int i = 0; i < EPL; ++i) {\n";
         if (sch.flush[t]) {
             o << "        const double fl_ = " << flush_factor(t) << ";\n";
-            flops += 1.0 + npc;
+            fcount += 1.0 + npc;
         }
         for (uint32_t l = 0; l < npc; ++l)
             o << "        " << vref(l) << " = n[i][" << l << "]" << (sch.flush[t] ? " * fl_" : "") << ";\n";
         o << "    }\n";
+    }
+    o << "    }}\n";
+    };
+    if (split_forms) {
+        // (s-form lanes: the stored coefficients; t-form: the reversed copy)
+        o << "    if (!tf) {\n    const double *Qs_ = Qh;\n";
+        qbase = "Qs_";
+        gmul = true;
+        emit_body();
+        flops += fcount;
+        o << "    } else {\n    const double *Qt_ = Qh + FC * LDQ;\n";
+        qbase = "Qt_";
+        gmul = false;
+        emit_body();
+        o << "    }\n";
+    } else {
+        emit_body();
+        flops += fcount;
     }
     // the pending exponent at the end: applied to L (last chunk); a chunk
     // that is not the last hands its states over unscaled (the next one
     // starts from this exponent, plan.e0)
     const std::string fin = power_expr("bb[i]", sch.final_exp, "fe");
     if (sch.final_exp && pl.last) flops += 1.0;
-    o << "    }}\n" << stamp(3) << "#define NPLAST " << pl.np.back() << "\n"
+    o << stamp(3) << "#define NPLAST " << pl.np.back() << "\n"
       << (pl.vlds ? "#define VREF(l) Vl[((l) * EPL + i) * KBLOCK + tid]\n" : "#define VREF(l) v[i][l]\n");
     if (pl.last && (pl.hack == 1 || pl.hack == 2))  // measurement only: the result is never stored
         o << "#pragma unroll\n"

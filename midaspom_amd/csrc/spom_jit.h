@@ -30,7 +30,7 @@ struct MdpJitPlan {
     // the var columns' dispersal rows Mv[nvar][n] (off_mv), each row's
     // explicit column list [kzmax][nj] (u8 for n < 255, else u16; off_zl)
     // and each row's hidden state j (off_rj); the kernel builds S itself
-    bool sbuild = true;
+    bool sbuild = false;  // measured slower on config 2 (10.4 vs 9.2-9.4 us): off by default
     uint32_t off_mv = 0, off_zl = 0, off_rj = 0, n = 0;
     std::vector<uint32_t> var_cols;
     uint32_t kzmax = 0;    // zs rows compiled in (grids with |c| <= 1; larger ones use k_qrows)
