@@ -273,6 +273,45 @@ std::string qsum_code(uint32_t qml, uint32_t qun)
     return o.str();
 }
 
+// The same sum with every gather unconditional (qflat): slots past the
+// entry's count read the zero slot pl[NITEMS] (set in the Pc phase), so all
+// loads are in flight at once instead of one branch and wait per item.  The
+// groups and the tree then run over the compile-time bound (groups of zeros
+// past the entry); every padded addition is x + (+0.0) = x for the
+// non-negative (or NaN / inf) sums here, so the bits are those of
+// qsum_code's canonical order.  Sets `a`.
+std::string qsum_flat_code(uint32_t qml, uint32_t qun)
+{
+    const uint32_t G = 8, ngm = (qml + G - 1) / G;  // = kQGroup (spom_engine.hip)
+    uint32_t ngp = 1;
+    while (ngp < ngm) ngp *= 2;
+    std::ostringstream o;
+    o << "            const u32 cnt_ = qn[k];\n"
+         "            double p_[" << qml << "];\n";
+    for (uint32_t u = 0; u < qml; ++u) {
+        if (u < qun)
+            o << "            p_[" << u << "] = pl[qx[k][" << u << "]];\n";
+        else
+            o << "            { const u32 t_ = Qil[qb[k] + " << u << "u]; p_[" << u << "] = pl[" << u
+              << "u < cnt_ ? t_ : (u32)NITEMS]; }\n";
+    }
+    o << "            (void)cnt_;\n            double g_[" << ngp << "];\n";
+    for (uint32_t g = 0; g < ngp; ++g) {
+        if (g >= ngm) {
+            o << "            g_[" << g << "] = 0.0;\n";
+            continue;
+        }
+        o << "            g_[" << g << "] = p_[" << G * g << "]";
+        for (uint32_t u = 1; u < G && G * g + u < qml; ++u) o << " + p_[" << G * g + u << "]";
+        o << ";\n";
+    }
+    for (uint32_t w = ngp; w > 1; w /= 2)
+        for (uint32_t i = 0; i < w / 2; ++i)
+            o << "            g_[" << i << "] = g_[" << 2 * i << "] + g_[" << 2 * i + 1 << "];\n";
+    o << "            const double a = g_[0];\n";
+    return o.str();
+}
+
 int mdp_jit_default_epl(const std::vector<uint32_t> &) { return 2; }
 
 uint32_t mdp_jit_end_exp(const MdpJitPlan &plan) { return schedule(plan).final_exp; }
@@ -362,6 +401,12 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                  : "    const u32 lb = blockIdx.x + 0 * full;\n") <<
          // FC columns per workgroup (fused variant): KBLOCK threads each
          "    const u32 half = threadIdx.x / KBLOCK, tid = threadIdx.x % KBLOCK;\n"
+         // the lane's place in its column's e block: with several columns per
+         // workgroup each column's lanes are rotated by half a block, so the
+         // waves a SIMD holds (wave w on SIMD w mod 4) take e rows from both
+         // halves -- on a grid with ratio forms split at the block's middle
+         // every SIMD then runs one s-form and one t-form wave, not two of one
+      << (FC > 1 && SPL == 1 && pl.rot ? "    const u32 tip = (tid + half * (KBLOCK / 2)) % KBLOCK;\n" : "    const u32 tip = tid;\n")
          // (column group, e block): FC columns x KBLOCK*EPL e values per workgroup
       << (pl.efast ? "    const u32 gy = (nlist + KBLOCK * EPL - 1) / (KBLOCK * EPL), ic0 = lb / gy * FC, by = lb % gy;\n"
                    : "    const u32 ncb = (nc + FC - 1) / FC, ic0 = lb % ncb * FC, by = lb / ncb;\n")
@@ -376,10 +421,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    u32 ie[EPL], pp[EPL];\n    bool st[EPL];\n    double ev[EPL];\n"
          "#pragma unroll\n"
          "    for (int i = 0; i < EPL; ++i) {\n"
-      << (EPL == 1 ? "        pp[i] = by * KBLOCK + tid;\n"
+      << (EPL == 1 ? "        pp[i] = by * KBLOCK + tip;\n"
                      "        ie[i] = pp[i];\n"
                      "        st[i] = ie[i] < ne;\n"
-                   : "        pp[i] = by * (KBLOCK * EPL) + tid * EPL + i;\n"
+                   : "        pp[i] = by * (KBLOCK * EPL) + tip * EPL + i;\n"
                      // (no list: the identity, which a sorted grid with an even
                      // number of s-form rows is -- no dependent load then)
                      "        const u32 q_ = pp[i] < nlist ? (plist ? plist[pp[i]] : pp[i]) : 0x80000000u;\n"
@@ -428,6 +473,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    double v[EPL][NPMAX];\n    double n[EPL][(NPMAX + SPL - 1) / SPL];\n";
     if (pl.vlds)  // wide years: state k of point i of lane tid at Vl[k][i][tid]
         o << "    __shared__ double Vl[NPMAX * EPL * KBLOCK];\n";
+    // the per-point set-up (ratio, its division, the power tables, the start
+    // vector) depends on the lane's e value alone: emitted first, its
+    // latency hides under the prologue's loads (early_w), or after it
+    if (pl.early_w) o << wblock;
     // the state k of point i, as an expression
     auto vref = [&](uint32_t k) {
         return pl.vlds ? "Vl[(" + std::to_string(k) + " * EPL + i) * KBLOCK + tid]" : "v[i][" + std::to_string(k) + "]";
@@ -489,7 +538,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         // all in flight, one barrier.
         o << "    extern __shared__ __attribute__((aligned(16))) double ct[];\n"
              "    __shared__ double Zl[FC * NJ];\n"
-             "    __shared__ double Pl[FC * NITEMS];\n"
+             "#define PLS (NITEMS + 1)\n"  // a column's items, then its zero slot (the flat Q sums' padding)
+             "    __shared__ double Pl[FC * PLS];\n"
              "    const uint2 *Itl = (const uint2 *)(ct + OFF_IT);\n"
              "    const u32 *Qsl = (const u32 *)(ct + OFF_QS);\n"
              "    const u32 *Qil = (const u32 *)(ct + OFF_QI);\n"
@@ -569,6 +619,122 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    double Fp[KPC];\n"
              "    u32 zi[KPC];\n"
              "#define ITEM_W(k) ((k) * NT + (((k) & 1) ? NT - 1 - threadIdx.x : threadIdx.x))\n"
+             // balanced prologue (pl.bal): the Z rows on the last threads, the Q
+             // entries just below them, the items from thread 0 -- so no wave
+             // carries an item, a Q entry's descriptors and a Z row at once
+             // (the Q descriptors stay with the thread that sums the entry)
+          << (pl.bal ? "#define ZW(k) ((k) * NT + NT - 1 - threadIdx.x)\n"
+                       "#define QROT (FC * NJ + FC * LDQ <= NT ? NT - FC * NJ - FC * LDQ : 0)\n"
+                       "#define QW(k) ((k) * NT + (threadIdx.x + NT - QROT) % NT)\n"
+                     : "#define ZW(k) ((k) * NT + threadIdx.x)\n#define QW(k) ((k) * NT + threadIdx.x)\n")
+          << (pl.ph2flat ? std::string(
+             // issue-first form (ph2flat): every first-level LDS load of the
+             // three roles (item descriptors, Q-entry bounds, Z rows and their
+             // series coefficients) unconditional and in flight together, then
+             // the second level (each item's row pressures S, each entry's item
+             // indices), then the arithmetic -- two LDS round trips on the
+             // critical path instead of one or two per role in sequence
+             "    constexpr int KZR = (FC * NJ + NT - 1) / NT;\n"
+             "    uint2 it_[KPC];\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < KPC; ++k) {\n"
+             "        const u32 w = ITEM_W(k);\n"
+             "        it_[k] = Itl[(w < FC * NITEMS ? w : FC * NITEMS - 1) / FC];\n"
+             "    }\n"
+             "    u32 qb[KQ], qn[KQ], qx[KQ][QUN];\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < KQ; ++k) {\n"
+             "        const u32 w = QW(k), q = w % LDQ;\n"
+             "        const bool live = w < FC * LDQ && q < NCOEF;\n"
+             "        const u32 qc = live ? q : 0u, q0 = Qsl[qc], q1 = Qsl[qc + 1];\n"
+             "        qb[k] = live ? q0 : 0u;\n"
+             "        qn[k] = live ? q1 - q0 : 0u;\n"
+             "    }\n"
+             "    double2 zr_[KZR][KZ / 2], zq_[KZR][4];\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < KZR; ++k) {\n"
+             "        const u32 w = ZW(k), r = (w < FC * NJ ? w : FC * NJ - 1) / FC;\n"
+             "#pragma unroll\n"
+             "        for (u32 kk = 0; kk < KZ; kk += 2) zr_[k][kk / 2] = ((const double2 *)zl)[(ZPAD || kk < kmax ? kk : kk % 8u) / 2 * NJ + r];\n"
+             "#pragma unroll\n"
+             "        for (int u = 0; u < 4; ++u) zq_[k][u] = ((const double2 *)(zcl + r * 8))[u];\n"
+             "    }\n"
+             "    double sv_[KPC][NVAR];\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < KPC; ++k) {\n"
+             "        const u32 r = (it_[k].x >> 24) | ((it_[k].y >> 24) << 8);\n"
+             "#pragma unroll\n"
+             "        for (int b = 0; b < NVAR; ++b) sv_[k][b] = Svl[r * NVAR + b];\n"
+             "    }\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < KQ; ++k)\n"
+             "#pragma unroll\n"
+             "        for (int u = 0; u < QUN; ++u) { const u32 t_ = Qil[qb[k] + u]; qx[k][u] = (u32)u < qn[k] ? t_ : (u32)NITEMS; }\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < KPC; ++k) {\n"
+             "        const u32 w = ITEM_W(k);\n"
+             "        const u32 col = w % FC;\n"
+             "        const double c = cc[col];\n"
+             "        const uint2 t = it_[k];\n"
+             "        const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
+             "        double f[NVAR];\n"
+             "        const u32 nB = ~B;\n"
+             "#pragma unroll\n"
+             "        for (int b = 0; b < NVAR; ++b) {\n"
+             "            const u32 bit = NVAR - 1 - b;\n"
+             "            const double pcv = c * sv_[k][b];\n"
+             "            const double p = (pcv > 1.0) | ((j >> bit) & 1u) ? 1.0 : pcv;\n"
+             "            const double sg = __hiloint2double((int)(0x3ff00000u | ((nB << (31 - bit)) & 0x80000000u)), 0);\n"
+             "            f[b] = fma(sg, p, fma(-0.5, sg, 0.5));\n"
+             "        }\n"
+             "#pragma unroll\n"
+             "        for (int s = 1; s < NVAR; s *= 2)\n"
+             "#pragma unroll\n"
+             "            for (int b = 0; b + s < NVAR; b += 2 * s) f[b] *= f[b + s];\n"
+             "        Fp[k] = w < FC * NITEMS ? f[0] : 0.0;\n"
+             "        zi[k] = w < FC * NITEMS ? col * NJ + r : 0u;\n"
+             // (kept before the Z phase's barrier: otherwise the compiler sinks
+             // this arithmetic past it, where every wave waits on it)
+             "        asm volatile(\"\" : \"+v\"(Fp[k]));\n"
+             "    }\n"
+             "#pragma unroll\n"
+             "    for (int k = 0; k < KZR; ++k) {\n"
+             "        const u32 w = ZW(k);\n"
+             "        if (w < FC * NJ) {\n"
+             "            const u32 col = w % FC, r = w / FC;\n"
+             "            const double c = cc[col];\n"
+             "            double sk[KZ];\n"
+             "#pragma unroll\n"
+             "            for (u32 kk = 0; kk < KZ; kk += 2) {\n"
+             "                const bool in = ZPAD || kk < kmax;\n"
+             "                sk[kk] = in ? zr_[k][kk / 2].x : 0.0;\n"
+             "                sk[kk + 1] = in ? zr_[k][kk / 2].y : 0.0;\n"
+             "            }\n"
+             "            double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
+             "#pragma unroll\n"
+             "            for (u32 kk = 0; kk < KZ; kk += 8) {\n"
+             "                za *= fma(-c, sk[kk + 0], 1.0) * fma(-c, sk[kk + 4], 1.0);\n"
+             "                zb *= fma(-c, sk[kk + 1], 1.0) * fma(-c, sk[kk + 5], 1.0);\n"
+             "                zc *= fma(-c, sk[kk + 2], 1.0) * fma(-c, sk[kk + 6], 1.0);\n"
+             "                zd *= fma(-c, sk[kk + 3], 1.0) * fma(-c, sk[kk + 7], 1.0);\n"
+             "            }\n"
+             "            double z = (za * zb) * (zc * zd);\n"
+             "            if (kmax && !(fma(-c, sk[0], 1.0) > 0.0)) z = 0.0;\n"
+             "            {\n"
+             "                const double2 p01 = zq_[k][0], p23 = zq_[k][1], p45 = zq_[k][2], p67 = zq_[k][3];\n"
+             "                double q = p67.y;\n"
+             "                q = fma(q, c, p67.x);\n"
+             "                q = fma(q, c, p45.y);\n"
+             "                q = fma(q, c, p45.x);\n"
+             "                q = fma(q, c, p23.y);\n"
+             "                q = fma(q, c, p23.x);\n"
+             "                q = fma(q, c, p01.y);\n"
+             "                q = fma(q, c, p01.x);\n"
+             "                z *= exp(-(q * c));\n"
+             "            }\n"
+             "            Zl[col * NJ + r] = z;\n"
+             "        }\n"
+             "    }\n") : std::string(
              "#pragma unroll\n"
              "    for (int k = 0; k < KPC; ++k) {\n"
              "        const u32 w = ITEM_W(k);\n"
@@ -603,22 +769,26 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    u32 qb[KQ], qn[KQ], qx[KQ][QUN];\n"
              "#pragma unroll\n"
              "    for (int k = 0; k < KQ; ++k) {\n"
-             "        const u32 w = threadIdx.x + k * NT, q = w % LDQ;\n"
+             "        const u32 w = QW(k), q = w % LDQ;\n"
              "        const bool live = w < FC * LDQ && q < NCOEF;\n"
              "        const u32 q0 = live ? Qsl[q] : 0u, q1 = live ? Qsl[q + 1] : 0u;\n"
              "        qb[k] = q0;\n"
              "        qn[k] = q1 - q0;\n"
-             "#pragma unroll\n"
+             "#pragma unroll\n") +
              // only the entry's own items: lanes past their count stay masked
-             // off, so the gathers below touch no other entry's banks
-             "        for (int u = 0; u < QUN; ++u) qx[k][u] = (u32)u < qn[k] ? Qil[q0 + u] : 0u;\n"
+             // off, so the gathers below touch no other entry's banks (qflat:
+             // every index load in flight, reading past the entry within the
+             // image; slots past the count name the zero slot)
+             (pl.qflat
+                  ? "        for (int u = 0; u < QUN; ++u) { const u32 t_ = Qil[q0 + u]; qx[k][u] = (u32)u < qn[k] ? t_ : (u32)NITEMS; }\n"
+                  : "        for (int u = 0; u < QUN; ++u) qx[k][u] = (u32)u < qn[k] ? Qil[q0 + u] : 0u;\n") + std::string(
              "    }\n"
              // Z per (column, row): the row's KZ (compile-time bound) values
              // all in flight; rows past kmax contribute fma(-c, 0, 1) = 1 (with
              // ZPAD the image holds those zero rows, so no per-value select)
              "#pragma unroll\n"
              "    for (int k = 0; k < (FC * NJ + NT - 1) / NT; ++k) {\n"
-             "        const u32 w = threadIdx.x + k * NT;\n"
+             "        const u32 w = ZW(k);\n"
              "        if (w < FC * NJ) {\n"
              "            const u32 col = w % FC, r = w / FC;\n"
              "            const double c = cc[col];\n"
@@ -659,29 +829,31 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "            }\n"
              "            Zl[col * NJ + r] = z;\n"
              "        }\n"
-             "    }\n"
+             "    }\n")) <<
              "    __syncthreads();\n"
           << stamp(5) <<
              "#pragma unroll\n"
              "    for (int k = 0; k < KPC; ++k) {\n"
              "        const u32 w = ITEM_W(k);\n"
-             "        if (w < FC * NITEMS) Pl[(w % FC) * NITEMS + w / FC] = Zl[zi[k]] * Fp[k];\n"
+             "        if (w < FC * NITEMS) Pl[(w % FC) * PLS + w / FC] = Zl[zi[k]] * Fp[k];\n"
              "    }\n"
+             "    if (threadIdx.x < FC) Pl[threadIdx.x * PLS + NITEMS] = 0.0;\n"
              "    __syncthreads();\n"
           << stamp(1) <<
              // Q entries: the items in CSR (ascending j) order
              "#pragma unroll\n"
              "    for (int k = 0; k < KQ; ++k) {\n"
-             "        const u32 w = threadIdx.x + k * NT;\n"
+             "        const u32 w = QW(k);\n"
              "        if (w < FC * LDQ) {\n"
-             "            const double *pl = Pl + (w / LDQ) * NITEMS;\n"
-          << qsum_code(std::max<uint32_t>(1u, pl.qmaxlen), std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)) <<
+             "            const double *pl = Pl + (w / LDQ) * PLS;\n"
+          << (pl.qflat ? qsum_flat_code(std::max<uint32_t>(1u, pl.qmaxlen), std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u))
+                       : qsum_code(std::max<uint32_t>(1u, pl.qmaxlen), std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u))) <<
              "            Ql[w] = a;\n"
              "            Ql[FC * LDQ + (w / LDQ) * LDQ + REVQ[w % LDQ]] = a;\n"
              "        }\n"
              "    }\n";
     }
-    o << wblock;
+    if (!pl.early_w) o << wblock;
     o << "    __syncthreads();\n"
       << stamp(2)
       // the prologue's extra threads (PRO > 1) are done: the forward runs on NTF
@@ -696,7 +868,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     // there, so the products it leaves out are exact: the same bits), 55 % of
     // config 2's uses; waves of one form run only their copy.  The LDS-state
     // kernels keep one copy (their wave groups already branch per year).
-    const bool split_forms = !pl.vlds;
+    const bool split_forms = !pl.vlds && pl.split_forms;
     const char *qbase = "Qp";  // the copy being emitted: "Qp", "Qs_" or "Qt_"
     bool gmul = true;          // the copy being emitted multiplies by g^d
     auto hexpr = [&](uint32_t d) {

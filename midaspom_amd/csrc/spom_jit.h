@@ -20,6 +20,22 @@ struct MdpJitPlan {
     // LDS reads per FMA in the forward: its waves take EPL points a lane)
     int pro = 1;
     bool fast_log = true;  // mdp_log (prelude) instead of the library log for log L
+    // register kernels: one copy of the forward per ratio form (the t-form
+    // copy without g^d factors); false: one copy for both
+    bool split_forms = true;
+    // the per-point set-up (ratio, power tables, start vector) before the
+    // prologue rather than after it
+    bool early_w = false;  // neutral on config 2, config 3 forward 43.1-43.7 vs 44.3-44.5 us with it
+    // fused prologue: Z rows, Q entries and items on disjoint threads
+    bool bal = false;  // measured slower (ph2 2.4 k -> 2.7 k cycles)
+    // fused Q sums and their index loads unconditional (zero slot padding)
+    bool qflat = true;
+    // fused prologue's Z-independent phase in issue-first form (all
+    // first-level LDS loads of items, Q entries and Z rows in flight together)
+    bool ph2flat = false;  // measured slower (ph2 + ph3 3.5 k vs 2.8 k cycles)
+    // several columns per workgroup: each column's lanes rotated by half a
+    // block (SIMD balance of the ratio forms)
+    bool rot = true;
     int hack = 0;  // diag build only (MDP_JIT_HACK; results wrong): 1 = no log, no stores; 2 = no stores
     uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
