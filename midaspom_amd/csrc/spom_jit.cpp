@@ -312,6 +312,168 @@ std::string qsum_flat_code(uint32_t qml, uint32_t qun)
     return o.str();
 }
 
+// The fused prologue's phases with every column of the workgroup in one
+// lane (cmerge): a lane per item, per Q entry and per Z row computes the FC
+// columns' values, which sit interleaved in LDS (Zl[row][FC], Pl[item][FC],
+// the zero slot Pl[NITEMS][.]), so each table row is read once for all
+// columns and an item's or entry's gathers return the FC values together.
+// Roles start at different threads (Z rows from thread 0, items after
+// them, Q entries from the last thread down), so a wave seldom holds two.
+// Per (item, column), (row, column) and (entry, column) the arithmetic and
+// its order are those of the one-column-per-lane phases (same bits).
+std::string fused_merged_phases(uint32_t qml, uint32_t qun, int fc, const std::string &st5, const std::string &st1)
+{
+    const uint32_t G = 8, ngm = (qml + G - 1) / G;  // = kQGroup (spom_engine.hip)
+    uint32_t ngp = 1;
+    while (ngp < ngm) ngp *= 2;
+    std::ostringstream o;
+    o << "    constexpr int KZR = (NJ + NT - 1) / NT, KPC = (NITEMS + NT - 1) / NT, KQ = (LDQ + NT - 1) / NT;\n"
+         "#define ZW(k) ((k) * NT + threadIdx.x)\n"
+         "#define IW(k) ((k) * NT + (threadIdx.x + NT - (NJ < NT ? NJ : 0)) % NT)\n"
+         "#define QW(k) ((k) * NT + NT - 1 - threadIdx.x)\n"
+         // items: their descriptor and row pressures, the FC columns' products
+         "    double Fp[KPC][FC];\n"
+         "    u32 zi[KPC];\n"
+         "#pragma unroll\n"
+         "    for (int k = 0; k < KPC; ++k) {\n"
+         "        const u32 w = IW(k), it = w < NITEMS ? w : NITEMS - 1;\n"
+         "        const uint2 t = Itl[it];\n"
+         "        const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
+         "        double sv[NVAR];\n"
+         "#pragma unroll\n"
+         "        for (int b = 0; b < NVAR; ++b) sv[b] = Svl[r * NVAR + b];\n"
+         "        const u32 nB = ~B;\n"
+         "#pragma unroll\n"
+         "        for (int f = 0; f < FC; ++f) {\n"
+         "            const double c = cc[f];\n"
+         "            double fb[NVAR];\n"
+         "#pragma unroll\n"
+         "            for (int b = 0; b < NVAR; ++b) {\n"
+         "                const u32 bit = NVAR - 1 - b;\n"
+         "                const double pcv = c * sv[b];\n"
+         "                const double p = (pcv > 1.0) | ((j >> bit) & 1u) ? 1.0 : pcv;\n"
+         "                const double sg = __hiloint2double((int)(0x3ff00000u | ((nB << (31 - bit)) & 0x80000000u)), 0);\n"
+         "                fb[b] = fma(sg, p, fma(-0.5, sg, 0.5));\n"
+         "            }\n"
+         "#pragma unroll\n"
+         "            for (int s = 1; s < NVAR; s *= 2)\n"
+         "#pragma unroll\n"
+         "                for (int b = 0; b + s < NVAR; b += 2 * s) fb[b] *= fb[b + s];\n"
+         "            Fp[k][f] = fb[0];\n"
+         // (kept before the Z phase's barrier: otherwise the compiler sinks
+         // this arithmetic past it, where every wave waits on it)
+         "            asm volatile(\"\" : \"+v\"(Fp[k][f]));\n"
+         "        }\n"
+         "        zi[k] = r;\n"
+         "    }\n"
+         // Q entries: bounds and first item indices (past the count: the zero slot)
+         "    u32 qb[KQ], qn[KQ], qx[KQ][QUN];\n"
+         "#pragma unroll\n"
+         "    for (int k = 0; k < KQ; ++k) {\n"
+         "        const u32 w = QW(k);\n"
+         "        const bool live = w < LDQ && w < NCOEF;\n"
+         "        const u32 qc = live ? w : 0u, q0 = Qsl[qc], q1 = Qsl[qc + 1];\n"
+         "        qb[k] = live ? q0 : 0u;\n"
+         "        qn[k] = live ? q1 - q0 : 0u;\n"
+         "#pragma unroll\n"
+         "        for (int u = 0; u < QUN; ++u) { const u32 t_ = Qil[qb[k] + u]; qx[k][u] = (u32)u < qn[k] ? t_ : (u32)NITEMS; }\n"
+         "    }\n"
+         // Z rows: the row's explicit columns once, the FC columns' chains
+         "#pragma unroll\n"
+         "    for (int k = 0; k < KZR; ++k) {\n"
+         "        const u32 w = ZW(k);\n"
+         "        if (w < NJ) {\n"
+         "            const u32 r = w;\n"
+         "            double sk[KZ];\n"
+         "#pragma unroll\n"
+         "            for (u32 kk = 0; kk < KZ; kk += 2) {\n"
+         "                const double2 t2 = ((const double2 *)zl)[(ZPAD || kk < kmax ? kk : kk % 8u) / 2 * NJ + r];\n"
+         "                const bool in = ZPAD || kk < kmax;\n"
+         "                sk[kk] = in ? t2.x : 0.0;\n"
+         "                sk[kk + 1] = in ? t2.y : 0.0;\n"
+         "            }\n"
+         "            const double2 *zq = (const double2 *)(zcl + r * 8);\n"
+         "            const double2 p01 = zq[0], p23 = zq[1], p45 = zq[2], p67 = zq[3];\n"
+         "            double zf[FC];\n"
+         "#pragma unroll\n"
+         "            for (int f = 0; f < FC; ++f) {\n"
+         "                const double c = cc[f];\n"
+         "                double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
+         "#pragma unroll\n"
+         "                for (u32 kk = 0; kk < KZ; kk += 8) {\n"
+         "                    za *= fma(-c, sk[kk + 0], 1.0) * fma(-c, sk[kk + 4], 1.0);\n"
+         "                    zb *= fma(-c, sk[kk + 1], 1.0) * fma(-c, sk[kk + 5], 1.0);\n"
+         "                    zc *= fma(-c, sk[kk + 2], 1.0) * fma(-c, sk[kk + 6], 1.0);\n"
+         "                    zd *= fma(-c, sk[kk + 3], 1.0) * fma(-c, sk[kk + 7], 1.0);\n"
+         "                }\n"
+         "                double z = (za * zb) * (zc * zd);\n"
+         "                if (kmax && !(fma(-c, sk[0], 1.0) > 0.0)) z = 0.0;\n"
+         "                double q = p67.y;\n"
+         "                q = fma(q, c, p67.x);\n"
+         "                q = fma(q, c, p45.y);\n"
+         "                q = fma(q, c, p45.x);\n"
+         "                q = fma(q, c, p23.y);\n"
+         "                q = fma(q, c, p23.x);\n"
+         "                q = fma(q, c, p01.y);\n"
+         "                q = fma(q, c, p01.x);\n"
+         "                zf[f] = z * exp(-(q * c));\n"
+         "            }\n"
+         "#pragma unroll\n"
+         "            for (int f = 0; f < FC; ++f) Zl[r * FC + f] = zf[f];\n"
+         "        }\n"
+         "    }\n"
+         "    __syncthreads();\n"
+      << st5 <<
+         // Pc per (item, column), and the zero slot
+         "#pragma unroll\n"
+         "    for (int k = 0; k < KPC; ++k) {\n"
+         "        const u32 w = IW(k);\n"
+         "        if (w < NITEMS) {\n"
+         "#pragma unroll\n"
+         "            for (int f = 0; f < FC; ++f) Pl[w * FC + f] = Zl[zi[k] * FC + f] * Fp[k][f];\n"
+         "        }\n"
+         "    }\n"
+         "    if (threadIdx.x < FC) Pl[NITEMS * FC + threadIdx.x] = 0.0;\n"
+         "    __syncthreads();\n"
+      << st1 <<
+         // Q entries: every gather unconditional, the canonical order per column
+         "#pragma unroll\n"
+         "    for (int k = 0; k < KQ; ++k) {\n"
+         "        const u32 w = QW(k);\n"
+         "        if (w < LDQ) {\n"
+         "            double p_[" << qml << "][FC];\n";
+    for (uint32_t u = 0; u < qml; ++u) {
+        const std::string idx = u < qun ? "qx[k][" + std::to_string(u) + "]"
+                                        : "(" + std::to_string(u) + "u < qn[k] ? Qil[qb[k] + " + std::to_string(u) +
+                                              "u] : (u32)NITEMS)";
+        o << "            { const u32 x_ = " << idx << ";\n"
+             "#pragma unroll\n"
+             "              for (int f = 0; f < FC; ++f) p_[" << u << "][f] = Pl[x_ * FC + f]; }\n";
+    }
+    o << "#pragma unroll\n"
+         "            for (int f = 0; f < FC; ++f) {\n"
+         "                double g_[" << ngp << "];\n";
+    for (uint32_t g = 0; g < ngp; ++g) {
+        if (g >= ngm) {
+            o << "                g_[" << g << "] = 0.0;\n";
+            continue;
+        }
+        o << "                g_[" << g << "] = p_[" << G * g << "][f]";
+        for (uint32_t u = 1; u < G && G * g + u < qml; ++u) o << " + p_[" << G * g + u << "][f]";
+        o << ";\n";
+    }
+    for (uint32_t w = ngp; w > 1; w /= 2)
+        for (uint32_t i = 0; i < w / 2; ++i)
+            o << "                g_[" << i << "] = g_[" << 2 * i << "] + g_[" << 2 * i + 1 << "];\n";
+    o << "                Ql[f * LDQ + w] = g_[0];\n"
+         "                Ql[FC * LDQ + f * LDQ + REVQ[w]] = g_[0];\n"
+         "            }\n"
+         "        }\n"
+         "    }\n";
+    (void)fc;
+    return o.str();
+}
+
 int mdp_jit_default_epl(const std::vector<uint32_t> &) { return 2; }
 
 uint32_t mdp_jit_end_exp(const MdpJitPlan &plan) { return schedule(plan).final_exp; }
@@ -606,7 +768,12 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                     "    }\n"
                     "    __syncthreads();\n"
                   : "")
-          << stamp(4) <<
+          << stamp(4);
+        if (pl.cmerge && FC > 1)
+            o << fused_merged_phases(std::max<uint32_t>(1u, pl.qmaxlen),
+                                     std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u), FC, stamp(5), stamp(1));
+        else
+            o <<
              // operands of the Pc and Q phases that do not depend on Z, read
              // and combined before the Z phase: per item its Z slot and the
              // product F of its var-column factors (a fixed pairwise tree),

@@ -36,6 +36,9 @@ struct MdpJitPlan {
     // several columns per workgroup: each column's lanes rotated by half a
     // block (SIMD balance of the ratio forms)
     bool rot = true;
+    // fused prologue: one lane per item / Q entry / Z row for all the
+    // workgroup's columns, per-column values interleaved in LDS
+    bool cmerge = false;  // measured slower (phase 2 4.3 k vs 2.4 k cycles: twice the VALU chain per lane)
     int hack = 0;  // diag build only (MDP_JIT_HACK; results wrong): 1 = no log, no stores; 2 = no stores
     uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
