@@ -1302,7 +1302,7 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
     "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_FUSED_SBUILD", "MDP_JIT_SPLIT",
-    "MDP_JIT_EARLYW", "MDP_FUSED_BAL", "MDP_FUSED_QFLAT", "MDP_FUSED_PH2FLAT", "MDP_JIT_ROT", "MDP_FUSED_CMERGE"};
+    "MDP_JIT_EARLYW", "MDP_FUSED_BAL", "MDP_FUSED_QFLAT", "MDP_FUSED_PH2FLAT", "MDP_JIT_ROT", "MDP_FUSED_CMERGE", "MDP_FUSED_DIRECT"};
 const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
@@ -2880,6 +2880,7 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
             if (const char *sv = eng->opts.get("MDP_FUSED_PH2FLAT")) plan.ph2flat = atoi(sv) != 0;
             if (const char *sv = eng->opts.get("MDP_JIT_ROT")) plan.rot = atoi(sv) != 0;
             if (const char *sv = eng->opts.get("MDP_FUSED_CMERGE")) plan.cmerge = atoi(sv) != 0;
+            if (const char *sv = eng->opts.get("MDP_FUSED_DIRECT")) plan.direct = atoi(sv) != 0;
             if (plan.sbuild) {  // var-column rows, items, CSR, series, column lists, row states
                 plan.off_mv = 0;
                 plan.off_it = even((size_t)eng->nvar * eng->n);

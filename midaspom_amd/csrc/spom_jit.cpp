@@ -702,10 +702,16 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    __shared__ double Zl[FC * NJ];\n"
              "#define PLS (NITEMS + 1)\n"  // a column's items, then its zero slot (the flat Q sums' padding)
              "    __shared__ double Pl[FC * PLS];\n"
-             "    const uint2 *Itl = (const uint2 *)(ct + OFF_IT);\n"
-             "    const u32 *Qsl = (const u32 *)(ct + OFF_QS);\n"
-             "    const u32 *Qil = (const u32 *)(ct + OFF_QI);\n"
-             "    const double *zcl = ct + OFF_ZC;\n"
+          << (pl.direct && !pl.sbuild
+                  // direct: the phases read the column tables where they lie
+                  // (HBM / L2) instead of a staged LDS image -- no staging
+                  // round trip and barrier before the first table read
+                  ? "    const double *ctg = coltab;\n"
+                  : "    const double *ctg = ct;\n") <<
+             "    const uint2 *Itl = (const uint2 *)(ctg + OFF_IT);\n"
+             "    const u32 *Qsl = (const u32 *)(ctg + OFF_QS);\n"
+             "    const u32 *Qil = (const u32 *)(ctg + OFF_QI);\n"
+             "    const double *zcl = ctg + OFF_ZC;\n"
           << (pl.sbuild
                   // the colonisation sums are built here (S-build, below) from the
                   // var columns' dispersal rows: half the bytes to stage
@@ -716,13 +722,12 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
                     "    const double *Mvl = ct + OFF_MV;\n"
                     "    const ZCT *Zcl = (const ZCT *)(ct + OFF_ZL);\n"
                     "    const u32 *Rjl = (const u32 *)(ct + OFF_RJ);\n"
-                  : "    const double *Svl = ct;\n"
-                    "    const double *zl = ct + OFF_ZS;\n") <<
+                  : "    const double *Svl = ctg;\n"
+                    "    const double *zl = ctg + OFF_ZS;\n") <<
              "    double cc[FC];\n"
              "#pragma unroll\n"
              "    for (int f = 0; f < FC; ++f) cc[f] = ic0 + f < nc ? cvals[ic0 + f] : 0.0;\n"
-          <<
-             "    {\n"
+          << (pl.direct && !pl.sbuild ? "    if (false) {\n" : "    {\n") <<
              "        const double2 *src = (const double2 *)coltab;\n"
              "        double2 *dst = (double2 *)ct;\n"
              "        const u32 n2 = ct_len / 2;\n"
@@ -740,7 +745,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "            dst[i < n2 ? i : n2] = t[k];\n"
              "        }\n"
              "    }\n"
-             "    __syncthreads();\n"
+          << (pl.direct && !pl.sbuild ? "" : "    __syncthreads();\n")
           << (pl.sbuild
                   // S-build: per row r (hidden state j) its explicit columns'
                   // S[j][k] into the zs image (row pairs [k/2][r][k%2]) and its

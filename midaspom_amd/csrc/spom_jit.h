@@ -38,7 +38,10 @@ struct MdpJitPlan {
     bool rot = true;
     // fused prologue: one lane per item / Q entry / Z row for all the
     // workgroup's columns, per-column values interleaved in LDS
-    bool cmerge = false;  // measured slower (phase 2 4.3 k vs 2.4 k cycles: twice the VALU chain per lane)
+    bool cmerge = false;
+    // fused prologue reads the column tables from HBM / L2 where used
+    // instead of staging them in LDS first
+    bool direct = false;  // measured slower (phase 2 4.3 k vs 2.4 k cycles: twice the VALU chain per lane)
     int hack = 0;  // diag build only (MDP_JIT_HACK; results wrong): 1 = no log, no stores; 2 = no stores
     uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
