@@ -380,8 +380,11 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // by one double2 so rows read by one wave fall on different banks
     constexpr uint32_t PRS = CB * NV + 2;
     double *Prl = Zl + (((size_t)nrows * CB + 1) & ~(size_t)1);  // [nrows][PRS], 16-byte aligned
-    double *Pl = Prl + (size_t)nrows * PRS;            // [CB/CP][nitems][CP]
-    uint2 *It = (uint2 *)(Pl + (size_t)nitems * CB);   // [nitems] {B, j}, row in the top bytes
+    // Pc per item and c, one more slot per c value after the items: zero,
+    // the padding phase 3's unconditional gathers read past an entry's end
+    const uint32_t npl = nitems + 1;
+    double *Pl = Prl + (size_t)nrows * PRS;            // [CB/CP][npl][CP]
+    uint2 *It = (uint2 *)(Pl + (size_t)npl * CB);      // [nitems] {B, j}, row in the top bytes
     uint32_t *Qs = (uint32_t *)(It + nitems);          // [ncoef + 1]
     uint32_t *Qi = Qs + ncoef + 1;                     // [nqi]
     double cv[CB];  // this workgroup's c values (the last one again past the grid: never stored)
@@ -475,9 +478,12 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         double pr[NV];
 #pragma unroll
         for (int b = 0; b < NV; ++b) {
-            // min(1, c S) as the reference clamps it (:355-357): NaN stays NaN
-            const double t = (EXACT || (uint32_t)b < nvar) ? c * sv[(size_t)r * nvar + b] : 0.0;
-            pr[b] = t > 1.0 ? 1.0 : t;
+            // min(1, c S) as the reference clamps it (:355-357): NaN stays NaN;
+            // exactly 1.0 for the columns of j (sv -1) and the padded slots, so
+            // that phase 2's fma(s, p, n) gives their factor 1.0 with no select
+            const double sb = (EXACT || (uint32_t)b < nvar) ? sv[(size_t)r * nvar + b] : -1.0;
+            const double t = c * sb;
+            pr[b] = sb < 0.0 || t > 1.0 ? 1.0 : t;
         }
         double2 *pd = (double2 *)(Prl + (size_t)r * PRS + cl * NV);
 #pragma unroll
@@ -499,13 +505,15 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         // padded slots select exactly 1.0 (a product 0 * p would turn an
         // infinite pressure into NaN) -- the values (hence the bits) are the
         // fused kernel's
+        // (the columns of j have B_b set, j <= B, and the padded slots are
+        // taken as set: their factor is fma(1, 1.0, 0) = 1.0 -- phase 1 stores
+        // pressure 1.0 there -- the value the select form gave)
         double sg[NV], nb[NV];
-        bool onef[NV];
+        (void)J;
 #pragma unroll
         for (int b = 0; b < NV; ++b) {
             const uint32_t bit = EXACT ? (uint32_t)(NV - 1 - b) : nvar - 1 - (uint32_t)b;  // wraps past nvar
-            onef[b] = (!EXACT && (uint32_t)b >= nvar) || ((J >> bit) & 1u);
-            const uint32_t nbit = (nB >> bit) & 1u;
+            const uint32_t nbit = !EXACT && (uint32_t)b >= nvar ? 0u : (nB >> bit) & 1u;
             sg[b] = __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
             nb[b] = __hiloint2double((int)(nbit * 0x3ff00000u), 0);
         }
@@ -519,8 +527,8 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
 #pragma unroll
             for (int b = 0; b < NV / 2; ++b) {
                 const double2 p2 = ps[b];
-                f[2 * b] = onef[2 * b] ? 1.0 : fma(sg[2 * b], p2.x, nb[2 * b]);
-                f[2 * b + 1] = onef[2 * b + 1] ? 1.0 : fma(sg[2 * b + 1], p2.y, nb[2 * b + 1]);
+                f[2 * b] = fma(sg[2 * b], p2.x, nb[2 * b]);
+                f[2 * b + 1] = fma(sg[2 * b + 1], p2.y, nb[2 * b + 1]);
             }
 #pragma unroll
             for (int sh = 1; sh < NV; sh *= 2)
@@ -529,8 +537,9 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
             pc[i] = zr[i] * f[0];
         }
 #pragma unroll
-        for (int i = 0; i < CB; ++i) Pl[pix(nitems, it, i)] = pc[i];
+        for (int i = 0; i < CB; ++i) Pl[pix(npl, it, i)] = pc[i];
     }
+    if (threadIdx.x < CB) Pl[pix(npl, nitems, threadIdx.x)] = 0.0;
     __syncthreads();
     MDP_STAMP(stamps, 2);
     // 3. Q rows in the canonical order.  Each entry owns an aligned
@@ -557,17 +566,20 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
 #pragma unroll
                 for (int i = 0; i < CB; ++i) sg[i] = 0.0;
                 if (j0 >= i1) return;
+                // items past the entry read the zero slot: x + (+0.0) = x for
+                // these non-negative (or NaN / inf) values, so the sums are the
+                // canonical order's bits without a select per item
                 uint32_t itm[kQGroup];
 #pragma unroll
-                for (uint32_t u = 0; u < kQGroup; ++u) itm[u] = Qi[j0 + u < i1 ? j0 + u : j0];
+                for (uint32_t u = 0; u < kQGroup; ++u) {
+                    const uint32_t t_ = Qi[j0 + u < i1 ? j0 + u : j0];
+                    itm[u] = j0 + u < i1 ? t_ : nitems;
+                }
 #pragma unroll
                 for (int i = 0; i < CB; ++i) {
-                    double x = Pl[pix(nitems, itm[0], i)];
+                    double x = Pl[pix(npl, itm[0], i)];
 #pragma unroll
-                    for (uint32_t u = 1; u < kQGroup; ++u) {
-                        const double y = Pl[pix(nitems, itm[u], i)];
-                        x = j0 + u < i1 ? x + y : x;
-                    }
+                    for (uint32_t u = 1; u < kQGroup; ++u) x = x + Pl[pix(npl, itm[u], i)];
                     sg[i] = x;
                 }
             };
@@ -1744,7 +1756,7 @@ constexpr size_t kFusedLdsMax = 64 * 1024;  // fused forward kernel: every table
 size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
 {
     const size_t nv = eng->nvar <= 8 ? 8 : eng->nvar <= 16 ? 16 : 24;  // k_qrows NV
-    return ((((size_t)cb * eng->nj + 1) & ~(size_t)1) + (size_t)eng->nj * (cb * nv + 2) + (size_t)cb * eng->nitems) *
+    return ((((size_t)cb * eng->nj + 1) & ~(size_t)1) + (size_t)eng->nj * (cb * nv + 2) + (size_t)cb * (eng->nitems + 1)) *
                sizeof(double) +
            (size_t)eng->nitems * sizeof(uint2) + ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);
 }
