@@ -1121,6 +1121,111 @@ __global__ __launch_bounds__(kBlock) void k_wq(uint32_t c0, uint32_t nitems, con
     Q[(size_t)(c0 + cl) * ldQ + q] = a;
 }
 
+// Wide years on the matrix cores (FP64 MFMA, v_mfma_f64_16x16x4_f64).  For
+// one column c and a block of kMmaPts points, year t's new state vector is
+//     n[p][l] = sum_(k, m) W[p][(k, m)] C[(k, m)][l],
+//     W[p][(k, m)] = v[p][k] x_p^(|A_k| - m) y_p^m,   C[(k, m)][l] = Q_kl[m]
+// (0 past the transition's nX): the transition P[k][l] = sum_m Q_kl[m]
+// x^(|A|-m) y^m of the wide kernels (direct weights, as k_fwd_wide), summed
+// over K = every source's (k, m <= |A_k|) -- one GEMM per year of M = the
+// points, N = the new states, K = sum_k (|A_k| + 1), on the matrix cores with
+// the states of the block's points in LDS.  C's fragments are gathered from
+// the column's Q row through a host index table (gidx, c-independent: the
+// Q-row slot of each (K, l), or none); W's are formed from the states and
+// per-point power tables in LDS.  The products sum in another order than
+// k_fwd_wide's (positive terms: ~1e-15 relative).
+constexpr uint32_t kMmaPts = 64;        // points per workgroup (4 row tiles of 16)
+constexpr uint32_t kMmaThreads = 256;   // 4 waves
+constexpr uint32_t kMmaNone = 0xffffffffu;
+typedef double mdp_d4 __attribute__((ext_vector_type(4)));
+template <int NPM>  // states per year, padded to 16 (64 or 128)
+__global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
+    const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint32_t *__restrict__ kt,
+    const uint32_t *__restrict__ kbase, const uint32_t *__restrict__ gidx, const uint32_t *__restrict__ gbase,
+    uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne, uint32_t c0, uint32_t maxA,
+    double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
+{
+    extern __shared__ __attribute__((aligned(16))) double mlds[];
+    double *Va = mlds, *Vb = mlds + (size_t)NPM * kMmaPts;           // [state][point]
+    double *xp = Vb + (size_t)NPM * kMmaPts, *yp = xp + (size_t)(maxA + 1) * kMmaPts;  // [r][point]
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t p0 = blockIdx.x * kMmaPts, ic = c0 + blockIdx.y;
+    if (threadIdx.x < kMmaPts) {
+        const uint32_t ie = p0 + threadIdx.x;
+        const double e = ie < ne ? evals[ie] : 0.0;
+        const double x = e > 1.0 ? 1.0 : e, y = 1.0 - x;
+        double a = 1.0, b = 1.0;
+        for (uint32_t r = 0; r <= maxA; ++r) {
+            xp[r * kMmaPts + threadIdx.x] = a;
+            yp[r * kMmaPts + threadIdx.x] = b;
+            a *= x;
+            b *= y;
+        }
+    }
+    const uint32_t np0 = np[0];
+    for (uint32_t i = threadIdx.x; i < (uint32_t)NPM * kMmaPts; i += kMmaThreads) Va[i] = i / kMmaPts < np0 ? 1.0 : 0.0;
+    __syncthreads();
+    const double *q = Q + (size_t)ic * ldQ;
+    const uint32_t kk = lane >> 4, col = lane & 15u;
+    for (uint32_t t = 1; t < tmax; ++t) {
+        const uint32_t npc = np[t], ncol = (npc + 15) / 16;
+        const uint32_t k0 = kbase[t], nstep = (kbase[t + 1] - k0) / 4, npcp = ncol * 16;
+        const uint32_t *gt = gidx + gbase[t];
+        // this wave's column tiles: wv, wv + 4 (NPM / 16 <= 8)
+        for (uint32_t ct = wv; ct < ncol; ct += kMmaThreads / 64) {
+            mdp_d4 acc[kMmaPts / 16];
+#pragma unroll
+            for (uint32_t rt = 0; rt < kMmaPts / 16; ++rt) acc[rt] = mdp_d4{0.0, 0.0, 0.0, 0.0};
+            const uint32_t lc = ct * 16 + col;
+            // software pipeline: the (k, a, m) entry and the C index two steps
+            // ahead, the C value one step ahead (steps past the end reload
+            // the last one: valid addresses, never used)
+            auto ent = [&](uint32_t st) { return kt[k0 + (st < nstep ? st : nstep - 1) * 4 + kk]; };
+            auto gix = [&](uint32_t st) { return gt[((st < nstep ? st : nstep - 1) * 4 + kk) * npcp + lc]; };
+            auto cval = [&](uint32_t g) {
+                const double v = q[g == kMmaNone ? 0u : g];
+                return g == kMmaNone ? 0.0 : v;
+            };
+            uint32_t e_cur = ent(0), e_nxt = ent(1), g_nxt = gix(1);
+            double b_cur = cval(gix(0));
+            for (uint32_t st = 0; st < nstep; ++st) {
+                const uint32_t e_n2 = ent(st + 2), g_n2 = gix(st + 2);
+                const double b_nxt = cval(g_nxt);
+                // W for the four row tiles: the source's state times its weight
+                const uint32_t k = e_cur & 0xffu, a = (e_cur >> 8) & 0xffu, m = (e_cur >> 16) & 0xffu;
+                const bool ok = (e_cur >> 31) != 0u;
+#pragma unroll
+                for (uint32_t rt = 0; rt < kMmaPts / 16; ++rt) {
+                    const uint32_t pp = rt * 16 + col;
+                    const double w = xp[(ok ? a - m : 0u) * kMmaPts + pp] * yp[(ok ? m : 0u) * kMmaPts + pp];
+                    const double av = ok ? Va[k * kMmaPts + pp] * w : 0.0;
+                    acc[rt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b_cur, acc[rt], 0, 0, 0);
+                }
+                e_cur = e_nxt;
+                e_nxt = e_n2;
+                b_cur = b_nxt;
+                g_nxt = g_n2;
+            }
+            // n[p][l]: lane holds column l = ct*16 + col, rows kk + 4 r of each tile
+            if (lc < npc)
+#pragma unroll
+                for (uint32_t rt = 0; rt < kMmaPts / 16; ++rt)
+#pragma unroll
+                    for (uint32_t r = 0; r < 4; ++r) Vb[lc * kMmaPts + rt * 16 + kk + 4 * r] = acc[rt][r];
+        }
+        __syncthreads();
+        double *tv = Va;
+        Va = Vb;
+        Vb = tv;
+    }
+    if (threadIdx.x < kMmaPts) {
+        const uint32_t ie = p0 + threadIdx.x, npl = np[tmax - 1];
+        double L = 0.0;
+        for (uint32_t l = 0; l < npl; ++l) L += Va[l * kMmaPts + threadIdx.x] * prior0;
+        if (ie < ne) out[(size_t)ie * ld_out + (size_t)ic * out_cs] = log(L);
+    }
+}
+
 typedef const __attribute__((address_space(4))) uint32_t cuint;
 
 // Forward recursion with the state vectors in HBM: lane per e value, one c
@@ -1290,6 +1395,7 @@ struct DevCtx {
     double *Pg = nullptr, *V = nullptr;
     size_t cap_pg = 0, cap_v = 0;
     uint32_t *np_d = nullptr, *udesc_w = nullptr;
+    uint32_t *mma_kt = nullptr, *mma_kbase = nullptr, *mma_gidx = nullptr, *mma_gbase = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     std::vector<uint8_t> ev_mask;  // per profiled run: slots whose kernel was launched
@@ -1314,7 +1420,7 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
     "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_FUSED_SBUILD", "MDP_JIT_SPLIT",
-    "MDP_JIT_EARLYW", "MDP_FUSED_BAL", "MDP_FUSED_QFLAT", "MDP_FUSED_PH2FLAT", "MDP_JIT_ROT", "MDP_FUSED_CMERGE", "MDP_FUSED_DIRECT"};
+    "MDP_JIT_EARLYW", "MDP_FUSED_BAL", "MDP_FUSED_QFLAT", "MDP_FUSED_PH2FLAT", "MDP_JIT_ROT", "MDP_FUSED_CMERGE", "MDP_FUSED_DIRECT", "MDP_WIDE_MMA"};
 const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
@@ -1407,6 +1513,12 @@ struct mdp_engine {
     std::vector<uint32_t> cj_bits, cj_item0, itemB, qstart, qitem, udesc_d, var_cols;
     std::vector<uint32_t> itemRow;  // row (j slot) of each item
     std::vector<uint2> qslot;       // k_qrows phase-3 lanes (build_direct_plan)
+    // k_fwd_mma (wide years on the matrix cores): per year t its K entries
+    // (k | |A_k| << 8 | m << 16 | valid << 31, padded to 4) from kbase[t],
+    // and the Q-row slot of each (K entry, new state l) from gbase[t]
+    bool mma = false;
+    uint32_t mma_npm = 0;
+    std::vector<uint32_t> mma_kt, mma_kbase, mma_gidx, mma_gbase;
     uint32_t qslot_lglmax = 0;      // log2 of the widest lane segment
     std::vector<uint8_t> isvar;
     std::vector<double> Sj;  // [nj][n] colonisation sums of every column for each needed j
@@ -1746,7 +1858,55 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
     double f = 2.0 * (eng->maxA + 1) + 2.0 * eng->np[eng->tmax - 1];
     for (uint32_t d : eng->udesc_d) f += 3.0 * (((d >> kOffBits) & 31u) + 1.0) + 2.0;
     eng->wide_flops_pt = f;
+    // k_fwd_mma's tables (c-independent): years of at most 128 states, at
+    // most 24 occupied patches a state (its per-point power tables)
+    eng->mma = false;
+    if (eng->npmax <= 128 && eng->maxA <= 24) {
+        const char *mv = eng->opts.get("MDP_WIDE_MMA");
+        if (!mv || atoi(mv) != 0) {
+            eng->mma = true;
+            eng->mma_npm = eng->npmax <= 64 ? 64u : 128u;
+            eng->mma_kt.clear();
+            eng->mma_gidx.clear();
+            eng->mma_kbase.assign(eng->tmax + 1, 0u);
+            eng->mma_gbase.assign(eng->tmax + 1, 0u);
+            size_t ub = 0;
+            for (uint32_t t = 1; t < eng->tmax; ++t) {
+                const uint32_t npp = eng->np[t - 1], npc = eng->np[t], npcp = (npc + 15) / 16 * 16;
+                eng->mma_kbase[t] = (uint32_t)eng->mma_kt.size();
+                eng->mma_gbase[t] = (uint32_t)eng->mma_gidx.size();
+                for (uint32_t k = 0; k < npp; ++k) {
+                    const uint32_t a = eng->udesc_d[ub + k] >> 27;  // |A_k| (any use from k; l = 0)
+                    for (uint32_t m = 0; m <= a; ++m) eng->mma_kt.push_back(k | (a << 8) | (m << 16) | (1u << 31));
+                }
+                while (eng->mma_kt.size() % 4) eng->mma_kt.push_back(0u);
+                for (size_t i = eng->mma_kbase[t]; i < eng->mma_kt.size(); ++i) {
+                    const uint32_t en = eng->mma_kt[i], k = en & 0xffu, m = (en >> 16) & 0xffu;
+                    for (uint32_t l = 0; l < npcp; ++l) {
+                        uint32_t g = kMmaNone;
+                        if ((en >> 31) && l < npc) {
+                            const uint32_t dsc = eng->udesc_d[ub + (size_t)l * npp + k];
+                            const uint32_t off = dsc & kOffMask, nX = (dsc >> kOffBits) & 31u;
+                            if (m <= nX) g = off + m;
+                        }
+                        eng->mma_gidx.push_back(g);
+                    }
+                }
+                ub += (size_t)npp * npc;
+            }
+            eng->mma_kbase[eng->tmax] = (uint32_t)eng->mma_kt.size();
+            eng->mma_gbase[eng->tmax] = (uint32_t)eng->mma_gidx.size();
+            if (eng->mma_kt.empty()) eng->mma_kt.push_back(0u);
+            if (eng->mma_gidx.empty()) eng->mma_gidx.push_back(kMmaNone);
+        }
+    }
     return MDP_OK;
+}
+
+// k_fwd_mma: two state buffers and the power tables of kMmaPts points
+size_t mma_lds(const mdp_engine *eng)
+{
+    return (2 * (size_t)eng->mma_npm + 2 * ((size_t)eng->maxA + 1)) * kMmaPts * sizeof(double);
 }
 
 constexpr size_t kQrowsLdsMax = 160 * 1024;
@@ -2160,6 +2320,13 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
             return rc;
         if (eng->wide) {
             if ((rc = dev_upload(&d.np_d, eng->np)) || (rc = dev_upload(&d.udesc_w, eng->udesc_d))) return rc;
+            if (eng->mma &&
+                ((rc = dev_upload(&d.mma_kt, eng->mma_kt)) || (rc = dev_upload(&d.mma_kbase, eng->mma_kbase)) ||
+                 (rc = dev_upload(&d.mma_gidx, eng->mma_gidx)) || (rc = dev_upload(&d.mma_gbase, eng->mma_gbase))))
+                return rc;
+            if (eng->mma)
+                HIP_TRY(hipFuncSetAttribute(eng->mma_npm == 64 ? (const void *)k_fwd_mma<64> : (const void *)k_fwd_mma<128>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)mma_lds(eng)));
             HIP_TRY(hipFuncSetAttribute((const void *)k_fwd_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)wide_lds(eng)));
             return MDP_OK;
@@ -2195,6 +2362,7 @@ void free_device(DevCtx &d)
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
                     d.zs, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
                     d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot,
+                    d.mma_kt, d.mma_kbase, d.mma_gidx, d.mma_gbase,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -2267,13 +2435,13 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     }
     if (eng->wide) {
         // c values per k_fwd_wide launch: the two state vectors of every
-        // point of a launch within kWideVBytes
+        // point of a launch within kWideVBytes (k_fwd_mma keeps them in LDS)
         const size_t ne_pad = (size_t)std::max<uint32_t>(1u, (ne + kBlock - 1) / kBlock) * kBlock;
         const size_t cap_c = std::max<size_t>(1, std::min<size_t>(nc, 65535));
         d.wide_cb_fwd = (uint32_t)std::min(cap_c, std::max<size_t>(1, kWideVBytes / 8 / (2 * (size_t)eng->npmax * ne_pad)));
         if (const char *cv = eng->opts.get("MDP_WIDE_CB"))
             d.wide_cb_fwd = std::min(d.wide_cb_fwd, (uint32_t)std::max(1, atoi(cv)));
-        if ((rc = dev_reserve(&d.V, &d.cap_v, 2 * (size_t)eng->npmax * d.wide_cb_fwd * ne_pad))) return rc;
+        if (!eng->mma && (rc = dev_reserve(&d.V, &d.cap_v, 2 * (size_t)eng->npmax * d.wide_cb_fwd * ne_pad))) return rc;
     } else if (eng->jit) {
         // forward kernels with several points per lane read them from a list
         // that puts only e rows of one ratio form in a lane (spom_jit.cpp)
@@ -2495,6 +2663,20 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
             note_launch(eng, "k_wq");
             hipLaunchKernelGGL(k_wq, gq, dim3(kBlock), 0, s, c0, eng->nitems, d.Pg, eng->ncoef_d, d.qstart, d.qitem,
                                d.Qrow, (uint32_t)eng->ldQ);
+        }
+    } else if (eng->mma) {  // the matrix-core forward: every c in one launch (no HBM state scratch)
+        uint32_t se = os.se, sc = os.sc;
+        for (uint32_t c0 = 0; c0 < d.nc; c0 += 65535) {
+            const uint32_t n = std::min(65535u, d.nc - c0);
+            const dim3 g((d.ne + kMmaPts - 1) / kMmaPts, n);
+            note_launch(eng, "k_fwd_mma<%u>", eng->mma_npm);
+#define MDP_MMA(NPM) \
+    hipLaunchKernelGGL((k_fwd_mma<NPM>), g, dim3(kMmaThreads), mma_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.np_d, \
+                       d.mma_kt, d.mma_kbase, d.mma_gidx, d.mma_gbase, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, \
+                       out, se, sc)
+            if (eng->mma_npm == 64) MDP_MMA(64);
+            else MDP_MMA(128);
+#undef MDP_MMA
         }
     } else {
         const uint32_t cb = d.wide_cb_fwd;
@@ -3219,7 +3401,7 @@ int mdp_engine_kernel_ms(mdp_engine *eng, double *ms, int max_k)
 const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
     if (!eng || k < 0 || k >= 3) return "";
-    if (eng->wide) return k < 2 && !eng->nitems ? "" : kKernelNames[2][k];
+    if (eng->wide) return k < 2 && !eng->nitems ? "" : k == 2 && eng->mma ? "k_fwd_mma" : kKernelNames[2][k];
     if (eng->jit && eng->qglobal)  // Q rows built in HBM, then the hipRTC forward kernel
         return k < 2 && !eng->nitems ? "" : k == 2 ? "k_forward" : kKernelNames[2][k];
     // direct path: Z rows inside k_qrows (slot 0 idle); fused: one kernel

@@ -24,11 +24,11 @@ from midaspom_amd import synth  # noqa: E402
 tmp = Path(tempfile.mkdtemp())
 PATHS = {  # path name -> engine knobs
     "default": {}, "nosplit": {"MDP_VSPLIT": "1"}, "split2": {"MDP_VSPLIT": "2"}, "split4": {"MDP_VSPLIT": "4"},
-    "wide": {"MDP_WIDE": "1"},
+    "wide": {"MDP_WIDE": "1"}, "wideplain": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "0"},
     "epl2": {"MDP_VLDS_EPL": "2"},
 }
 CASES = [(0.45, 30, 512, p) for p in os.environ.get("WIDE_PATHS", "default,nosplit,wide").split(",")]
-CASES.append((0.6, 50, 256, "default"))
+CASES += [(0.6, 50, 256, p) for p in os.environ.get("WIDE60_PATHS", "default").split(",")]
 for pmiss, T, s, path in CASES:
     for k in [k for k in os.environ if k.startswith("MDP_")]:
         os.environ.pop(k, None)
@@ -60,7 +60,7 @@ for pmiss, T, s, path in CASES:
     per_pt = (time.perf_counter() - t0) / 8
     w = eng.work(s, s)
     fa = eng.work_fact(s, s)  # the algorithmic minimum (each distinct transition once per point)
-    fwd = [v for k, v in kms.items() if k in ("k_forward", "k_fwd_wide")]
+    fwd = [v for k, v in kms.items() if k in ("k_forward", "k_fwd_wide", "k_fwd_mma")]
     print(json.dumps({"pmiss": pmiss, "years": T, "grid": s, "path": path, "npstates_max": int(model.npstates.max()),
                       "nuses": eng.info()["nuses"], "variant": eng.info()["variant"], "create_s": t_create,
                       "launched": sorted(eng.launched()), "step_ms": step * 1e3,

@@ -60,7 +60,7 @@ def _reference(nvar):
 
 
 def _run(model, e, c, env, monkeypatch):
-    for k in ("MDP_JIT", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB"):
+    for k in ("MDP_JIT", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB", "MDP_WIDE_MMA"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -128,13 +128,16 @@ def test_generic_path(nvar, monkeypatch):
 
 @pytest.mark.parametrize("nvar", sorted(PROBLEMS))
 @pytest.mark.parametrize("chunked", [False, True])
-def test_wide_path(nvar, chunked, monkeypatch):
-    """MDP_WIDE=1: k_zrows + k_witems<NV> + k_wq + k_fwd_wide (whole and
-    one c value per launch)."""
+@pytest.mark.parametrize("mma", [True, False])
+def test_wide_path(nvar, chunked, mma, monkeypatch):
+    """MDP_WIDE=1: k_zrows + k_witems<NV> + k_wq + the forward on the matrix
+    cores, k_fwd_mma (or k_fwd_wide, MDP_WIDE_MMA=0), whole and one c value
+    per item launch."""
     _, model = _problem(nvar)
     ie, ic, ref = _reference(nvar)
-    env = {"MDP_WIDE": "1", **({"MDP_WIDE_CB": "1"} if chunked else {})}
+    env = {"MDP_WIDE": "1", **({"MDP_WIDE_CB": "1"} if chunked else {}), **({} if mma else {"MDP_WIDE_MMA": "0"})}
     got, launched, info = _run(model, E_SMALL, C_SMALL, env, monkeypatch)
     assert info["variant"] >= 20000
-    assert {f"k_witems<{NV[nvar]}>", "k_wq", "k_fwd_wide", "k_zrows"} <= launched, launched
+    fwd = "k_fwd_mma<64>" if mma else "k_fwd_wide"
+    assert {f"k_witems<{NV[nvar]}>", "k_wq", fwd, "k_zrows"} <= launched, launched
     assert_loglik_close(got[ie, ic], ref)

@@ -16,7 +16,7 @@ GOLDEN = Path(__file__).parent / "golden"
 
 pytestmark = pytest.mark.gpu
 
-KNOBS = ("MDP_JIT", "MDP_FUSED", "MDP_WIDE", "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_VSPLIT")
+KNOBS = ("MDP_JIT", "MDP_FUSED", "MDP_WIDE", "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_VSPLIT", "MDP_WIDE_MMA")
 
 
 def _run_both(model, e, c, env, monkeypatch):
@@ -58,7 +58,9 @@ CASES = {
     "lds_states": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37, {},
                    "mdp_fwd_jit<reading"),
     "wide": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
-             {"MDP_WIDE": "1"}, "k_fwd_wide"),
+             {"MDP_WIDE": "1"}, "k_fwd_mma"),
+    "wide_plain": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
+                   {"MDP_WIDE": "1", "MDP_WIDE_MMA": "0"}, "k_fwd_wide"),
 }
 
 

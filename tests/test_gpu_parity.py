@@ -144,20 +144,23 @@ def test_q5_impossible_transition(tmp_path):
 # ---------------------------------------------------------------------------
 # fuzzing: random problems covering every forward-kernel variant
 # ---------------------------------------------------------------------------
-@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic", "wide", "wide-chunked"])
+@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic", "wide", "wide-chunked", "wide-plain"])
 def engine_path(request, monkeypatch):
     """Every engine path: the direct one (the hipRTC-specialised forward
     kernel; on these small grids it computes its column's Q itself), the same
     with Q rows from k_qrows (MDP_FUSED=0), the direct path with the
     transition cache and XCD ordering off (MDP_JIT_SLOTS=0, MDP_JIT_XCD=0), and
     the generic kernels (MDP_JIT=0), and the wide path that years with more
-    than 16 states need (MDP_WIDE=1; chunked: one c value per launch)."""
-    for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB"):
+    than 16 states need (MDP_WIDE=1: its forward on the matrix cores,
+    k_fwd_mma; chunked: one c value per item launch; plain: k_fwd_wide)."""
+    for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB", "MDP_WIDE_MMA"):
         monkeypatch.delenv(k, raising=False)
     if request.param.startswith("wide"):
         monkeypatch.setenv("MDP_WIDE", "1")
         if request.param == "wide-chunked":
             monkeypatch.setenv("MDP_WIDE_CB", "1")
+        if request.param == "wide-plain":
+            monkeypatch.setenv("MDP_WIDE_MMA", "0")
     elif request.param == "generic":
         monkeypatch.setenv("MDP_JIT", "0")
     elif request.param == "direct-qrows":
@@ -239,22 +242,28 @@ def _wide_obs(rng, n, T, missing):
 def _wide_engine_run(model, e, c, path, monkeypatch):
     """Run on the named path and check it ran: "default" (years of 17-64
     states: the specialised kernel with its states in LDS; more: the wide
-    kernels) or "wide" (MDP_WIDE=1: k_witems + k_wq + k_fwd_wide)."""
+    kernels), "wide" (MDP_WIDE=1: k_witems + k_wq + the matrix-core forward
+    k_fwd_mma) or "wide-plain" (the same with k_fwd_wide, MDP_WIDE_MMA=0)."""
     monkeypatch.delenv("MDP_WIDE", raising=False)
-    if path == "wide":
+    monkeypatch.delenv("MDP_WIDE_MMA", raising=False)
+    if path.startswith("wide"):
         monkeypatch.setenv("MDP_WIDE", "1")
+    if path == "wide-plain":
+        monkeypatch.setenv("MDP_WIDE_MMA", "0")
     with mdp.Engine(model) as eng:
         got = eng.loglik_grid(e, c)
         launched, info = eng.launched(), eng.info()
-    if path == "wide" or model.npstates.max() > 64:
-        assert info["variant"] >= 20000 and "k_fwd_wide" in launched, launched
+    if path.startswith("wide") or model.npstates.max() > 64:
+        mma = path != "wide-plain" and model.npstates.max() <= 128
+        want = f"k_fwd_mma<{64 if model.npstates.max() <= 64 else 128}>" if mma else "k_fwd_wide"
+        assert info["variant"] >= 20000 and want in launched, launched
     else:
         assert 10000 <= info["variant"] < 20000, info
         assert any(k.startswith("mdp_fwd_jit<reading") for k in launched), launched
     return got
 
 
-@pytest.mark.parametrize("path", ["default", "wide"])
+@pytest.mark.parametrize("path", ["default", "wide", "wide-plain"])
 @pytest.mark.parametrize("missing", [{0: 5}, {3: 5}, {2: 6}, {4: 6}, {0: 8}, {3: 8}, {1: 5, 2: 6}, {0: 6, 4: 7}])
 def test_wide_years_vs_oracle(missing, path, monkeypatch):
     """Years with more than 4 missing patches (> 16 states), in year 0, in
@@ -288,7 +297,7 @@ def test_random_wide_problems(seed, monkeypatch):
     e, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.2])))
     c, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.5])))
     ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c, threads=16)
-    for path, cb in (("default", None), ("wide", None), ("wide", "1")):
+    for path, cb in (("default", None), ("wide", None), ("wide-plain", None), ("wide", "1")):
         if cb:
             monkeypatch.setenv("MDP_WIDE_CB", cb)
         got = _wide_engine_run(model, e, c, path, monkeypatch)
@@ -327,7 +336,7 @@ def test_wide_path_matches_direct_path(golden, monkeypatch, fname, s):
     with mdp.Engine(model) as eng:
         assert eng.info()["variant"] >= 20000
         b = eng.loglik_grid(g, g)
-        assert set(eng.kernel_ms()) <= {"k_zrows", "k_witems+k_wq", "k_fwd_wide"}
+        assert set(eng.kernel_ms()) <= {"k_zrows", "k_witems+k_wq", "k_fwd_wide", "k_fwd_mma"}
     assert_loglik_close(b, a, atol=1e-11)
 
 
