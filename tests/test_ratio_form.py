@@ -143,3 +143,45 @@ def test_ratio_forms_flush(golden):
         Q = _q_table(model, c)
         ref, got = _forward(model, Q, e, False), _forward(model, Q, e, True)
         assert abs(got - ref) <= 1e-11 * abs(ref), (e, c, got, ref)
+
+
+def _forward_gemm(model, Q, es):
+    """The matrix-core wide kernel's formulation (k_fwd_mma):
+    per year one product n = W C over K = every source's (k, m <= |A_k|), with
+    W[p][(k, m)] = v[p][k] x_p^(|A_k| - m) y_p^m and C[(k, m)][l] = Q_kl[m]
+    (zero past the transition's nX), for a batch of points at once."""
+    n, nvar, off, yid, ss, M, varc, prior = _problem(model)
+    pcnt = lambda v: bin(v).count("1")
+    x = np.minimum(np.asarray(es, float), 1.0)
+    y = 1.0 - x
+    V = np.ones((len(es), int(off[1])))
+    for t in range(1, len(off) - 1):
+        prev, cur = yid[off[t - 1]:off[t]], yid[off[t]:off[t + 1]]
+        Ks = [(k, pcnt(int(ss[ak])), m) for k, ak in enumerate(prev) for m in range(pcnt(int(ss[ak])) + 1)]
+        W = np.stack([V[:, k] * x ** (a - m) * y ** m for k, a, m in Ks], axis=1)
+        C = np.zeros((len(Ks), len(cur)))
+        for i, (k, a, m) in enumerate(Ks):
+            A = int(ss[prev[k]])
+            for l, bl in enumerate(cur):
+                q = Q[(A & int(ss[bl]), int(ss[bl]))]
+                if m < len(q):
+                    C[i, l] = q[m]
+        V = W @ C
+    L = V.sum(axis=1) * prior
+    with np.errstate(divide="ignore"):
+        return np.log(L)
+
+
+@pytest.mark.parametrize("fname", ["manual_p3_obs.txt", "occupancies.txt", "config2_64x50.txt"])
+def test_gemm_form_matches_direct(golden, fname):
+    model = mdp.Model.load(golden / fname, m=400, d=100)
+    es = [0.0, 0.2, 0.5, 0.8, 1.0, 1.3]
+    for c in (0.1, 0.52):
+        Q = _q_table(model, c)
+        got = _forward_gemm(model, Q, es)
+        for e, g in zip(es, got):
+            ref = _forward(model, Q, e, False)
+            if np.isfinite(ref):
+                assert abs(g - ref) <= 1e-11 * max(1.0, abs(ref)), (e, c, g, ref)
+            else:
+                assert not np.isfinite(g), (e, c, g, ref)
