@@ -1130,24 +1130,39 @@ __global__ __launch_bounds__(kBlock) void k_wq(uint32_t c0, uint32_t nitems, con
 // over K = every source's (k, m <= |A_k|) -- one GEMM per year of M = the
 // points, N = the new states, K = sum_k (|A_k| + 1), on the matrix cores with
 // the states of the block's points in LDS.  C's fragments are gathered from
-// the column's Q row through a host index table (gidx, c-independent: the
-// Q-row slot of each (K, l), or none); W's are formed from the states and
-// per-point power tables in LDS.  The products sum in another order than
-// k_fwd_wide's (positive terms: ~1e-15 relative).
+// the column's Q row: a lane's K entry (k, |A_k|, m; staged in LDS two years
+// ahead) names the transition descriptor (k, l) (host table, c-independent:
+// the Q-row offset of the transition's coefficients and its nX), and m <= nX
+// picks the slot.  W's are formed from the states and per-point power tables
+// in LDS.
+// 16 waves, one work item each per year: (column tile, pair of row tiles,
+// slice of the year's K chunks) -- with 16 / (2 ncol) slices in years of 16,
+// 32 or 64 states, so that every wave is busy; later slices leave their
+// partial products in the state buffer's rows past the year's column tiles
+// and the first adds them in slice order.  A wave's gathers run one chunk of
+// kMmaU steps ahead (descriptors two), and its first chunks of year t + 1 are
+// issued before year t's closing barriers.  The products sum in another
+// order than k_fwd_wide's (positive terms: ~1e-15 relative).
 constexpr uint32_t kMmaPts = 64;        // points per workgroup (4 row tiles of 16)
-constexpr uint32_t kMmaThreads = 256;   // 4 waves
-constexpr uint32_t kMmaNone = 0xffffffffu;
+constexpr uint32_t kMmaThreads = 1024;  // 16 waves
+constexpr uint32_t kMmaU = 4;           // K steps (of 4) per pipeline chunk: years padded to 16 entries
+constexpr uint32_t kMmaNone = 0x80000000u;  // descriptor of a padded column (l >= the year's states)
+constexpr uint32_t kMmaRows = 128;      // state buffer rows (also the K slices' partial sums)
+constexpr uint32_t kMmaPS = 80;         // power-table row stride: rows r, r + 1 on different bank halves
+constexpr uint32_t kMmaKtRegs = 4;      // K entries per thread staged per year (<= 4096)
 typedef double mdp_d4 __attribute__((ext_vector_type(4)));
 template <int NPM>  // states per year, padded to 16 (64 or 128)
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint32_t *__restrict__ kt,
-    const uint32_t *__restrict__ kbase, const uint32_t *__restrict__ gidx, const uint32_t *__restrict__ gbase,
+    const uint32_t *__restrict__ kbase, const uint32_t *__restrict__ desc, const uint32_t *__restrict__ dbase,
     uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne, uint32_t c0, uint32_t maxA,
-    double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
+    uint32_t ktmax, double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
 {
+    static_assert(NPM <= (int)kMmaRows, "state rows");
     extern __shared__ __attribute__((aligned(16))) double mlds[];
-    double *Va = mlds, *Vb = mlds + (size_t)NPM * kMmaPts;           // [state][point]
-    double *xp = Vb + (size_t)NPM * kMmaPts, *yp = xp + (size_t)(maxA + 1) * kMmaPts;  // [r][point]
+    double *Va = mlds, *Vb = mlds + (size_t)kMmaRows * kMmaPts;      // [state][point]
+    double *xp = Vb + (size_t)kMmaRows * kMmaPts, *yp = xp + (size_t)(maxA + 1) * kMmaPS;  // [r][point]
+    uint32_t *Kl = (uint32_t *)(yp + (size_t)(maxA + 1) * kMmaPS);  // [3][ktmax]: year t's K entries at t % 3
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t p0 = blockIdx.x * kMmaPts, ic = c0 + blockIdx.y;
     if (threadIdx.x < kMmaPts) {
@@ -1156,67 +1171,156 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         const double x = e > 1.0 ? 1.0 : e, y = 1.0 - x;
         double a = 1.0, b = 1.0;
         for (uint32_t r = 0; r <= maxA; ++r) {
-            xp[r * kMmaPts + threadIdx.x] = a;
-            yp[r * kMmaPts + threadIdx.x] = b;
+            xp[r * kMmaPS + threadIdx.x] = a;
+            yp[r * kMmaPS + threadIdx.x] = b;
             a *= x;
             b *= y;
         }
     }
     const uint32_t np0 = np[0];
     for (uint32_t i = threadIdx.x; i < (uint32_t)NPM * kMmaPts; i += kMmaThreads) Va[i] = i / kMmaPts < np0 ? 1.0 : 0.0;
+    for (uint32_t t = 1; t < 3 && t < tmax; ++t)
+        for (uint32_t i = threadIdx.x; i < kbase[t + 1] - kbase[t]; i += kMmaThreads) Kl[(t % 3) * ktmax + i] = kt[kbase[t] + i];
     __syncthreads();
     const double *q = Q + (size_t)ic * ldQ;
     const uint32_t kk = lane >> 4, col = lane & 15u;
+    // this wave's work item of year t
+    struct Item {
+        uint32_t npc, npcp, nch, nit, S, item, ks, cb, ce, lc, r0;
+        bool active;
+        const uint32_t *kl, *dt;
+    };
+    auto plan = [&](uint32_t t) {
+        Item it;
+        it.npc = np[t];
+        const uint32_t ncol = (it.npc + 15) / 16;
+        it.npcp = ncol * 16;
+        it.nch = (kbase[t + 1] - kbase[t]) / (4 * kMmaU);
+        it.nit = 2 * ncol;
+        it.S = 16 % it.nit == 0 ? 16 / it.nit : 1;  // S > 1: every wave has the year's one item
+        it.active = wv < it.nit * it.S;
+        it.item = wv % it.nit;
+        it.ks = wv / it.nit;
+        it.cb = it.nch * it.ks / it.S;
+        it.ce = it.nch * (it.ks + 1) / it.S;
+        it.lc = (it.item >> 1) * 16 + col;
+        it.r0 = (it.item & 1u) * 2;
+        it.kl = Kl + (t % 3) * ktmax;
+        it.dt = desc + dbase[t];  // [k][npcp]
+        return it;
+    };
+    auto kent = [&](const Item &it, uint32_t ch, uint32_t u) {
+        return it.kl[((ch < it.nch ? ch : it.nch - 1) * kMmaU + u) * 4 + kk];
+    };
+    auto dsc = [&](const Item &it, uint32_t en) { return it.dt[(en & 0xffu) * it.npcp + it.lc]; };
+    auto cval = [&](uint32_t en, uint32_t d) {
+        const uint32_t m = (en >> 16) & 0xffu;
+        const bool ok = (en >> 31) != 0u && (d >> 31) == 0u && m <= ((d >> kOffBits) & 31u);
+        const double v = q[ok ? (d & kOffMask) + m : 0u];
+        return ok ? v : 0.0;
+    };
+    // K entries of chunks ch, ch + 1, ch + 2; descriptors of ch + 1, ch + 2;
+    // C values of ch, ch + 1
+    uint32_t e0[kMmaU], e1[kMmaU], e2[kMmaU], d1[kMmaU], d2[kMmaU];
+    double b0[kMmaU], b1[kMmaU];
+    auto prime = [&](const Item &it) {
+#pragma unroll
+        for (uint32_t u = 0; u < kMmaU; ++u) {
+            e0[u] = kent(it, it.cb, u);
+            e1[u] = kent(it, it.cb + 1, u);
+            b0[u] = cval(e0[u], dsc(it, e0[u]));
+            d1[u] = dsc(it, e1[u]);
+        }
+    };
+    Item cur = plan(tmax > 1 ? 1u : 0u);
+    if (tmax > 1 && cur.active) prime(cur);
     for (uint32_t t = 1; t < tmax; ++t) {
-        const uint32_t npc = np[t], ncol = (npc + 15) / 16;
-        const uint32_t k0 = kbase[t], nstep = (kbase[t + 1] - k0) / 4, npcp = ncol * 16;
-        const uint32_t *gt = gidx + gbase[t];
-        // this wave's column tiles: wv, wv + 4 (NPM / 16 <= 8)
-        for (uint32_t ct = wv; ct < ncol; ct += kMmaThreads / 64) {
-            mdp_d4 acc[kMmaPts / 16];
+        // year t + 2's K entries: loaded now, stored before the year's barrier
+        uint32_t nk[kMmaKtRegs];
+        const uint32_t kn0 = t + 2 < tmax ? kbase[t + 2] : 0u, kn = t + 2 < tmax ? kbase[t + 3] - kn0 : 0u;
 #pragma unroll
-            for (uint32_t rt = 0; rt < kMmaPts / 16; ++rt) acc[rt] = mdp_d4{0.0, 0.0, 0.0, 0.0};
-            const uint32_t lc = ct * 16 + col;
-            // software pipeline: the (k, a, m) entry and the C index two steps
-            // ahead, the C value one step ahead (steps past the end reload
-            // the last one: valid addresses, never used)
-            auto ent = [&](uint32_t st) { return kt[k0 + (st < nstep ? st : nstep - 1) * 4 + kk]; };
-            auto gix = [&](uint32_t st) { return gt[((st < nstep ? st : nstep - 1) * 4 + kk) * npcp + lc]; };
-            auto cval = [&](uint32_t g) {
-                const double v = q[g == kMmaNone ? 0u : g];
-                return g == kMmaNone ? 0.0 : v;
-            };
-            uint32_t e_cur = ent(0), e_nxt = ent(1), g_nxt = gix(1);
-            double b_cur = cval(gix(0));
-            for (uint32_t st = 0; st < nstep; ++st) {
-                const uint32_t e_n2 = ent(st + 2), g_n2 = gix(st + 2);
-                const double b_nxt = cval(g_nxt);
-                // W for the four row tiles: the source's state times its weight
-                const uint32_t k = e_cur & 0xffu, a = (e_cur >> 8) & 0xffu, m = (e_cur >> 16) & 0xffu;
-                const bool ok = (e_cur >> 31) != 0u;
+        for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
+            const uint32_t i = threadIdx.x + r * kMmaThreads;
+            nk[r] = i < kn ? kt[kn0 + i] : 0u;
+        }
+        mdp_d4 acc[2];
+        acc[0] = mdp_d4{0.0, 0.0, 0.0, 0.0};
+        acc[1] = acc[0];
+        if (cur.active) {
+            for (uint32_t ch = cur.cb; ch < cur.ce; ++ch) {
 #pragma unroll
-                for (uint32_t rt = 0; rt < kMmaPts / 16; ++rt) {
-                    const uint32_t pp = rt * 16 + col;
-                    const double w = xp[(ok ? a - m : 0u) * kMmaPts + pp] * yp[(ok ? m : 0u) * kMmaPts + pp];
-                    const double av = ok ? Va[k * kMmaPts + pp] * w : 0.0;
-                    acc[rt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b_cur, acc[rt], 0, 0, 0);
+                for (uint32_t u = 0; u < kMmaU; ++u) {
+                    e2[u] = kent(cur, ch + 2, u);
+                    d2[u] = dsc(cur, e2[u]);
                 }
-                e_cur = e_nxt;
-                e_nxt = e_n2;
-                b_cur = b_nxt;
-                g_nxt = g_n2;
+#pragma unroll
+                for (uint32_t u = 0; u < kMmaU; ++u) b1[u] = cval(e1[u], d1[u]);
+#pragma unroll
+                for (uint32_t u = 0; u < kMmaU; ++u) {
+                    // W for the wave's two row tiles: the source's state times its weight
+                    const uint32_t en = e0[u];
+                    const uint32_t k = en & 0xffu, a = (en >> 8) & 0xffu, m = (en >> 16) & 0xffu;
+                    const bool ok = (en >> 31) != 0u;
+#pragma unroll
+                    for (uint32_t h = 0; h < 2; ++h) {
+                        const uint32_t pp = (cur.r0 + h) * 16 + col;
+                        const double wt = xp[(ok ? a - m : 0u) * kMmaPS + pp] * yp[(ok ? m : 0u) * kMmaPS + pp];
+                        const double av = ok ? Va[k * kMmaPts + pp] * wt : 0.0;
+                        acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0[u], acc[h], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kMmaU; ++u) {
+                    e0[u] = e1[u];
+                    e1[u] = e2[u];
+                    b0[u] = b1[u];
+                    d1[u] = d2[u];
+                }
             }
-            // n[p][l]: lane holds column l = ct*16 + col, rows kk + 4 r of each tile
-            if (lc < npc)
+        }
+        // next year's first chunks in flight across this year's barriers
+        // (its K entries were staged a year ago)
+        const Item nxt = plan(t + 1 < tmax ? t + 1 : t);
+        if (t + 1 < tmax && nxt.active) prime(nxt);
+        // n[p][l]: lane holds column l = lc, rows kk + 4 r of each tile; slice
+        // j > 0's partials: (S - 1) x 2 ncol x 512 doubles past row npcp, at
+        // most the (kMmaRows - npcp) x kMmaPts the buffer has
+        auto part = [&](uint32_t j) {
+            return Vb + (size_t)cur.npcp * kMmaPts + (size_t)((j - 1) * cur.nit + cur.item) * 512 + lane;
+        };
+        if (cur.active && cur.ks > 0) {
+            double *pk = part(cur.ks);
 #pragma unroll
-                for (uint32_t rt = 0; rt < kMmaPts / 16; ++rt)
+            for (uint32_t h = 0; h < 2; ++h)
 #pragma unroll
-                    for (uint32_t r = 0; r < 4; ++r) Vb[lc * kMmaPts + rt * 16 + kk + 4 * r] = acc[rt][r];
+                for (uint32_t r = 0; r < 4; ++r) pk[(h * 4 + r) * 64] = acc[h][r];
+        }
+        if (cur.S > 1) __syncthreads();
+        if (cur.active && cur.ks == 0) {
+            for (uint32_t j = 1; j < cur.S; ++j) {
+                const double *pj = part(j);
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h)
+#pragma unroll
+                    for (uint32_t r = 0; r < 4; ++r) acc[h][r] = acc[h][r] + pj[(h * 4 + r) * 64];
+            }
+            if (cur.lc < cur.npc)
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h)
+#pragma unroll
+                    for (uint32_t r = 0; r < 4; ++r) Vb[cur.lc * kMmaPts + (cur.r0 + h) * 16 + kk + 4 * r] = acc[h][r];
+        }
+        uint32_t *kw = Kl + ((t + 2) % 3) * ktmax;
+#pragma unroll
+        for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
+            const uint32_t i = threadIdx.x + r * kMmaThreads;
+            if (i < kn) kw[i] = nk[r];
         }
         __syncthreads();
         double *tv = Va;
         Va = Vb;
         Vb = tv;
+        cur = nxt;
     }
     if (threadIdx.x < kMmaPts) {
         const uint32_t ie = p0 + threadIdx.x, npl = np[tmax - 1];
@@ -1395,7 +1499,7 @@ struct DevCtx {
     double *Pg = nullptr, *V = nullptr;
     size_t cap_pg = 0, cap_v = 0;
     uint32_t *np_d = nullptr, *udesc_w = nullptr;
-    uint32_t *mma_kt = nullptr, *mma_kbase = nullptr, *mma_gidx = nullptr, *mma_gbase = nullptr;
+    uint32_t *mma_kt = nullptr, *mma_kbase = nullptr, *mma_desc = nullptr, *mma_dbase = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     std::vector<uint8_t> ev_mask;  // per profiled run: slots whose kernel was launched
@@ -1518,7 +1622,8 @@ struct mdp_engine {
     // and the Q-row slot of each (K entry, new state l) from gbase[t]
     bool mma = false;
     uint32_t mma_npm = 0;
-    std::vector<uint32_t> mma_kt, mma_kbase, mma_gidx, mma_gbase;
+    std::vector<uint32_t> mma_kt, mma_kbase, mma_desc, mma_dbase;
+    uint32_t mma_ktmax = 16;
     uint32_t qslot_lglmax = 0;      // log2 of the widest lane segment
     std::vector<uint8_t> isvar;
     std::vector<double> Sj;  // [nj][n] colonisation sums of every column for each needed j
@@ -1850,6 +1955,14 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
 // plus the FP64 work per grid point of k_fwd_wide (every use a (nX+1)-term
 // dot product with a weight multiply per term, one FMA into the state
 // vector; the per-lane power tables; the final prior sum).
+// k_fwd_mma: two state buffers and the power tables of kMmaPts points, three
+// years' K entries
+size_t mma_lds(const mdp_engine *eng)
+{
+    return (2 * (size_t)kMmaRows * kMmaPts + 2 * ((size_t)eng->maxA + 1) * kMmaPS) * sizeof(double) +
+           3 * (size_t)eng->mma_ktmax * sizeof(uint32_t);
+}
+
 int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
 {
     int rc = build_direct_plan(eng, p);
@@ -1859,55 +1972,53 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
     for (uint32_t d : eng->udesc_d) f += 3.0 * (((d >> kOffBits) & 31u) + 1.0) + 2.0;
     eng->wide_flops_pt = f;
     // k_fwd_mma's tables (c-independent): years of at most 128 states, at
-    // most 24 occupied patches a state (its per-point power tables)
+    // most 24 occupied patches a state (its per-point power tables); per
+    // year its K entries (k, |A_k|, m), padded to whole pipeline chunks, and
+    // the transition descriptors [k][l] (Q-row offset | nX << kOffBits)
     eng->mma = false;
     if (eng->npmax <= 128 && eng->maxA <= 24) {
         const char *mv = eng->opts.get("MDP_WIDE_MMA");
         if (!mv || atoi(mv) != 0) {
-            eng->mma = true;
             eng->mma_npm = eng->npmax <= 64 ? 64u : 128u;
             eng->mma_kt.clear();
-            eng->mma_gidx.clear();
+            eng->mma_desc.clear();
             eng->mma_kbase.assign(eng->tmax + 1, 0u);
-            eng->mma_gbase.assign(eng->tmax + 1, 0u);
+            eng->mma_dbase.assign(eng->tmax + 1, 0u);
+            eng->mma_ktmax = 16;
             size_t ub = 0;
             for (uint32_t t = 1; t < eng->tmax; ++t) {
                 const uint32_t npp = eng->np[t - 1], npc = eng->np[t], npcp = (npc + 15) / 16 * 16;
                 eng->mma_kbase[t] = (uint32_t)eng->mma_kt.size();
-                eng->mma_gbase[t] = (uint32_t)eng->mma_gidx.size();
+                eng->mma_dbase[t] = (uint32_t)eng->mma_desc.size();
                 for (uint32_t k = 0; k < npp; ++k) {
                     const uint32_t a = eng->udesc_d[ub + k] >> 27;  // |A_k| (any use from k; l = 0)
                     for (uint32_t m = 0; m <= a; ++m) eng->mma_kt.push_back(k | (a << 8) | (m << 16) | (1u << 31));
                 }
-                while (eng->mma_kt.size() % 4) eng->mma_kt.push_back(0u);
-                for (size_t i = eng->mma_kbase[t]; i < eng->mma_kt.size(); ++i) {
-                    const uint32_t en = eng->mma_kt[i], k = en & 0xffu, m = (en >> 16) & 0xffu;
+                while (eng->mma_kt.size() % (4 * kMmaU)) eng->mma_kt.push_back(0u);
+                eng->mma_ktmax = std::max<uint32_t>(eng->mma_ktmax, (uint32_t)eng->mma_kt.size() - eng->mma_kbase[t]);
+                for (uint32_t k = 0; k < npp; ++k)
                     for (uint32_t l = 0; l < npcp; ++l) {
-                        uint32_t g = kMmaNone;
-                        if ((en >> 31) && l < npc) {
+                        uint32_t dv = kMmaNone;
+                        if (l < npc) {
                             const uint32_t dsc = eng->udesc_d[ub + (size_t)l * npp + k];
-                            const uint32_t off = dsc & kOffMask, nX = (dsc >> kOffBits) & 31u;
-                            if (m <= nX) g = off + m;
+                            dv = (dsc & kOffMask) | (((dsc >> kOffBits) & 31u) << kOffBits);
                         }
-                        eng->mma_gidx.push_back(g);
+                        eng->mma_desc.push_back(dv);
                     }
-                }
                 ub += (size_t)npp * npc;
             }
             eng->mma_kbase[eng->tmax] = (uint32_t)eng->mma_kt.size();
-            eng->mma_gbase[eng->tmax] = (uint32_t)eng->mma_gidx.size();
+            eng->mma_dbase[eng->tmax] = (uint32_t)eng->mma_desc.size();
             if (eng->mma_kt.empty()) eng->mma_kt.push_back(0u);
-            if (eng->mma_gidx.empty()) eng->mma_gidx.push_back(kMmaNone);
+            if (eng->mma_desc.empty()) eng->mma_desc.push_back(kMmaNone);
+            // the next year's K entries are staged through kMmaKtRegs registers
+            // a thread, and everything must fit the LDS
+            eng->mma = eng->mma_ktmax <= kMmaKtRegs * kMmaThreads && mma_lds(eng) <= 160 * 1024;
         }
     }
     return MDP_OK;
 }
 
-// k_fwd_mma: two state buffers and the power tables of kMmaPts points
-size_t mma_lds(const mdp_engine *eng)
-{
-    return (2 * (size_t)eng->mma_npm + 2 * ((size_t)eng->maxA + 1)) * kMmaPts * sizeof(double);
-}
 
 constexpr size_t kQrowsLdsMax = 160 * 1024;
 constexpr size_t kFusedLdsMax = 64 * 1024;  // fused forward kernel: every table of one column
@@ -2322,7 +2433,7 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
             if ((rc = dev_upload(&d.np_d, eng->np)) || (rc = dev_upload(&d.udesc_w, eng->udesc_d))) return rc;
             if (eng->mma &&
                 ((rc = dev_upload(&d.mma_kt, eng->mma_kt)) || (rc = dev_upload(&d.mma_kbase, eng->mma_kbase)) ||
-                 (rc = dev_upload(&d.mma_gidx, eng->mma_gidx)) || (rc = dev_upload(&d.mma_gbase, eng->mma_gbase))))
+                 (rc = dev_upload(&d.mma_desc, eng->mma_desc)) || (rc = dev_upload(&d.mma_dbase, eng->mma_dbase))))
                 return rc;
             if (eng->mma)
                 HIP_TRY(hipFuncSetAttribute(eng->mma_npm == 64 ? (const void *)k_fwd_mma<64> : (const void *)k_fwd_mma<128>,
@@ -2362,7 +2473,7 @@ void free_device(DevCtx &d)
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
                     d.zs, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
                     d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot,
-                    d.mma_kt, d.mma_kbase, d.mma_gidx, d.mma_gbase,
+                    d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -2672,8 +2783,8 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
             note_launch(eng, "k_fwd_mma<%u>", eng->mma_npm);
 #define MDP_MMA(NPM) \
     hipLaunchKernelGGL((k_fwd_mma<NPM>), g, dim3(kMmaThreads), mma_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.np_d, \
-                       d.mma_kt, d.mma_kbase, d.mma_gidx, d.mma_gbase, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, \
-                       out, se, sc)
+                       d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, \
+                       eng->mma_ktmax, out, se, sc)
             if (eng->mma_npm == 64) MDP_MMA(64);
             else MDP_MMA(128);
 #undef MDP_MMA
