@@ -1153,17 +1153,17 @@ constexpr uint32_t kMmaKtRegs = 4;      // K entries per thread staged per year 
 typedef double mdp_d4 __attribute__((ext_vector_type(4)));
 template <int NPM>  // states per year, padded to 16 (64 or 128)
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
-    const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint32_t *__restrict__ kt,
+    const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint2 *__restrict__ kt,
     const uint32_t *__restrict__ kbase, const uint32_t *__restrict__ desc, const uint32_t *__restrict__ dbase,
     uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne, uint32_t c0, uint32_t maxA,
-    uint32_t ktmax, double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
+    uint32_t ktmax, uint32_t zslot, double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
 {
     static_assert(NPM <= (int)kMmaRows, "state rows");
     extern __shared__ __attribute__((aligned(16))) double mlds[];
     double *Va = mlds, *Vb = mlds + (size_t)kMmaRows * kMmaPts;      // [state][point]
     double *xp = Vb + (size_t)kMmaRows * kMmaPts, *yp = xp + (size_t)(maxA + 1) * kMmaPS;  // [r][point]
-    uint32_t *Kl = (uint32_t *)(yp + (size_t)(maxA + 1) * kMmaPS);  // [3][ktmax]: year t's K entries at t % 3
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint2 *Kl = (uint2 *)(yp + (size_t)(maxA + 1) * kMmaPS);  // [3][ktmax]: year t's K entries at t % 3
+    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const uint32_t p0 = blockIdx.x * kMmaPts, ic = c0 + blockIdx.y;
     if (threadIdx.x < kMmaPts) {
         const uint32_t ie = p0 + threadIdx.x;
@@ -1188,7 +1188,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     struct Item {
         uint32_t npc, npcp, nch, nit, S, item, ks, cb, ce, lc, r0;
         bool active;
-        const uint32_t *kl, *dt;
+        const uint2 *kl;
+        const uint32_t *dt;
     };
     auto plan = [&](uint32_t t) {
         Item it;
@@ -1206,78 +1207,79 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         it.lc = (it.item >> 1) * 16 + col;
         it.r0 = (it.item & 1u) * 2;
         it.kl = Kl + (t % 3) * ktmax;
-        it.dt = desc + dbase[t];  // [k][npcp]
+        it.dt = desc + __builtin_amdgcn_readfirstlane(dbase[t]);  // [k][npcp]
         return it;
     };
     auto kent = [&](const Item &it, uint32_t ch, uint32_t u) {
         return it.kl[((ch < it.nch ? ch : it.nch - 1) * kMmaU + u) * 4 + kk];
     };
-    auto dsc = [&](const Item &it, uint32_t en) { return it.dt[(en & 0xffu) * it.npcp + it.lc]; };
-    auto cval = [&](uint32_t en, uint32_t d) {
-        const uint32_t m = (en >> 16) & 0xffu;
-        const bool ok = (en >> 31) != 0u && (d >> 31) == 0u && m <= ((d >> kOffBits) & 31u);
-        const double v = q[ok ? (d & kOffMask) + m : 0u];
-        return ok ? v : 0.0;
+    // (32-bit byte offsets from uniform bases: the loads take the scalar-base
+    // form, with no 64-bit address arithmetic per lane)
+    auto dsc = [&](const Item &it, uint2 en) {
+        return *(const uint32_t *)((const char *)it.dt + ((((en.y >> 24) & 0x7fu) * it.npcp + it.lc) << 2));
     };
-    // K entries of chunks ch, ch + 1, ch + 2; descriptors of ch + 1, ch + 2;
-    // C values of ch, ch + 1
-    uint32_t e0[kMmaU], e1[kMmaU], e2[kMmaU], d1[kMmaU], d2[kMmaU];
-    double b0[kMmaU], b1[kMmaU];
-    auto prime = [&](const Item &it) {
+    // C[(k, m)][l]: the slot of Q_kl[m], or the Q row's zero slot (ldQ > ncoef)
+    auto cval = [&](uint2 en, uint32_t d) {
+        const uint32_t m = (en.y >> 16) & 0xffu;
+        const bool ok = (en.y >> 31) != 0u && (d >> 31) == 0u && m <= ((d >> kOffBits) & 31u);
+        return *(const double *)((const char *)q + ((ok ? (d & kOffMask) + m : zslot) << 3));
+    };
+    // ring slots by chunk parity (relative to the item's first chunk): the
+    // descriptors of chunks ch + 1 and ch + 2, the C values of ch and ch + 1;
+    // the loop body runs twice per pass with the slots fixed, so nothing moves
+    uint32_t dd[2][kMmaU];
+    double bb[2][kMmaU];
+    auto issue_d = [&](const Item &it, uint32_t ch, uint32_t sl) {
 #pragma unroll
-        for (uint32_t u = 0; u < kMmaU; ++u) {
-            e0[u] = kent(it, it.cb, u);
-            e1[u] = kent(it, it.cb + 1, u);
-            b0[u] = cval(e0[u], dsc(it, e0[u]));
-            d1[u] = dsc(it, e1[u]);
-        }
+        for (uint32_t u = 0; u < kMmaU; ++u) dd[sl][u] = dsc(it, kent(it, ch, u));
+    };
+    auto issue_b = [&](const Item &it, uint32_t ch, uint32_t sl) {
+#pragma unroll
+        for (uint32_t u = 0; u < kMmaU; ++u) bb[sl][u] = cval(kent(it, ch, u), dd[sl][u]);
+    };
+    auto prime = [&](const Item &it) {
+        issue_d(it, it.cb, 0);
+        issue_d(it, it.cb + 1, 1);
+        issue_b(it, it.cb, 0);
     };
     Item cur = plan(tmax > 1 ? 1u : 0u);
     if (tmax > 1 && cur.active) prime(cur);
     for (uint32_t t = 1; t < tmax; ++t) {
         // year t + 2's K entries: loaded now, stored before the year's barrier
-        uint32_t nk[kMmaKtRegs];
+        uint2 nk[kMmaKtRegs];
         const uint32_t kn0 = t + 2 < tmax ? kbase[t + 2] : 0u, kn = t + 2 < tmax ? kbase[t + 3] - kn0 : 0u;
 #pragma unroll
         for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
             const uint32_t i = threadIdx.x + r * kMmaThreads;
-            nk[r] = i < kn ? kt[kn0 + i] : 0u;
+            nk[r] = i < kn ? kt[kn0 + i] : make_uint2(0u, 0u);
         }
         mdp_d4 acc[2];
         acc[0] = mdp_d4{0.0, 0.0, 0.0, 0.0};
         acc[1] = acc[0];
-        if (cur.active) {
-            for (uint32_t ch = cur.cb; ch < cur.ce; ++ch) {
+        // one chunk: the descriptors of ch + 2, the C values of ch + 1, then
+        // ch's products (W formed unconditionally: padded entries name row 0
+        // and meet C = 0)
+        auto chunk = [&](uint32_t ch, uint32_t sl) {
+            issue_d(cur, ch + 2, sl);
+            issue_b(cur, ch + 1, sl ^ 1u);
 #pragma unroll
-                for (uint32_t u = 0; u < kMmaU; ++u) {
-                    e2[u] = kent(cur, ch + 2, u);
-                    d2[u] = dsc(cur, e2[u]);
-                }
+            for (uint32_t u = 0; u < kMmaU; ++u) {
+                const uint2 en = kent(cur, ch, u);
 #pragma unroll
-                for (uint32_t u = 0; u < kMmaU; ++u) b1[u] = cval(e1[u], d1[u]);
-#pragma unroll
-                for (uint32_t u = 0; u < kMmaU; ++u) {
-                    // W for the wave's two row tiles: the source's state times its weight
-                    const uint32_t en = e0[u];
-                    const uint32_t k = en & 0xffu, a = (en >> 8) & 0xffu, m = (en >> 16) & 0xffu;
-                    const bool ok = (en >> 31) != 0u;
-#pragma unroll
-                    for (uint32_t h = 0; h < 2; ++h) {
-                        const uint32_t pp = (cur.r0 + h) * 16 + col;
-                        const double wt = xp[(ok ? a - m : 0u) * kMmaPS + pp] * yp[(ok ? m : 0u) * kMmaPS + pp];
-                        const double av = ok ? Va[k * kMmaPts + pp] * wt : 0.0;
-                        acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0[u], acc[h], 0, 0, 0);
-                    }
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < kMmaU; ++u) {
-                    e0[u] = e1[u];
-                    e1[u] = e2[u];
-                    b0[u] = b1[u];
-                    d1[u] = d2[u];
+                for (uint32_t h = 0; h < 2; ++h) {
+                    const uint32_t pb = ((cur.r0 + h) * 16 + col) * 8u;
+                    const double wt = *(const double *)((const char *)xp + (en.x >> 16) + pb) *
+                                      *(const double *)((const char *)yp + (en.y & 0xffffu) + pb);
+                    const double av = *(const double *)((const char *)Va + (en.x & 0xffffu) + pb) * wt;
+                    acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bb[sl][u], acc[h], 0, 0, 0);
                 }
             }
-        }
+        };
+        if (cur.active)
+            for (uint32_t ch = cur.cb; ch < cur.ce; ch += 2) {
+                chunk(ch, 0);
+                if (ch + 1 < cur.ce) chunk(ch + 1, 1);
+            }
         // next year's first chunks in flight across this year's barriers
         // (its K entries were staged a year ago)
         const Item nxt = plan(t + 1 < tmax ? t + 1 : t);
@@ -1310,7 +1312,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
 #pragma unroll
                     for (uint32_t r = 0; r < 4; ++r) Vb[cur.lc * kMmaPts + (cur.r0 + h) * 16 + kk + 4 * r] = acc[h][r];
         }
-        uint32_t *kw = Kl + ((t + 2) % 3) * ktmax;
+        uint2 *kw = Kl + ((t + 2) % 3) * ktmax;
 #pragma unroll
         for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
             const uint32_t i = threadIdx.x + r * kMmaThreads;
@@ -1499,7 +1501,8 @@ struct DevCtx {
     double *Pg = nullptr, *V = nullptr;
     size_t cap_pg = 0, cap_v = 0;
     uint32_t *np_d = nullptr, *udesc_w = nullptr;
-    uint32_t *mma_kt = nullptr, *mma_kbase = nullptr, *mma_desc = nullptr, *mma_dbase = nullptr;
+    uint2 *mma_kt = nullptr;
+    uint32_t *mma_kbase = nullptr, *mma_desc = nullptr, *mma_dbase = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     std::vector<uint8_t> ev_mask;  // per profiled run: slots whose kernel was launched
@@ -1622,7 +1625,8 @@ struct mdp_engine {
     // and the Q-row slot of each (K entry, new state l) from gbase[t]
     bool mma = false;
     uint32_t mma_npm = 0;
-    std::vector<uint32_t> mma_kt, mma_kbase, mma_desc, mma_dbase;
+    std::vector<uint2> mma_kt;  // per year its K entries: LDS byte offsets of the W rows, m, k
+    std::vector<uint32_t> mma_kbase, mma_desc, mma_dbase;
     uint32_t mma_ktmax = 16;
     uint32_t qslot_lglmax = 0;      // log2 of the widest lane segment
     std::vector<uint8_t> isvar;
@@ -1960,14 +1964,16 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
 size_t mma_lds(const mdp_engine *eng)
 {
     return (2 * (size_t)kMmaRows * kMmaPts + 2 * ((size_t)eng->maxA + 1) * kMmaPS) * sizeof(double) +
-           3 * (size_t)eng->mma_ktmax * sizeof(uint32_t);
+           3 * (size_t)eng->mma_ktmax * sizeof(uint2);
 }
 
 int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
 {
     int rc = build_direct_plan(eng, p);
     if (rc) return rc;
-    eng->ldQ = ((size_t)eng->ncoef_d + 1) & ~(size_t)1;
+    // Q rows with at least one zero slot past the coefficients (slot ncoef:
+    // k_fwd_mma's gathers of absent coefficients read it)
+    eng->ldQ = ((size_t)eng->ncoef_d + 2) & ~(size_t)1;
     double f = 2.0 * (eng->maxA + 1) + 2.0 * eng->np[eng->tmax - 1];
     for (uint32_t d : eng->udesc_d) f += 3.0 * (((d >> kOffBits) & 31u) + 1.0) + 2.0;
     eng->wide_flops_pt = f;
@@ -1992,9 +1998,11 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
                 eng->mma_dbase[t] = (uint32_t)eng->mma_desc.size();
                 for (uint32_t k = 0; k < npp; ++k) {
                     const uint32_t a = eng->udesc_d[ub + k] >> 27;  // |A_k| (any use from k; l = 0)
-                    for (uint32_t m = 0; m <= a; ++m) eng->mma_kt.push_back(k | (a << 8) | (m << 16) | (1u << 31));
+                    for (uint32_t m = 0; m <= a; ++m)  // Va row k, xp row a - m, yp row m (bytes); m; k; valid
+                        eng->mma_kt.push_back(make_uint2((k * kMmaPts * 8u) | (((a - m) * kMmaPS * 8u) << 16),
+                                                         (m * kMmaPS * 8u) | (m << 16) | (k << 24) | (1u << 31)));
                 }
-                while (eng->mma_kt.size() % (4 * kMmaU)) eng->mma_kt.push_back(0u);
+                while (eng->mma_kt.size() % (4 * kMmaU)) eng->mma_kt.push_back(make_uint2(0u, 0u));
                 eng->mma_ktmax = std::max<uint32_t>(eng->mma_ktmax, (uint32_t)eng->mma_kt.size() - eng->mma_kbase[t]);
                 for (uint32_t k = 0; k < npp; ++k)
                     for (uint32_t l = 0; l < npcp; ++l) {
@@ -2009,7 +2017,7 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
             }
             eng->mma_kbase[eng->tmax] = (uint32_t)eng->mma_kt.size();
             eng->mma_dbase[eng->tmax] = (uint32_t)eng->mma_desc.size();
-            if (eng->mma_kt.empty()) eng->mma_kt.push_back(0u);
+            if (eng->mma_kt.empty()) eng->mma_kt.push_back(make_uint2(0u, 0u));
             if (eng->mma_desc.empty()) eng->mma_desc.push_back(kMmaNone);
             // the next year's K entries are staged through kMmaKtRegs registers
             // a thread, and everything must fit the LDS
@@ -2784,7 +2792,7 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
 #define MDP_MMA(NPM) \
     hipLaunchKernelGGL((k_fwd_mma<NPM>), g, dim3(kMmaThreads), mma_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.np_d, \
                        d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, \
-                       eng->mma_ktmax, out, se, sc)
+                       eng->mma_ktmax, eng->ncoef_d, out, se, sc)
             if (eng->mma_npm == 64) MDP_MMA(64);
             else MDP_MMA(128);
 #undef MDP_MMA
