@@ -140,16 +140,23 @@ def _oracle_leg(om, g_e, g_c, lik_gpu, ltot_gpu, tmax, threads, budget_s, per_pt
 
 def cli_walls(cfg_inputs, tmpdir):
     """End-to-end wall time of the drop-in CLI (parse -> hipRTC -> grid -> Ltot
-    -> write; main_MIDASPOM.c:330,437-439 time the same span) with a cold
-    (fresh) and a warm hipRTC code-object cache, and of the oracle's own CLI
+    -> write; main_MIDASPOM.c:330,437-439 time the same span) with cold
+    (fresh) caches, on the first run with caches on, and warm (steady state),
+    and of the oracle's own CLI
     (the reference formulation, naive dgemm, 1 core) on config 1."""
     from midaspom_amd import _lib
     out = {}
     cache = Path(tempfile.mkdtemp(prefix="mdp_jitcache_", dir=tmpdir))
     for name, (inp, s) in cfg_inputs.items():
-        for leg in ("cold", "warm"):
+        for leg in ("cold", "warm_first", "warm"):
             # cold: an empty code-object cache and no compiler-side cache
-            # (ROCm's comgr keeps its own, which this process has warmed)
+            # (ROCm's comgr keeps its own, which this process has warmed).
+            # warm_first: the first run with both caches on.  Besides our
+            # code object, the HIP runtime's own first kernel launch goes
+            # through comgr, 0.15 s with its cache cold even for a one-kernel
+            # program (scripts/ubench/tiny_launch, scripts/jitcache_probe.py),
+            # and comgr's cache keeps that across processes: warm is the
+            # steady state after it
             env = dict(os.environ, MDP_JIT_CACHE=str(cache / name), MIDASPOM_TIMING="1",
                        **({"AMD_COMGR_CACHE": "0"} if leg == "cold" else {}))
             t0 = time.perf_counter()

@@ -3057,6 +3057,12 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
 {
     if (!p || !out || n_devices < 0) return mdp_set_error(MDP_EINVAL, "null argument");
     *out = nullptr;
+    // MDP_SETUP_TIMING=1: the set-up's split on stderr (planning, hipRTC /
+    // code-object cache, device set-up)
+    const bool st_on = getenv("MDP_SETUP_TIMING") && atoi(getenv("MDP_SETUP_TIMING")) != 0;
+    auto st_now = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double st0 = st_now();
+    double st_jit0 = st0, st_jit1 = st0;
     EngineOpts opts;
     if (int orc = parse_engine_opts(options, opts)) return orc;
     if (p->n == 0 || p->tmax == 0 || !p->M || !p->year_off || !p->year_ids || !p->prior ||
@@ -3252,7 +3258,10 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
             const bool fused_first = eng->fused_mode == 1 ||
                                      (eng->fused_mode == -1 && !vlds && !eng->qglobal &&
                                       fused_lds(eng, plan.ct_max) <= kFusedLdsMax);
-            if ((chunked ? jit_build_chunks(eng) : jit_build(eng, fused_first)) == MDP_OK) eng->jit = true;
+            st_jit0 = st_now();
+            const int jrc = chunked ? jit_build_chunks(eng) : jit_build(eng, fused_first);
+            st_jit1 = st_now();
+            if (jrc == MDP_OK) eng->jit = true;
             else fprintf(stderr, "midaspom: hipRTC specialisation failed, using the %s kernels:\n%s\n",
                          vlds ? "wide" : "generic", eng->jit_log.c_str());
         }
@@ -3288,6 +3297,7 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
             return mdp_set_error(MDP_ENODEV, "device %d not present (%d visible)", id, ndev);
         }
     eng->devs.resize(ids.size());
+    const double st_dev0 = st_now();
     for (size_t i = 0; i < ids.size(); ++i) {
         eng->devs[i].device = ids[i];
         rc = init_device(eng, eng->devs[i], p);
@@ -3296,6 +3306,9 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
             return rc;
         }
     }
+    if (st_on)
+        fprintf(stderr, "mdp setup (s): plan %.3f jit %.3f plan2 %.3f devices %.3f\n", st_jit0 - st0, st_jit1 - st_jit0,
+                st_dev0 - st_jit1, st_now() - st_dev0);
     *out = eng;
     return MDP_OK;
 }

@@ -40,5 +40,5 @@ timeout -k 10 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VAL
 python3 $R/scripts/pmc_valu.py $O/pmc/c5p1 1000000 50 $O/pmc_valu_cfg5.json || exit 1
 # long series (chunked) against the generic kernels, and the wide-year paths
 (cd $R && timeout -k 10 300 python scripts/sweep_forward.py --configs 6 --steps 20 --variants "MDP_JIT=1;MDP_JIT=1;MDP_JIT=0" > $O/sweep_cfg6.jsonl 2> $O/sweep_cfg6.err) || { echo "sweep cfg6 failed"; exit 1; }
-(cd $R && WIDE_PATHS=default,wide timeout -k 10 300 python scripts/wide_timing.py > $O/wide_timing.jsonl 2> $O/wide_timing.err) || { echo "wide timing failed"; exit 1; }
+(cd $R && WIDE_PATHS=default,wide WIDE60_PATHS=default,wideplain timeout -k 10 300 python scripts/wide_timing.py > $O/wide_timing.jsonl 2> $O/wide_timing.err) || { echo "wide timing failed"; exit 1; }
 echo "all ok"
