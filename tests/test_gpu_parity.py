@@ -325,6 +325,27 @@ def test_wide_survey_series_sampled(tmp_path, path, monkeypatch):
     assert_loglik_close(got[ie, ic], ref)
 
 
+@pytest.mark.parametrize("path", ["default", "wide-plain"])
+def test_wide_survey_series_128_states(tmp_path, path, monkeypatch):
+    """The 60 %-unvisited survey series of scripts/wide_timing.py (up to 128
+    states a year, 66 416 uses per point): k_fwd_mma<128> by default, and
+    k_fwd_wide, on a 130 x 70 grid (three 64-point blocks, the last partial),
+    sampled against the oracle."""
+    cfg = dict(synth.CONFIG2, pmiss=0.6, seed=5, T=50)
+    f = synth.write(tmp_path / "wide60.txt", **cfg)
+    model = mdp.Model.load(f)
+    assert model.npstates.max() == 128
+    e, _ = mdp.grid(130)
+    c, _ = mdp.grid(70)
+    got = _wide_engine_run(model, e, c, path, monkeypatch)
+    rng = np.random.default_rng(4)
+    ie, ic = rng.integers(0, 130, 24), rng.integers(0, 70, 24)
+    ie[:4], ic[:4] = [0, 129, 0, 129], [0, 0, 69, 69]
+    ref = oracle.OracleModel.load(f).loglik_points(e[ie], c[ic], threads=16)
+    assert np.isfinite(ref).sum() >= 16
+    assert_loglik_close(got[ie, ic], ref)
+
+
 @pytest.mark.parametrize("fname,s", [("config2_64x50.txt", 64), ("occupancies.txt", 33)])
 def test_wide_path_matches_direct_path(golden, monkeypatch, fname, s):
     """Forced onto the wide path, a problem the register kernels also run
