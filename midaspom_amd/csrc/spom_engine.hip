@@ -1145,7 +1145,7 @@ __global__ __launch_bounds__(kBlock) void k_wq(uint32_t c0, uint32_t nitems, con
 // order than k_fwd_wide's (positive terms: ~1e-15 relative).
 constexpr uint32_t kMmaPts = 64;        // points per workgroup (4 row tiles of 16)
 constexpr uint32_t kMmaThreads = 1024;  // 16 waves
-constexpr uint32_t kMmaU = 4;           // K steps (of 4) per pipeline chunk: years padded to 16 entries
+constexpr uint32_t kMmaU = 2;           // K steps (of 4) per pipeline chunk: years padded to 8 entries
 constexpr uint32_t kMmaNone = 0x80000000u;  // descriptor of a padded column (l >= the year's states)
 constexpr uint32_t kMmaRows = 128;      // state buffer rows (also the K slices' partial sums)
 constexpr uint32_t kMmaPS = 80;         // power-table row stride: rows r, r + 1 on different bank halves
