@@ -1198,7 +1198,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         it.npcp = ncol * 16;
         it.nch = (kbase[t + 1] - kbase[t]) / (4 * kMmaU);
         it.nit = 2 * ncol;
-        it.S = 16 % it.nit == 0 ? 16 / it.nit : 1;  // S > 1: every wave has the year's one item
+        // slices of at least two chunks; a wave has at most one item a year
+        it.S = 16 % it.nit == 0 ? min(16 / it.nit, max(1u, it.nch / 2)) : 1;
         it.active = wv < it.nit * it.S;
         it.item = wv % it.nit;
         it.ks = wv / it.nit;
