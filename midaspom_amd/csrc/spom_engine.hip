@@ -1149,6 +1149,7 @@ constexpr uint32_t kMmaU = 2;           // K steps (of 4) per pipeline chunk: ye
 constexpr uint32_t kMmaNone = 0x80000000u;  // descriptor of a padded column (l >= the year's states)
 constexpr uint32_t kMmaRows = 128;      // state buffer rows (also the K slices' partial sums)
 constexpr uint32_t kMmaPS = 80;         // power-table row stride: rows r, r + 1 on different bank halves
+constexpr uint32_t kMmaRT = 4;         // row tiles a wave takes (2 or 4)
 constexpr uint32_t kMmaKtRegs = 4;      // K entries per thread staged per year (<= 4096)
 typedef double mdp_d4 __attribute__((ext_vector_type(4)));
 template <int NPM>  // states per year, padded to 16 (64 or 128)
@@ -1197,16 +1198,16 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         const uint32_t ncol = (it.npc + 15) / 16;
         it.npcp = ncol * 16;
         it.nch = (kbase[t + 1] - kbase[t]) / (4 * kMmaU);
-        it.nit = 2 * ncol;
+        it.nit = ncol * (4 / kMmaRT);
         // slices of at least two chunks; a wave has at most one item a year
-        it.S = 16 % it.nit == 0 ? min(16 / it.nit, max(1u, it.nch / 2)) : 1;
+        it.S = 16 % it.nit == 0 ? min(min(16 / it.nit, 8 / ncol), max(1u, it.nch / 2)) : 1;
         it.active = wv < it.nit * it.S;
         it.item = wv % it.nit;
         it.ks = wv / it.nit;
         it.cb = it.nch * it.ks / it.S;
         it.ce = it.nch * (it.ks + 1) / it.S;
-        it.lc = (it.item >> 1) * 16 + col;
-        it.r0 = (it.item & 1u) * 2;
+        it.lc = (it.item / (4 / kMmaRT)) * 16 + col;
+        it.r0 = (it.item % (4 / kMmaRT)) * kMmaRT;
         it.kl = Kl + (t % 3) * ktmax;
         it.dt = desc + __builtin_amdgcn_readfirstlane(dbase[t]);  // [k][npcp]
         return it;
@@ -1254,9 +1255,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
             const uint32_t i = threadIdx.x + r * kMmaThreads;
             nk[r] = i < kn ? kt[kn0 + i] : make_uint2(0u, 0u);
         }
-        mdp_d4 acc[2];
-        acc[0] = mdp_d4{0.0, 0.0, 0.0, 0.0};
-        acc[1] = acc[0];
+        mdp_d4 acc[kMmaRT];
+#pragma unroll
+        for (uint32_t h = 0; h < kMmaRT; ++h) acc[h] = mdp_d4{0.0, 0.0, 0.0, 0.0};
         // one chunk: the descriptors of ch + 2, the C values of ch + 1, then
         // ch's products (W formed unconditionally: padded entries name row 0
         // and meet C = 0)
@@ -1267,7 +1268,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
             for (uint32_t u = 0; u < kMmaU; ++u) {
                 const uint2 en = kent(cur, ch, u);
 #pragma unroll
-                for (uint32_t h = 0; h < 2; ++h) {
+                for (uint32_t h = 0; h < kMmaRT; ++h) {
                     const uint32_t pb = ((cur.r0 + h) * 16 + col) * 8u;
                     const double wt = *(const double *)((const char *)xp + (en.x >> 16) + pb) *
                                       *(const double *)((const char *)yp + (en.y & 0xffffu) + pb);
@@ -1289,12 +1290,12 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         // j > 0's partials: (S - 1) x 2 ncol x 512 doubles past row npcp, at
         // most the (kMmaRows - npcp) x kMmaPts the buffer has
         auto part = [&](uint32_t j) {
-            return Vb + (size_t)cur.npcp * kMmaPts + (size_t)((j - 1) * cur.nit + cur.item) * 512 + lane;
+            return Vb + (size_t)cur.npcp * kMmaPts + (size_t)((j - 1) * cur.nit + cur.item) * (kMmaRT * 256) + lane;
         };
         if (cur.active && cur.ks > 0) {
             double *pk = part(cur.ks);
 #pragma unroll
-            for (uint32_t h = 0; h < 2; ++h)
+            for (uint32_t h = 0; h < kMmaRT; ++h)
 #pragma unroll
                 for (uint32_t r = 0; r < 4; ++r) pk[(h * 4 + r) * 64] = acc[h][r];
         }
@@ -1303,13 +1304,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
             for (uint32_t j = 1; j < cur.S; ++j) {
                 const double *pj = part(j);
 #pragma unroll
-                for (uint32_t h = 0; h < 2; ++h)
+                for (uint32_t h = 0; h < kMmaRT; ++h)
 #pragma unroll
                     for (uint32_t r = 0; r < 4; ++r) acc[h][r] = acc[h][r] + pj[(h * 4 + r) * 64];
             }
             if (cur.lc < cur.npc)
 #pragma unroll
-                for (uint32_t h = 0; h < 2; ++h)
+                for (uint32_t h = 0; h < kMmaRT; ++h)
 #pragma unroll
                     for (uint32_t r = 0; r < 4; ++r) Vb[cur.lc * kMmaPts + (cur.r0 + h) * 16 + kk + 4 * r] = acc[h][r];
         }
