@@ -16,7 +16,7 @@ ranks on fewer GPUs (collectives through host memory).
 
 Workload: 64 patches x 50 years (synthetic,
 Appendix C generator, md5-checked), 512 x 512 grid, -m 400 -d 100, FP64.
-Launch:  python bench.py [--gpus N --steps K --warmup W]
+Launch:  python bench.py [--gpus N --steps K --warmup W]   (N > 1: starts N ranks itself)
          torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -516,23 +516,91 @@ def strong_scaling(model, s, tmax, rank, world, dev, args):
             "steps_what": f"{args.steps} passes + one gather (the gather amortised)"}
 
 
+def resolve_world(args, env=None):
+    """(world, rank, local, spawn): the job's shape from the launcher's
+    environment (torchrun: WORLD_SIZE / RANK / LOCAL_RANK) or, when no
+    launcher set it, from --gpus (spawn = True: this process starts --gpus
+    ranks itself).  A launcher world that contradicts an explicit --gpus is
+    an error: the line would name one GPU count and time another."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher's WORLD_SIZE is {world}")
+        return world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0")), False
+    world = args.gpus if args.gpus is not None else 1
+    if world < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    return world, 0, 0, world > 1
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _spawned_rank(local, argv, world, port):
+    """Entry of a rank started by bench.py itself (--gpus N, no launcher): the
+    launcher's environment, then the ordinary path.  Started with the spawn
+    method, so it is a fresh interpreter: the parent never touched the GPU."""
+    os.environ.update({"WORLD_SIZE": str(world), "RANK": str(local), "LOCAL_RANK": str(local),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.argv = [sys.argv[0]] + list(argv)
+    main()
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the multi-rank plumbing without a GPU (CPU tests): the
+    process group over gloo, each rank's e-row slabs of the weak (N s x s)
+    and strong (s x s, configs 2 and 3) grids, gathered to rank 0."""
+    from midaspom_amd import dist as mdist
+    if world > 1:
+        dist.init_process_group("gloo")
+    s = CONFIGS[args.config]["s"]
+    mine = {"rank": rank, "weak_rows": [rank * s, (rank + 1) * s],
+            "strong_rows": {str(c): list(mdist.row_slab(rank, world, CONFIGS[c]["s"])) for c in (2, 3)}}
+    allr = [None] * world
+    if world > 1:
+        dist.all_gather_object(allr, mine)
+        dist.destroy_process_group()
+    else:
+        allr = [mine]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": allr}))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node; under a launcher it must equal WORLD_SIZE, without one "
+                         "bench.py starts that many ranks itself (default 1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [4, 5])
     ap.add_argument("--grid4", type=int, default=256, help="config 4 grid points per axis")
     ap.add_argument("--replicates", type=int, default=1_000_000, help="config 5 ensemble size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the fixed-grid (strong) blocks")
     ap.add_argument("--layout", default="ce", choices=["ce", "ec"],
                     help="device layout of log L: ce = [c][e] (coalesced stores, default), ec = [e][c] rows")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--dry-run", action="store_true", help="multi-rank plumbing only, no GPU (tests)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local, spawn = resolve_world(args)
+    if spawn:
+        # no launcher: start the ranks here, before this process makes any
+        # GPU call (they are fresh interpreters; this one only waits)
+        import torch.multiprocessing as tmp
+        argv = [a for a in sys.argv[1:]]
+        tmp.start_processes(_spawned_rank, args=(argv, world, _free_port()), nprocs=world, join=True,
+                            start_method="spawn")
+        return
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
     # the drop-in CLI's end-to-end walls (cpu_baseline.end_to_end) are taken
     # first, while this process holds no GPU context: a user's CLI run does
     # not share the device with a live bench process either (round 3 took
@@ -567,7 +635,8 @@ def main():
     tmax = model.tmax
 
     # weak scaling: rank r owns e-rows [r*s, (r+1)*s) of an (world*s) x s grid
-    # (N > 1 lines also carry "strong": the fixed s x s grid split over N)
+    # (N > 1 lines also carry "strong": the fixed s x s grids of configs 2
+    # and 3 split over the N ranks)
     g_all, _ = mdp.grid(world * s, 0.0, 1.0)
     g_e = g_all[rank * s:(rank + 1) * s].copy()
     g_c, win = mdp.grid(s, 0.0, 1.0)
@@ -611,7 +680,16 @@ def main():
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     job_ms = time_job(step, gather, dev, world)
-    strong = strong_scaling(model, s, tmax, rank, world, dev, args) if world > 1 else None
+    strong = None
+    if world > 1 and not args.no_strong:
+        strong = {}
+        for sc in (2, 3):
+            if sc == args.config:
+                m_sc = model
+            else:
+                m_sc = mdp.Model.load(synth.write(tmpdir / f"strong_cfg{sc}.txt", **CONFIGS[sc]["gen"]),
+                                      m=400.0, p=0.5, d=100.0)
+            strong[f"config{sc}"] = strong_scaling(m_sc, CONFIGS[sc]["s"], m_sc.tmax, rank, world, dev, args)
     # Kernel durations, measured live with HIP events on the stream the path
     # runs on (torch's current stream):
     # each kernel of the path launched K times back to back between two
@@ -639,13 +717,17 @@ def main():
     info = eng.info()
     fwd_ms = kms.get("k_forward", float("nan"))
     fused = "k_qrows" not in kms  # the fused forward kernel does the per-c work too
-    # numerator: the algorithmic minimum (mdp_engine_work_fact flop_min): each
-    # distinct transition's dot product once per point, every use's state
-    # update, the weight table, the prior sum (+ the per-c tables when the
-    # fused kernel forms them); a transition that recurs is algorithmic
-    # reuse, not work (the every-use count is reported beside it)
-    per_pt_min = fact["weight_pt"] + fact["use_pt_min"] + fact["final_pt"]
-    flop_fwd = fact["flop_min"] if fused else s * s * per_pt_min
+    # numerator: the algorithmic minimum of the ratio forms the kernels
+    # evaluate (mdp_engine_work_fact flop_min, ABI 8): each distinct Q
+    # group's Horner chain once per point, g^d once per distinct (group, d)
+    # on s-form points, every year's state update, the pre-scales, flushes,
+    # set-up and prior sum (+ the per-c tables when the fused kernel forms
+    # them); a transition that recurs is algorithmic reuse, not work.  The
+    # round-4 direct-form counts (with the weight table the ratio forms no
+    # longer build) are reported beside it as legacy figures.
+    flop_fwd = fact["flop_min"] if fused else s * s * fact["pt_min"]
+    flop_direct = fact["flop_min_direct"] if fused else s * s * (fact["weight_pt"] + fact["use_pt_min"]
+                                                                  + fact["final_pt"])
     flop_every = fact["flop"] if fused else s * s * (fact["weight_pt"] + fact["use_pt"] + fact["final_pt"])
     achieved_tf = flop_fwd / (fwd_ms * 1e-3) / 1e12
     result = {
@@ -657,6 +739,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
+        # value: each rank its own s x s slab (per-GPU work fixed as N grows);
+        # N > 1 lines carry the fixed-grid figures of configs 2 and 3 in "strong"
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
@@ -688,12 +772,15 @@ def main():
             # closed-form factorised count from the plan's dimensions
             # (mdp_engine_work_fact): the kernel's share of it
             "flop_per_launch": flop_fwd,
-            "flop_basis": "closed-form factorised minimum, each distinct transition once per point, "
+            "flop_basis": "closed-form minimum of the ratio forms (each distinct Q group once per point), "
                           + ("per-c + per-point terms (fused kernel)" if fused
                              else "per-point terms (k_qrows does the per-c work)"),
+            "flop_per_launch_direct_form": flop_direct,
+            "frac_direct_form": flop_direct / (fwd_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
             "flop_per_launch_every_use": flop_every,
             "work_fact": fact,
-            "step_tflops_fact": fact["flop"] / (dt / args.steps) / 1e12,
+            # the whole step's minimum (per-c tables + per-point work) over the step time
+            "step_tflops_fact": fact["flop_min"] / (dt / args.steps) / 1e12,
             # the hipRTC generator's count of the code it emitted (transition caching included)
             "flop_per_launch_generated": work["flop_impl"],
             # SURVEY §8(d) F_alg (dense-in-j form): exceeds the FP64 peak as a

@@ -36,7 +36,7 @@ extern "C" {
 #define MDP_ENODEV (-5)       /* no usable GPU                             */
 #define MDP_EUNSUPPORTED (-6) /* problem outside the engine's limits       */
 
-#define MDP_ABI_VERSION 7
+#define MDP_ABI_VERSION 8
 
 /* ------------------------------------------------------------------ */
 /* Host model: parse + state enumeration (the reference's L2 layer)    */
@@ -198,22 +198,35 @@ int mdp_engine_work(const mdp_engine *engine, uint64_t ne, uint64_t nc, double *
  * always-zero column and 2*8 + 2 for the series over the small ones, for the
  * engine's current grid), var-column pressures
  * (1 per row and var column), item factors (1 - pC where B_b = 0, one
- * multiply per free column), Q sums (len - 1 adds per entry).  Per grid
- * point: the weight table (2 maxA powers + one product per W[|A|][m] entry
- * used), every forward use (2 nX + 3: the (nX+1)-term dot product and the
- * state multiply-add), the prior sum (2 np_last - 1).  use_pt counts a
- * transition that recurs at every use; use_pt_min is the algorithmic
- * minimum: each distinct transition's dot product once per point (2 nX + 1)
- * plus the state updates, npc (2 npp - 1) per year -- the hipRTC kernel caches recurring
- * transitions and executes between the two.  flop = nc * per-c + ne * nc *
- * per-point, flop_min the same with use_pt_min.  The per-c terms are zero on
+ * multiply per free column), Q sums (len - 1 adds per entry).
+ *
+ * Per grid point, the algorithmic minimum of the ratio forms the forward
+ * kernels evaluate (ABI 8): setup_pt -- y = 1 - x, the
+ * ratio's division, the power tables past their first powers (g's on s-form
+ * points only); use_pt_ratio -- every distinct Q group's Horner chain once
+ * (2 nX), g^d once per distinct (group, d > 0) on s-form points, each
+ * year's state update npc (2 npp - 1), the source pre-scales, the
+ * deferred-exponent flushes; final_pt_ratio -- the prior sum (np_last), the
+ * final B^E, log.  Those three are means over the engine's current e grid
+ * (its s-form share; one half before a grid is set); pt_min is their sum and
+ * flop_min = nc * per-c + ne * nc * pt_min.
+ *
+ * Legacy (rounds 1-4, the direct form P = sum_m Q[m] W[|A|][m] with a
+ * per-point weight table, which the ratio forms no longer build):
+ * weight_pt (2 maxA powers + one product per W entry used), use_pt (every
+ * use 2 nX + 3), use_pt_min (each distinct transition's dot product once,
+ * 2 nX + 1, plus the state updates), final_pt (2 np_last - 1); flop =
+ * nc * per-c + ne * nc * (weight_pt + use_pt + final_pt) and
+ * flop_min_direct the same with use_pt_min.  The per-c terms are zero on
  * the generic path (MDP_JIT=0), which has no direct plan. */
 typedef struct mdp_work {
     double z_c, pc_c, item_c, q_c;        /* per c value */
-    double weight_pt, use_pt, final_pt;   /* per grid point */
-    double flop;                          /* the grid's total */
-    double use_pt_min;                    /* per grid point, distinct transitions once */
-    double flop_min;                      /* the grid's total with use_pt_min */
+    double weight_pt, use_pt, final_pt;   /* per grid point (legacy direct form) */
+    double flop;                          /* the grid's total, every use (legacy) */
+    double use_pt_min;                    /* per grid point, distinct transitions once (legacy) */
+    double flop_min;                      /* the grid's algorithmic minimum (ratio forms, ABI 8) */
+    double setup_pt, use_pt_ratio, final_pt_ratio, pt_min;  /* per grid point, ratio forms (ABI 8) */
+    double flop_min_direct;               /* legacy: the direct form's minimum (flop_min before ABI 8) */
 } mdp_work;
 int mdp_engine_work_fact(const mdp_engine *engine, uint64_t ne, uint64_t nc, mdp_work *work);
 

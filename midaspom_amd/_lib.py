@@ -70,7 +70,7 @@ class Work(ctypes.Structure):
 
     _fields_ = [(f, ctypes.c_double) for f in
                 ("z_c", "pc_c", "item_c", "q_c", "weight_pt", "use_pt", "final_pt", "flop", "use_pt_min",
-                 "flop_min")]
+                 "flop_min", "setup_pt", "use_pt_ratio", "final_pt_ratio", "pt_min", "flop_min_direct")]
 
 
 class EngineInfo(ctypes.Structure):
@@ -203,18 +203,36 @@ ENGINE_OPTION_NAMES = (
     "MDP_JIT", "MDP_FUSED", "MDP_FUSED_COLS", "MDP_EPL", "MDP_JIT_SLOTS", "MDP_JIT_WINDOW", "MDP_JIT_XCD",
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
-    "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_FUSED_SBUILD", "MDP_JIT_SPLIT",
-    "MDP_JIT_EARLYW", "MDP_FUSED_BAL", "MDP_FUSED_QFLAT", "MDP_FUSED_PH2FLAT", "MDP_JIT_ROT", "MDP_FUSED_CMERGE", "MDP_FUSED_DIRECT", "MDP_WIDE_MMA",
+    "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_JIT_SPLIT", "MDP_JIT_ROT",
+    "MDP_WIDE_MMA",
     # measurement-only: accepted by the diag build alone
     "MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE")
 SCENARIO_OPTION_NAMES = ("MDP_SCN_BIG", "MDP_SCN_ROW")
 
 
+DIAG_OPTION_NAMES = ("MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE")
+
+
 def options_string(options=None, names=ENGINE_OPTION_NAMES) -> bytes | None:
     """The options argument of mdp_*_create_opts: a dict or "K=V;..." string
-    as given, or (None) the MDP_* variables of `names` set in the environment."""
+    as given, or (None) the MDP_* variables of `names` set in the environment.
+    Measurement-only names (DIAG_OPTION_NAMES) are forwarded from the
+    environment only to the diag library; with the default library they are
+    skipped with a warning -- the C CLIs ignore the environment altogether,
+    and a stale variable must not make every engine creation fail.  Passed
+    explicitly, the default library refuses them (MDP_EINVAL)."""
     if options is None:
-        options = {k: os.environ[k] for k in names if k in os.environ}
+        diag_lib = os.environ.get("MIDASPOM_DIAG_LIB") == "1"
+        options = {}
+        for k in names:
+            if k not in os.environ:
+                continue
+            if k in DIAG_OPTION_NAMES and not diag_lib:
+                import warnings
+                warnings.warn(f"{k} is measurement-only (libmidaspom_diag.so): ignored from the environment",
+                              RuntimeWarning, stacklevel=3)
+                continue
+            options[k] = os.environ[k]
     if isinstance(options, dict):
         options = ";".join(f"{k}={v}" for k, v in options.items())
     return options.encode() if options else None

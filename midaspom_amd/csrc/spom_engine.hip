@@ -1460,6 +1460,7 @@ struct DevCtx {
     double *e = nullptr, *c = nullptr;
     size_t cap_e = 0, cap_c = 0;
     uint32_t ne = 0, nc = 0;
+    uint32_t ne_sform = 0;  // e rows of this grid on the s-form (x < y), for the work count
     // forward kernels with several points per lane: list positions -> e rows
     // (bit 31: a duplicate that is computed, not stored), grouped by ratio form
     uint32_t *plist = nullptr;
@@ -1528,8 +1529,8 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT", "MDP_FUSED", "MDP_FUSED_COLS", "MDP_EPL", "MDP_JIT_SLOTS", "MDP_JIT_WINDOW", "MDP_JIT_XCD",
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
-    "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_FUSED_SBUILD", "MDP_JIT_SPLIT",
-    "MDP_JIT_EARLYW", "MDP_FUSED_BAL", "MDP_FUSED_QFLAT", "MDP_FUSED_PH2FLAT", "MDP_JIT_ROT", "MDP_FUSED_CMERGE", "MDP_FUSED_DIRECT", "MDP_WIDE_MMA"};
+    "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_JIT_SPLIT", "MDP_JIT_ROT",
+    "MDP_WIDE_MMA"};
 const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
@@ -1633,7 +1634,6 @@ struct mdp_engine {
     uint32_t qslot_lglmax = 0;      // log2 of the widest lane segment
     std::vector<uint8_t> isvar;
     std::vector<double> Sj;  // [nj][n] colonisation sums of every column for each needed j
-    std::vector<double> Mv;  // [nvar][n] dispersal rows of the var columns
     std::string jit_log;
     size_t coef_lds = 0;      // k_coefs dynamic LDS bytes
     double prior0 = 1.0;
@@ -1939,9 +1939,6 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
     eng->var_cols.assign(p->var_cols, p->var_cols + nvar);
     eng->isvar.assign(n, 0);
     for (uint32_t b = 0; b < nvar; ++b) eng->isvar[p->var_cols[b]] = 1;
-    eng->Mv.assign((size_t)nvar * n, 0.0);  // the var columns' dispersal rows (the fused kernel's S-build)
-    for (uint32_t b = 0; b < nvar; ++b)
-        for (uint32_t k = 0; k < n; ++k) eng->Mv[(size_t)b * n + k] = p->M[(size_t)p->var_cols[b] * n + k];
     eng->Sj.assign((size_t)eng->nj * n, 0.0);
     for (uint32_t js = 0; js < eng->nj; ++js) {
         const uint32_t j = eng->cj_bits[js];
@@ -2119,39 +2116,6 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     // the fused kernel's column tables: one contiguous image it copies to LDS
     // (with zpad, all KZ zs rows, zero past kmax: the kernel reads them unmasked)
     const MdpJitPlan &pl = eng->jit_plan;
-    if (pl.sbuild) {  // S-build layout: Mv, items, CSR, series, column lists, row states
-        const size_t ct = pl.ct_max;
-        std::vector<double> img(ct, 0.0);
-        memcpy(img.data() + pl.off_mv, eng->Mv.data(), eng->Mv.size() * sizeof(double));
-        uint2 *it = (uint2 *)(img.data() + pl.off_it);
-        for (uint32_t i = 0; i < eng->nitems; ++i) {
-            const uint32_t r = eng->itemRow[i];
-            it[i] = make_uint2(eng->itemB[i] | ((r & 0xffu) << 24), eng->cj_bits[r] | ((r >> 8) << 24));
-        }
-        memcpy(img.data() + pl.off_qs, eng->qstart.data(), eng->qstart.size() * sizeof(uint32_t));
-        memcpy(img.data() + pl.off_zc, zc.data(), (size_t)nj * kZTerms * sizeof(double));
-        if (!eng->qitem.empty())
-            memcpy(img.data() + pl.off_qi, eng->qitem.data(), eng->qitem.size() * sizeof(uint32_t));
-        const bool small_n = n < 255;
-        unsigned char *zl8 = (unsigned char *)(img.data() + pl.off_zl);
-        uint16_t *zl16 = (uint16_t *)(img.data() + pl.off_zl);
-        std::vector<double> large;
-        std::vector<uint32_t> cols;
-        for (uint32_t js = 0; js < nj; ++js) {
-            z_split(eng, js, cmax, large, nullptr, &cols);
-            for (uint32_t k = 0; k < pl.kzmax; ++k) {
-                const uint32_t col = k < cols.size() ? cols[k] : (small_n ? 0xffu : 0xffffu);
-                if (small_n) zl8[(size_t)k * nj + js] = (unsigned char)col;
-                else zl16[(size_t)k * nj + js] = (uint16_t)col;
-            }
-        }
-        uint32_t *rj = (uint32_t *)(img.data() + pl.off_rj);
-        for (uint32_t js = 0; js < nj; ++js) rj[js] = eng->cj_bits[js];
-        if ((rc = dev_reserve(&d.coltab, &d.cap_coltab, ct))) return rc;
-        HIP_TRY(hipMemcpy(d.coltab, img.data(), ct * sizeof(double), hipMemcpyHostToDevice));
-        d.ct_len = (uint32_t)ct;
-        return MDP_OK;
-    }
     const size_t kimg = pl.zpad ? std::max<size_t>(kmax, std::max<uint32_t>(8u, pl.kzmax)) : kmax;
     const size_t ct = ((size_t)pl.off_zs + kimg * nj + 127) & ~(size_t)127;
     std::vector<double> img(ct, 0.0);
@@ -2345,8 +2309,7 @@ int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 size_t fused_lds(const mdp_engine *eng, size_t ct_len)
 {
     const size_t fc = (size_t)eng->jit_plan.fused_cols;
-    const size_t sb = eng->jit_plan.sbuild ? (size_t)eng->jit_plan.kzmax * eng->nj + (size_t)eng->nj * eng->nvar + 1 : 0;
-    return (ct_len + 2 + sb + fc * (eng->nj + eng->nitems + 2 * eng->ldQ)) * sizeof(double);  // + staging scratch
+    return (ct_len + 2 + fc * (eng->nj + eng->nitems + 2 * eng->ldQ)) * sizeof(double);  // + staging scratch
 }
 
 constexpr size_t kWidePgBytes = 256ull << 20;  // wide path: item-factor chunk
@@ -2531,6 +2494,11 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     HIP_TRY(hipSetDevice(d.device));
     int rc;
     if ((rc = dev_reserve(&d.e, &d.cap_e, ne)) || (rc = dev_reserve(&d.c, &d.cap_c, nc))) return rc;
+    d.ne_sform = 0;
+    for (uint32_t i = 0; i < ne; ++i) {  // the kernels' form test: x = min(e, 1), s-form where x < 1 - x
+        const double x = e[i] > 1.0 ? 1.0 : e[i];
+        d.ne_sform += x < 1.0 - x;
+    }
     const bool qglobal = eng->wide || eng->qglobal;  // Q rows from k_zrows + k_witems + k_wq
     if (eng->wide || eng->jit) {
         double cmax = 0.0;
@@ -3191,30 +3159,9 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
             for (size_t q = 0; q + 1 < eng->qstart.size(); ++q)
                 plan.qmaxlen = std::max(plan.qmaxlen, eng->qstart[q + 1] - eng->qstart[q]);
             auto even = [](size_t v) { return (uint32_t)((v + 1) & ~(size_t)1); };
-            plan.n = eng->n;
-            plan.var_cols = eng->var_cols;
-            if (const char *sv = eng->opts.get("MDP_FUSED_SBUILD")) plan.sbuild = atoi(sv) != 0;
             if (const char *sv = eng->opts.get("MDP_JIT_SPLIT")) plan.split_forms = atoi(sv) != 0;
-            if (const char *sv = eng->opts.get("MDP_JIT_EARLYW")) plan.early_w = atoi(sv) != 0;
-            if (const char *sv = eng->opts.get("MDP_FUSED_BAL")) plan.bal = atoi(sv) != 0;
-            if (const char *sv = eng->opts.get("MDP_FUSED_QFLAT")) plan.qflat = atoi(sv) != 0;
-            if (const char *sv = eng->opts.get("MDP_FUSED_PH2FLAT")) plan.ph2flat = atoi(sv) != 0;
             if (const char *sv = eng->opts.get("MDP_JIT_ROT")) plan.rot = atoi(sv) != 0;
-            if (const char *sv = eng->opts.get("MDP_FUSED_CMERGE")) plan.cmerge = atoi(sv) != 0;
-            if (const char *sv = eng->opts.get("MDP_FUSED_DIRECT")) plan.direct = atoi(sv) != 0;
-            if (plan.sbuild) {  // var-column rows, items, CSR, series, column lists, row states
-                plan.off_mv = 0;
-                plan.off_it = even((size_t)eng->nvar * eng->n);
-                plan.off_qs = even(plan.off_it + eng->nitems);
-                plan.off_qi = even(plan.off_qs + (eng->ncoef_d + 2) / 2);
-                plan.off_zc = even(plan.off_qi + (eng->qitem.size() + 1) / 2);
-                plan.off_zl = even(plan.off_zc + (size_t)eng->nj * kZTerms);
-                const size_t zlb = (size_t)plan.kzmax * eng->nj * (eng->n < 255 ? 1 : 2);
-                plan.off_rj = even(plan.off_zl + (zlb + 7) / 8);
-                plan.off_zs = even(plan.off_rj + (eng->nj + 1) / 2);  // (the end)
-                plan.ct_max = (uint32_t)((plan.off_zs + 127) & ~(size_t)127);
-                plan.zpad = true;  // the in-kernel image always holds KZ rows (zero past a row's list)
-            } else {
+            {
                 plan.off_it = even((size_t)eng->nj * eng->nvar);
                 plan.off_qs = even(plan.off_it + eng->nitems);
                 plan.off_qi = even(plan.off_qs + (eng->ncoef_d + 2) / 2);
@@ -3678,7 +3625,24 @@ int mdp_engine_work_fact(const mdp_engine *eng, uint64_t ne, uint64_t nc, mdp_wo
     const double per_c = w->z_c + w->pc_c + w->item_c + w->q_c;
     const double per_pt = w->weight_pt + w->use_pt + w->final_pt;
     w->flop = (double)nc * per_c + (double)ne * (double)nc * per_pt;
-    w->flop_min = (double)nc * per_c + (double)ne * (double)nc * (w->weight_pt + w->use_pt_min + w->final_pt);
+    w->flop_min_direct = (double)nc * per_c + (double)ne * (double)nc * (w->weight_pt + w->use_pt_min + w->final_pt);
+    // the ratio forms (ABI 8): per form from the plan, then the mean over the
+    // current grid's e rows (half s-form before a grid is set)
+    MdpJitPlan pl;
+    pl.np = eng->np;
+    pl.udesc = ud;
+    const MdpRatioWork rw = mdp_jit_ratio_work(pl);
+    double ns = 0.0, nall = 0.0;
+    for (const DevCtx &d : eng->devs) {
+        ns += d.ne_sform;
+        nall += d.ne;
+    }
+    const double fs = nall > 0.0 ? ns / nall : 0.5;
+    w->setup_pt = fs * rw.setup_s + (1.0 - fs) * rw.setup_t;
+    w->use_pt_ratio = fs * rw.use_s + (1.0 - fs) * rw.use_t;
+    w->final_pt_ratio = rw.final_pt;
+    w->pt_min = w->setup_pt + w->use_pt_ratio + w->final_pt_ratio;
+    w->flop_min = (double)nc * per_c + (double)ne * (double)nc * w->pt_min;
     return MDP_OK;
 }
 

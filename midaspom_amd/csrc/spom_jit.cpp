@@ -11,7 +11,12 @@
 // year instead.  Code objects are cached in memory and on disk, keyed by the
 // FNV-1a hash of the generated source, the compile options and the hipRTC
 // version; a cached file that is not a gfx950 code object, or that the
-// runtime refuses to load (spom_engine.hip jit_load), is rebuilt.
+// runtime refuses to load (spom_engine.hip jit_load), is rebuilt.  hipRTC
+// itself (and the compiler library it brings in) is loaded with dlopen on
+// the first cache miss only: a run whose code objects are all cached never
+// maps it (the drop-in CLI's start-up, main_MIDASPOM.c:326-332).
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
 #include <hip/hiprtc.h>
 #include <unistd.h>
 
@@ -27,6 +32,7 @@
 #include <cstdint>
 #include <string>
 #include <sys/stat.h>
+#include <type_traits>
 #include <vector>
 
 #include "spom_jit.h"
@@ -87,14 +93,31 @@ uint64_t fnv1a(const std::string &s)
     return h;
 }
 
+// The disk cache: MDP_JIT_CACHE, else ~/.cache/midaspom_jit, else (no
+// HOME) a per-user /tmp/midaspom_jit-<uid>.  The directory is created 0700
+// and used only while it is owned by this user and writable by nobody else
+// (cache_dir_private): a code object found there is loaded into the GPU, so
+// a directory another user can write to is not a cache.
 std::string cache_dir()
 {
     if (const char *d = getenv("MDP_JIT_CACHE")) return d;
-    if (const char *h = getenv("HOME")) {
-        std::string p = std::string(h) + "/.cache/midaspom_jit";
-        return p;
-    }
-    return "/tmp/midaspom_jit";
+    if (const char *h = getenv("HOME")) return std::string(h) + "/.cache/midaspom_jit";
+    return "/tmp/midaspom_jit-" + std::to_string((long)geteuid());
+}
+
+bool cache_dir_private(const std::string &dir)
+{
+    struct stat st;
+    if (lstat(dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode)) return false;
+    return st.st_uid == geteuid() && (st.st_mode & (S_IWGRP | S_IWOTH)) == 0;
+}
+
+// create the cache directory (and its parent, e.g. ~/.cache) if missing
+void make_cache_dir(const std::string &dir)
+{
+    const size_t sl = dir.find_last_of('/');
+    if (sl != std::string::npos && sl > 0) mkdir(dir.substr(0, sl).c_str(), 0755);
+    mkdir(dir.c_str(), 0700);
 }
 
 bool read_file(const std::string &path, std::vector<char> &out)
@@ -116,10 +139,8 @@ bool read_file(const std::string &path, std::vector<char> &out)
 
 void write_file(const std::string &dir, const std::string &path, const std::vector<char> &data)
 {
-    mkdir(dir.c_str(), 0755);  // one level is enough for the default layouts
-    std::string parent = dir.substr(0, dir.find_last_of('/'));
-    mkdir(parent.c_str(), 0755);
-    mkdir(dir.c_str(), 0755);
+    make_cache_dir(dir);
+    if (!cache_dir_private(dir)) return;
     static std::atomic<unsigned> seq{0};  // threads of one process write distinct temporaries
     std::string tmp = path + ".tmp" + std::to_string((long)getpid()) + "." + std::to_string(seq++);
     FILE *f = fopen(tmp.c_str(), "wb");
@@ -233,53 +254,14 @@ std::string power_expr(const std::string &base, uint32_t E, const std::string &t
 
 // The fused kernel's Q-entry sum in the canonical order of spom_engine.hip
 // (kQGroup = 8: the items in groups of eight summed left to right, the group
-// sums as a pairwise tree padded to a power of two, i.e. a binary counter
-// folded from its lowest occupied level up), unrolled for entries of at most
-// qml items; items u < qun come from the preloaded indices qx[k][u], the
-// rest from the CSR in LDS.  Sets `a`.
-std::string qsum_code(uint32_t qml, uint32_t qun)
-{
-    const uint32_t G = 8, ngm = (qml + G - 1) / G;  // = kQGroup (spom_engine.hip)
-    uint32_t nlev = 1;
-    while ((1u << nlev) <= ngm) ++nlev;
-    std::ostringstream o;
-    auto item = [&](uint32_t u) {
-        return u < qun ? "pl[qx[k][" + std::to_string(u) + "]]" : "pl[Qil[qb[k] + " + std::to_string(u) + "]]";
-    };
-    o << "            const u32 cnt_ = qn[k];\n"
-         "            double a = 0.0, lev_[" << nlev << "];\n";
-    for (uint32_t g = 0; g < ngm; ++g) {
-        o << "            if (" << G * g << "u < cnt_) {\n"
-          << "                double s_ = " << item(G * g) << ";\n";
-        for (uint32_t u = 1; u < G && G * g + u < qml; ++u)
-            o << "                if (" << G * g + u << "u < cnt_) s_ = s_ + " << item(G * g + u) << ";\n";
-        for (uint32_t l = 0; l < nlev; ++l) {
-            if ((g >> l) & 1u) {
-                o << "                s_ = lev_[" << l << "] + s_;\n";
-            } else {
-                o << "                lev_[" << l << "] = s_;\n";
-                break;
-            }
-        }
-        o << "            }\n";
-    }
-    o << "            {\n"
-         "                const u32 ng_ = (cnt_ + " << G - 1 << "u) / " << G << "u;\n"
-         "                bool hv_ = false;\n";
-    for (uint32_t l = 0; l < nlev; ++l)
-        o << "                if ((ng_ >> " << l << ") & 1u) { a = hv_ ? lev_[" << l << "] + a : lev_[" << l
-          << "]; hv_ = true; }\n";
-    o << "            }\n";
-    return o.str();
-}
-
-// The same sum with every gather unconditional (qflat): slots past the
-// entry's count read the zero slot pl[NITEMS] (set in the Pc phase), so all
-// loads are in flight at once instead of one branch and wait per item.  The
-// groups and the tree then run over the compile-time bound (groups of zeros
-// past the entry); every padded addition is x + (+0.0) = x for the
-// non-negative (or NaN / inf) sums here, so the bits are those of
-// qsum_code's canonical order.  Sets `a`.
+// sums as a pairwise tree over the entry's groups: a binary counter folded
+// from its lowest occupied level up).  Every gather is unconditional: slots
+// past the entry's count read the zero slot pl[NITEMS] (set in the Pc
+// phase), so all loads are in flight at once instead of one branch and wait
+// per item.  The groups and the tree then run over the compile-time bound
+// (groups of zeros past the entry, a tree padded to a power of two); every
+// padded addition is x + (+0.0) = x for the non-negative (or NaN / inf) sums
+// here, so the bits are those of the canonical order.  Sets `a`.
 std::string qsum_flat_code(uint32_t qml, uint32_t qun)
 {
     const uint32_t G = 8, ngm = (qml + G - 1) / G;  // = kQGroup (spom_engine.hip)
@@ -312,166 +294,39 @@ std::string qsum_flat_code(uint32_t qml, uint32_t qun)
     return o.str();
 }
 
-// The fused prologue's phases with every column of the workgroup in one
-// lane (cmerge): a lane per item, per Q entry and per Z row computes the FC
-// columns' values, which sit interleaved in LDS (Zl[row][FC], Pl[item][FC],
-// the zero slot Pl[NITEMS][.]), so each table row is read once for all
-// columns and an item's or entry's gathers return the FC values together.
-// Roles start at different threads (Z rows from thread 0, items after
-// them, Q entries from the last thread down), so a wave seldom holds two.
-// Per (item, column), (row, column) and (entry, column) the arithmetic and
-// its order are those of the one-column-per-lane phases (same bits).
-std::string fused_merged_phases(uint32_t qml, uint32_t qun, int fc, const std::string &st5, const std::string &st1)
+MdpRatioWork mdp_jit_ratio_work(const MdpJitPlan &pl)
 {
-    const uint32_t G = 8, ngm = (qml + G - 1) / G;  // = kQGroup (spom_engine.hip)
-    uint32_t ngp = 1;
-    while (ngp < ngm) ngp *= 2;
-    std::ostringstream o;
-    o << "    constexpr int KZR = (NJ + NT - 1) / NT, KPC = (NITEMS + NT - 1) / NT, KQ = (LDQ + NT - 1) / NT;\n"
-         "#define ZW(k) ((k) * NT + threadIdx.x)\n"
-         "#define IW(k) ((k) * NT + (threadIdx.x + NT - (NJ < NT ? NJ : 0)) % NT)\n"
-         "#define QW(k) ((k) * NT + NT - 1 - threadIdx.x)\n"
-         // items: their descriptor and row pressures, the FC columns' products
-         "    double Fp[KPC][FC];\n"
-         "    u32 zi[KPC];\n"
-         "#pragma unroll\n"
-         "    for (int k = 0; k < KPC; ++k) {\n"
-         "        const u32 w = IW(k), it = w < NITEMS ? w : NITEMS - 1;\n"
-         "        const uint2 t = Itl[it];\n"
-         "        const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
-         "        double sv[NVAR];\n"
-         "#pragma unroll\n"
-         "        for (int b = 0; b < NVAR; ++b) sv[b] = Svl[r * NVAR + b];\n"
-         "        const u32 nB = ~B;\n"
-         "#pragma unroll\n"
-         "        for (int f = 0; f < FC; ++f) {\n"
-         "            const double c = cc[f];\n"
-         "            double fb[NVAR];\n"
-         "#pragma unroll\n"
-         "            for (int b = 0; b < NVAR; ++b) {\n"
-         "                const u32 bit = NVAR - 1 - b;\n"
-         "                const double pcv = c * sv[b];\n"
-         "                const double p = (pcv > 1.0) | ((j >> bit) & 1u) ? 1.0 : pcv;\n"
-         "                const double sg = __hiloint2double((int)(0x3ff00000u | ((nB << (31 - bit)) & 0x80000000u)), 0);\n"
-         "                fb[b] = fma(sg, p, fma(-0.5, sg, 0.5));\n"
-         "            }\n"
-         "#pragma unroll\n"
-         "            for (int s = 1; s < NVAR; s *= 2)\n"
-         "#pragma unroll\n"
-         "                for (int b = 0; b + s < NVAR; b += 2 * s) fb[b] *= fb[b + s];\n"
-         "            Fp[k][f] = fb[0];\n"
-         // (kept before the Z phase's barrier: otherwise the compiler sinks
-         // this arithmetic past it, where every wave waits on it)
-         "            asm volatile(\"\" : \"+v\"(Fp[k][f]));\n"
-         "        }\n"
-         "        zi[k] = r;\n"
-         "    }\n"
-         // Q entries: bounds and first item indices (past the count: the zero slot)
-         "    u32 qb[KQ], qn[KQ], qx[KQ][QUN];\n"
-         "#pragma unroll\n"
-         "    for (int k = 0; k < KQ; ++k) {\n"
-         "        const u32 w = QW(k);\n"
-         "        const bool live = w < LDQ && w < NCOEF;\n"
-         "        const u32 qc = live ? w : 0u, q0 = Qsl[qc], q1 = Qsl[qc + 1];\n"
-         "        qb[k] = live ? q0 : 0u;\n"
-         "        qn[k] = live ? q1 - q0 : 0u;\n"
-         "#pragma unroll\n"
-         "        for (int u = 0; u < QUN; ++u) { const u32 t_ = Qil[qb[k] + u]; qx[k][u] = (u32)u < qn[k] ? t_ : (u32)NITEMS; }\n"
-         "    }\n"
-         // Z rows: the row's explicit columns once, the FC columns' chains
-         "#pragma unroll\n"
-         "    for (int k = 0; k < KZR; ++k) {\n"
-         "        const u32 w = ZW(k);\n"
-         "        if (w < NJ) {\n"
-         "            const u32 r = w;\n"
-         "            double sk[KZ];\n"
-         "#pragma unroll\n"
-         "            for (u32 kk = 0; kk < KZ; kk += 2) {\n"
-         "                const double2 t2 = ((const double2 *)zl)[(ZPAD || kk < kmax ? kk : kk % 8u) / 2 * NJ + r];\n"
-         "                const bool in = ZPAD || kk < kmax;\n"
-         "                sk[kk] = in ? t2.x : 0.0;\n"
-         "                sk[kk + 1] = in ? t2.y : 0.0;\n"
-         "            }\n"
-         "            const double2 *zq = (const double2 *)(zcl + r * 8);\n"
-         "            const double2 p01 = zq[0], p23 = zq[1], p45 = zq[2], p67 = zq[3];\n"
-         "            double zf[FC];\n"
-         "#pragma unroll\n"
-         "            for (int f = 0; f < FC; ++f) {\n"
-         "                const double c = cc[f];\n"
-         "                double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
-         "#pragma unroll\n"
-         "                for (u32 kk = 0; kk < KZ; kk += 8) {\n"
-         "                    za *= fma(-c, sk[kk + 0], 1.0) * fma(-c, sk[kk + 4], 1.0);\n"
-         "                    zb *= fma(-c, sk[kk + 1], 1.0) * fma(-c, sk[kk + 5], 1.0);\n"
-         "                    zc *= fma(-c, sk[kk + 2], 1.0) * fma(-c, sk[kk + 6], 1.0);\n"
-         "                    zd *= fma(-c, sk[kk + 3], 1.0) * fma(-c, sk[kk + 7], 1.0);\n"
-         "                }\n"
-         "                double z = (za * zb) * (zc * zd);\n"
-         "                if (kmax && !(fma(-c, sk[0], 1.0) > 0.0)) z = 0.0;\n"
-         "                double q = p67.y;\n"
-         "                q = fma(q, c, p67.x);\n"
-         "                q = fma(q, c, p45.y);\n"
-         "                q = fma(q, c, p45.x);\n"
-         "                q = fma(q, c, p23.y);\n"
-         "                q = fma(q, c, p23.x);\n"
-         "                q = fma(q, c, p01.y);\n"
-         "                q = fma(q, c, p01.x);\n"
-         "                zf[f] = z * exp(-(q * c));\n"
-         "            }\n"
-         "#pragma unroll\n"
-         "            for (int f = 0; f < FC; ++f) Zl[r * FC + f] = zf[f];\n"
-         "        }\n"
-         "    }\n"
-         "    __syncthreads();\n"
-      << st5 <<
-         // Pc per (item, column), and the zero slot
-         "#pragma unroll\n"
-         "    for (int k = 0; k < KPC; ++k) {\n"
-         "        const u32 w = IW(k);\n"
-         "        if (w < NITEMS) {\n"
-         "#pragma unroll\n"
-         "            for (int f = 0; f < FC; ++f) Pl[w * FC + f] = Zl[zi[k] * FC + f] * Fp[k][f];\n"
-         "        }\n"
-         "    }\n"
-         "    if (threadIdx.x < FC) Pl[NITEMS * FC + threadIdx.x] = 0.0;\n"
-         "    __syncthreads();\n"
-      << st1 <<
-         // Q entries: every gather unconditional, the canonical order per column
-         "#pragma unroll\n"
-         "    for (int k = 0; k < KQ; ++k) {\n"
-         "        const u32 w = QW(k);\n"
-         "        if (w < LDQ) {\n"
-         "            double p_[" << qml << "][FC];\n";
-    for (uint32_t u = 0; u < qml; ++u) {
-        const std::string idx = u < qun ? "qx[k][" + std::to_string(u) + "]"
-                                        : "(" + std::to_string(u) + "u < qn[k] ? Qil[qb[k] + " + std::to_string(u) +
-                                              "u] : (u32)NITEMS)";
-        o << "            { const u32 x_ = " << idx << ";\n"
-             "#pragma unroll\n"
-             "              for (int f = 0; f < FC; ++f) p_[" << u << "][f] = Pl[x_ * FC + f]; }\n";
-    }
-    o << "#pragma unroll\n"
-         "            for (int f = 0; f < FC; ++f) {\n"
-         "                double g_[" << ngp << "];\n";
-    for (uint32_t g = 0; g < ngp; ++g) {
-        if (g >= ngm) {
-            o << "                g_[" << g << "] = 0.0;\n";
-            continue;
+    MdpRatioWork w;
+    if (pl.np.empty()) return w;
+    const Schedule sch = schedule(pl);
+    // B^E by squaring: floor(log2 E) squarings + popcount(E) - 1 products
+    auto powcost = [](uint32_t E) -> double {
+        if (E <= 1) return 0.0;
+        return (double)(31 - __builtin_clz(E)) + (double)__builtin_popcount(E) - 1.0;
+    };
+    w.setup_t = 2.0 + (sch.dp > 1 ? sch.dp - 1.0 : 0.0);
+    w.setup_s = w.setup_t + (sch.dg > 1 ? sch.dg - 1.0 : 0.0);
+    const uint32_t kOffM = (1u << 22) - 1u;
+    std::set<uint32_t> groups, gd;
+    for (uint32_t d : pl.udesc) {
+        const uint32_t off = d & kOffM, nX = (d >> 22) & 31u, nA = d >> 27;
+        if (groups.insert(off).second) {
+            w.use_s += 2.0 * nX;
+            w.use_t += 2.0 * nX;
         }
-        o << "                g_[" << g << "] = p_[" << G * g << "][f]";
-        for (uint32_t u = 1; u < G && G * g + u < qml; ++u) o << " + p_[" << G * g + u << "][f]";
-        o << ";\n";
+        if (nA > nX && gd.insert(off | (nA - nX) << 22).second) w.use_s += 1.0;
     }
-    for (uint32_t w = ngp; w > 1; w /= 2)
-        for (uint32_t i = 0; i < w / 2; ++i)
-            o << "                g_[" << i << "] = g_[" << 2 * i << "] + g_[" << 2 * i + 1 << "];\n";
-    o << "                Ql[f * LDQ + w] = g_[0];\n"
-         "                Ql[FC * LDQ + f * LDQ + REVQ[w]] = g_[0];\n"
-         "            }\n"
-         "        }\n"
-         "    }\n";
-    (void)fc;
-    return o.str();
+    double yr = 0.0;
+    for (size_t t = 1; t < pl.np.size(); ++t) {
+        const double npp = pl.np[t - 1], npc = pl.np[t];
+        yr += npc * (2.0 * npp - 1.0);
+        for (uint32_t df : sch.diff[t]) yr += df ? 1.0 : 0.0;
+        if (sch.flush[t]) yr += npc + powcost(sch.flush[t]);
+    }
+    w.use_s += yr;
+    w.use_t += yr;
+    w.final_pt = (double)pl.np.back() + 1.0 + (sch.final_exp ? powcost(sch.final_exp) + 1.0 : 0.0);
+    return w;
 }
 
 int mdp_jit_default_epl(const std::vector<uint32_t> &) { return 2; }
@@ -508,9 +363,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
           << pl.off_it << "\n#define OFF_QS " << pl.off_qs << "\n#define OFF_QI " << pl.off_qi << "\n#define OFF_ZC "
           << pl.off_zc << "\n#define OFF_ZS "
           << pl.off_zs << "\n#define KZ " << std::max<uint32_t>(8u, pl.kzmax) << "\n#define ZPAD " << (pl.zpad ? 1 : 0)
-          << "\n#define OFF_MV " << pl.off_mv << "\n#define OFF_ZL " << pl.off_zl << "\n#define OFF_RJ " << pl.off_rj
-          << "\n#define NN " << pl.n << "\n#define ZCT " << (pl.n < 255 ? "unsigned char" : "unsigned short")
-          << "\n#define ZNONE " << (pl.n < 255 ? "0xffu" : "0xffffu")
           << "\n#define QML "
           << std::max<uint32_t>(1u, pl.qmaxlen) << "\n#define QUN " << std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)
           << "\n#define NSTG "
@@ -535,12 +387,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         all.push_back((uint32_t)ldq_local);
         all.push_back((uint32_t)ldq_local + 1);
         for (size_t q = 0; q < all.size(); ++q) o << (q ? (q % 32 ? "," : ",\n") : "") << all[q];
-        o << "};\n";
-    }
-    if (pl.fused && pl.sbuild) {  // the var columns (S-build)
-        o << "__constant__ const unsigned short VC[" << std::max<size_t>(1, pl.var_cols.size()) << "] = {";
-        for (size_t b = 0; b < pl.var_cols.size(); ++b) o << (b ? "," : "") << pl.var_cols[b];
-        if (pl.var_cols.empty()) o << "0";
         o << "};\n";
     }
     o << "extern \"C\" __global__ __launch_bounds__(NT) "
@@ -635,10 +481,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
          "    double v[EPL][NPMAX];\n    double n[EPL][(NPMAX + SPL - 1) / SPL];\n";
     if (pl.vlds)  // wide years: state k of point i of lane tid at Vl[k][i][tid]
         o << "    __shared__ double Vl[NPMAX * EPL * KBLOCK];\n";
-    // the per-point set-up (ratio, its division, the power tables, the start
-    // vector) depends on the lane's e value alone: emitted first, its
-    // latency hides under the prologue's loads (early_w), or after it
-    if (pl.early_w) o << wblock;
     // the state k of point i, as an expression
     auto vref = [&](uint32_t k) {
         return pl.vlds ? "Vl[(" + std::to_string(k) + " * EPL + i) * KBLOCK + tid]" : "v[i][" + std::to_string(k) + "]";
@@ -702,32 +544,16 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    __shared__ double Zl[FC * NJ];\n"
              "#define PLS (NITEMS + 1)\n"  // a column's items, then its zero slot (the flat Q sums' padding)
              "    __shared__ double Pl[FC * PLS];\n"
-          << (pl.direct && !pl.sbuild
-                  // direct: the phases read the column tables where they lie
-                  // (HBM / L2) instead of a staged LDS image -- no staging
-                  // round trip and barrier before the first table read
-                  ? "    const double *ctg = coltab;\n"
-                  : "    const double *ctg = ct;\n") <<
-             "    const uint2 *Itl = (const uint2 *)(ctg + OFF_IT);\n"
-             "    const u32 *Qsl = (const u32 *)(ctg + OFF_QS);\n"
-             "    const u32 *Qil = (const u32 *)(ctg + OFF_QI);\n"
-             "    const double *zcl = ctg + OFF_ZC;\n"
-          << (pl.sbuild
-                  // the colonisation sums are built here (S-build, below) from the
-                  // var columns' dispersal rows: half the bytes to stage
-                  ? "    __shared__ __attribute__((aligned(16))) double Zsb[KZ * NJ];\n"
-                    "    __shared__ double Svb[NJ * NVAR + 1];\n"
-                    "    const double *Svl = Svb;\n"
-                    "    const double *zl = Zsb;\n"
-                    "    const double *Mvl = ct + OFF_MV;\n"
-                    "    const ZCT *Zcl = (const ZCT *)(ct + OFF_ZL);\n"
-                    "    const u32 *Rjl = (const u32 *)(ct + OFF_RJ);\n"
-                  : "    const double *Svl = ctg;\n"
-                    "    const double *zl = ctg + OFF_ZS;\n") <<
+             "    const uint2 *Itl = (const uint2 *)(ct + OFF_IT);\n"
+             "    const u32 *Qsl = (const u32 *)(ct + OFF_QS);\n"
+             "    const u32 *Qil = (const u32 *)(ct + OFF_QI);\n"
+             "    const double *zcl = ct + OFF_ZC;\n"
+             "    const double *Svl = ct;\n"
+             "    const double *zl = ct + OFF_ZS;\n"
              "    double cc[FC];\n"
              "#pragma unroll\n"
              "    for (int f = 0; f < FC; ++f) cc[f] = ic0 + f < nc ? cvals[ic0 + f] : 0.0;\n"
-          << (pl.direct && !pl.sbuild ? "    if (false) {\n" : "    {\n") <<
+             "    {\n"
              "        const double2 *src = (const double2 *)coltab;\n"
              "        double2 *dst = (double2 *)ct;\n"
              "        const u32 n2 = ct_len / 2;\n"
@@ -745,40 +571,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "            dst[i < n2 ? i : n2] = t[k];\n"
              "        }\n"
              "    }\n"
-          << (pl.direct && !pl.sbuild ? "" : "    __syncthreads();\n")
-          << (pl.sbuild
-                  // S-build: per row r (hidden state j) its explicit columns'
-                  // S[j][k] into the zs image (row pairs [k/2][r][k%2]) and its
-                  // var columns' into Svb, each the host's sum (spom_engine.hip
-                  // build_direct_plan): M[V_b][k] over the var columns b of j,
-                  // V_b != k, ascending b -- the same bits as the staged tables
-                  ? "    {\n"
-                    "        constexpr u32 NSB = NJ * (KZ + NVAR), KSB = (NSB + NT - 1) / NT;\n"
-                    "#pragma unroll\n"
-                    "        for (u32 k = 0; k < KSB; ++k) {\n"
-                    "            const u32 w = threadIdx.x + k * NT;\n"
-                    "            if (w < NSB) {\n"
-                    "                const u32 r = w % NJ, sl = w / NJ, j = Rjl[r];\n"
-                    "                const u32 col = sl < KZ ? (u32)Zcl[sl * NJ + r] : (u32)VC[sl - KZ];\n"
-                    "                double S = 0.0;\n"
-                    "                if (col != ZNONE) {\n"
-                    "#pragma unroll\n"
-                    "                    for (int b = 0; b < NVAR; ++b)\n"
-                    "                        if (((j >> (NVAR - 1 - b)) & 1u) && (u32)VC[b] != col) S += Mvl[b * NN + col];\n"
-                    "                }\n"
-                    "                if (sl < KZ) Zsb[((sl / 2) * NJ + r) * 2 + (sl & 1)] = S;\n"
-                    "                else Svb[r * NVAR + (sl - KZ)] = S;\n"
-                    "            }\n"
-                    "        }\n"
-                    "    }\n"
-                    "    __syncthreads();\n"
-                  : "")
-          << stamp(4);
-        if (pl.cmerge && FC > 1)
-            o << fused_merged_phases(std::max<uint32_t>(1u, pl.qmaxlen),
-                                     std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u), FC, stamp(5), stamp(1));
-        else
-            o <<
+             "    __syncthreads();\n"
+          << stamp(4) <<
              // operands of the Pc and Q phases that do not depend on Z, read
              // and combined before the Z phase: per item its Z slot and the
              // product F of its var-column factors (a fixed pairwise tree),
@@ -791,123 +585,8 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    double Fp[KPC];\n"
              "    u32 zi[KPC];\n"
              "#define ITEM_W(k) ((k) * NT + (((k) & 1) ? NT - 1 - threadIdx.x : threadIdx.x))\n"
-             // balanced prologue (pl.bal): the Z rows on the last threads, the Q
-             // entries just below them, the items from thread 0 -- so no wave
-             // carries an item, a Q entry's descriptors and a Z row at once
-             // (the Q descriptors stay with the thread that sums the entry)
-          << (pl.bal ? "#define ZW(k) ((k) * NT + NT - 1 - threadIdx.x)\n"
-                       "#define QROT (FC * NJ + FC * LDQ <= NT ? NT - FC * NJ - FC * LDQ : 0)\n"
-                       "#define QW(k) ((k) * NT + (threadIdx.x + NT - QROT) % NT)\n"
-                     : "#define ZW(k) ((k) * NT + threadIdx.x)\n#define QW(k) ((k) * NT + threadIdx.x)\n")
-          << (pl.ph2flat ? std::string(
-             // issue-first form (ph2flat): every first-level LDS load of the
-             // three roles (item descriptors, Q-entry bounds, Z rows and their
-             // series coefficients) unconditional and in flight together, then
-             // the second level (each item's row pressures S, each entry's item
-             // indices), then the arithmetic -- two LDS round trips on the
-             // critical path instead of one or two per role in sequence
-             "    constexpr int KZR = (FC * NJ + NT - 1) / NT;\n"
-             "    uint2 it_[KPC];\n"
-             "#pragma unroll\n"
-             "    for (int k = 0; k < KPC; ++k) {\n"
-             "        const u32 w = ITEM_W(k);\n"
-             "        it_[k] = Itl[(w < FC * NITEMS ? w : FC * NITEMS - 1) / FC];\n"
-             "    }\n"
-             "    u32 qb[KQ], qn[KQ], qx[KQ][QUN];\n"
-             "#pragma unroll\n"
-             "    for (int k = 0; k < KQ; ++k) {\n"
-             "        const u32 w = QW(k), q = w % LDQ;\n"
-             "        const bool live = w < FC * LDQ && q < NCOEF;\n"
-             "        const u32 qc = live ? q : 0u, q0 = Qsl[qc], q1 = Qsl[qc + 1];\n"
-             "        qb[k] = live ? q0 : 0u;\n"
-             "        qn[k] = live ? q1 - q0 : 0u;\n"
-             "    }\n"
-             "    double2 zr_[KZR][KZ / 2], zq_[KZR][4];\n"
-             "#pragma unroll\n"
-             "    for (int k = 0; k < KZR; ++k) {\n"
-             "        const u32 w = ZW(k), r = (w < FC * NJ ? w : FC * NJ - 1) / FC;\n"
-             "#pragma unroll\n"
-             "        for (u32 kk = 0; kk < KZ; kk += 2) zr_[k][kk / 2] = ((const double2 *)zl)[(ZPAD || kk < kmax ? kk : kk % 8u) / 2 * NJ + r];\n"
-             "#pragma unroll\n"
-             "        for (int u = 0; u < 4; ++u) zq_[k][u] = ((const double2 *)(zcl + r * 8))[u];\n"
-             "    }\n"
-             "    double sv_[KPC][NVAR];\n"
-             "#pragma unroll\n"
-             "    for (int k = 0; k < KPC; ++k) {\n"
-             "        const u32 r = (it_[k].x >> 24) | ((it_[k].y >> 24) << 8);\n"
-             "#pragma unroll\n"
-             "        for (int b = 0; b < NVAR; ++b) sv_[k][b] = Svl[r * NVAR + b];\n"
-             "    }\n"
-             "#pragma unroll\n"
-             "    for (int k = 0; k < KQ; ++k)\n"
-             "#pragma unroll\n"
-             "        for (int u = 0; u < QUN; ++u) { const u32 t_ = Qil[qb[k] + u]; qx[k][u] = (u32)u < qn[k] ? t_ : (u32)NITEMS; }\n"
-             "#pragma unroll\n"
-             "    for (int k = 0; k < KPC; ++k) {\n"
-             "        const u32 w = ITEM_W(k);\n"
-             "        const u32 col = w % FC;\n"
-             "        const double c = cc[col];\n"
-             "        const uint2 t = it_[k];\n"
-             "        const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
-             "        double f[NVAR];\n"
-             "        const u32 nB = ~B;\n"
-             "#pragma unroll\n"
-             "        for (int b = 0; b < NVAR; ++b) {\n"
-             "            const u32 bit = NVAR - 1 - b;\n"
-             "            const double pcv = c * sv_[k][b];\n"
-             "            const double p = (pcv > 1.0) | ((j >> bit) & 1u) ? 1.0 : pcv;\n"
-             "            const double sg = __hiloint2double((int)(0x3ff00000u | ((nB << (31 - bit)) & 0x80000000u)), 0);\n"
-             "            f[b] = fma(sg, p, fma(-0.5, sg, 0.5));\n"
-             "        }\n"
-             "#pragma unroll\n"
-             "        for (int s = 1; s < NVAR; s *= 2)\n"
-             "#pragma unroll\n"
-             "            for (int b = 0; b + s < NVAR; b += 2 * s) f[b] *= f[b + s];\n"
-             "        Fp[k] = w < FC * NITEMS ? f[0] : 0.0;\n"
-             "        zi[k] = w < FC * NITEMS ? col * NJ + r : 0u;\n"
-             // (kept before the Z phase's barrier: otherwise the compiler sinks
-             // this arithmetic past it, where every wave waits on it)
-             "        asm volatile(\"\" : \"+v\"(Fp[k]));\n"
-             "    }\n"
-             "#pragma unroll\n"
-             "    for (int k = 0; k < KZR; ++k) {\n"
-             "        const u32 w = ZW(k);\n"
-             "        if (w < FC * NJ) {\n"
-             "            const u32 col = w % FC, r = w / FC;\n"
-             "            const double c = cc[col];\n"
-             "            double sk[KZ];\n"
-             "#pragma unroll\n"
-             "            for (u32 kk = 0; kk < KZ; kk += 2) {\n"
-             "                const bool in = ZPAD || kk < kmax;\n"
-             "                sk[kk] = in ? zr_[k][kk / 2].x : 0.0;\n"
-             "                sk[kk + 1] = in ? zr_[k][kk / 2].y : 0.0;\n"
-             "            }\n"
-             "            double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
-             "#pragma unroll\n"
-             "            for (u32 kk = 0; kk < KZ; kk += 8) {\n"
-             "                za *= fma(-c, sk[kk + 0], 1.0) * fma(-c, sk[kk + 4], 1.0);\n"
-             "                zb *= fma(-c, sk[kk + 1], 1.0) * fma(-c, sk[kk + 5], 1.0);\n"
-             "                zc *= fma(-c, sk[kk + 2], 1.0) * fma(-c, sk[kk + 6], 1.0);\n"
-             "                zd *= fma(-c, sk[kk + 3], 1.0) * fma(-c, sk[kk + 7], 1.0);\n"
-             "            }\n"
-             "            double z = (za * zb) * (zc * zd);\n"
-             "            if (kmax && !(fma(-c, sk[0], 1.0) > 0.0)) z = 0.0;\n"
-             "            {\n"
-             "                const double2 p01 = zq_[k][0], p23 = zq_[k][1], p45 = zq_[k][2], p67 = zq_[k][3];\n"
-             "                double q = p67.y;\n"
-             "                q = fma(q, c, p67.x);\n"
-             "                q = fma(q, c, p45.y);\n"
-             "                q = fma(q, c, p45.x);\n"
-             "                q = fma(q, c, p23.y);\n"
-             "                q = fma(q, c, p23.x);\n"
-             "                q = fma(q, c, p01.y);\n"
-             "                q = fma(q, c, p01.x);\n"
-             "                z *= exp(-(q * c));\n"
-             "            }\n"
-             "            Zl[col * NJ + r] = z;\n"
-             "        }\n"
-             "    }\n") : std::string(
-             "#pragma unroll\n"
+             "#define ZW(k) ((k) * NT + threadIdx.x)\n#define QW(k) ((k) * NT + threadIdx.x)\n"
+"#pragma unroll\n"
              "    for (int k = 0; k < KPC; ++k) {\n"
              "        const u32 w = ITEM_W(k);\n"
              "        Fp[k] = 0.0;\n"
@@ -946,14 +625,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        const u32 q0 = live ? Qsl[q] : 0u, q1 = live ? Qsl[q + 1] : 0u;\n"
              "        qb[k] = q0;\n"
              "        qn[k] = q1 - q0;\n"
-             "#pragma unroll\n") +
-             // only the entry's own items: lanes past their count stay masked
-             // off, so the gathers below touch no other entry's banks (qflat:
              // every index load in flight, reading past the entry within the
-             // image; slots past the count name the zero slot)
-             (pl.qflat
-                  ? "        for (int u = 0; u < QUN; ++u) { const u32 t_ = Qil[q0 + u]; qx[k][u] = (u32)u < qn[k] ? t_ : (u32)NITEMS; }\n"
-                  : "        for (int u = 0; u < QUN; ++u) qx[k][u] = (u32)u < qn[k] ? Qil[q0 + u] : 0u;\n") + std::string(
+             // image; slots past the count name the zero slot
+             "#pragma unroll\n"
+             "        for (int u = 0; u < QUN; ++u) { const u32 t_ = Qil[q0 + u]; qx[k][u] = (u32)u < qn[k] ? t_ : (u32)NITEMS; }\n"
              "    }\n"
              // Z per (column, row): the row's KZ (compile-time bound) values
              // all in flight; rows past kmax contribute fma(-c, 0, 1) = 1 (with
@@ -1001,7 +676,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "            }\n"
              "            Zl[col * NJ + r] = z;\n"
              "        }\n"
-             "    }\n")) <<
+             "    }\n"
              "    __syncthreads();\n"
           << stamp(5) <<
              "#pragma unroll\n"
@@ -1018,14 +693,13 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        const u32 w = QW(k);\n"
              "        if (w < FC * LDQ) {\n"
              "            const double *pl = Pl + (w / LDQ) * PLS;\n"
-          << (pl.qflat ? qsum_flat_code(std::max<uint32_t>(1u, pl.qmaxlen), std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u))
-                       : qsum_code(std::max<uint32_t>(1u, pl.qmaxlen), std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u))) <<
+          << qsum_flat_code(std::max<uint32_t>(1u, pl.qmaxlen), std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)) <<
              "            Ql[w] = a;\n"
              "            Ql[FC * LDQ + (w / LDQ) * LDQ + REVQ[w % LDQ]] = a;\n"
              "        }\n"
              "    }\n";
     }
-    if (!pl.early_w) o << wblock;
+    o << wblock;
     o << "    __syncthreads();\n"
       << stamp(2)
       // the prologue's extra threads (PRO > 1) are done: the forward runs on NTF
@@ -1331,27 +1005,79 @@ std::string mdp_jit_log_source()
 
 namespace {
 
+// hipRTC entry points, resolved from libhiprtc on first use
+struct RtcApi {
+    bool ok = false;
+    std::string err;
+    decltype(&hiprtcCreateProgram) create = nullptr;
+    decltype(&hiprtcCompileProgram) compile = nullptr;
+    decltype(&hiprtcGetProgramLogSize) log_size = nullptr;
+    decltype(&hiprtcGetProgramLog) get_log = nullptr;
+    decltype(&hiprtcGetCodeSize) code_size = nullptr;
+    decltype(&hiprtcGetCode) get_code = nullptr;
+    decltype(&hiprtcDestroyProgram) destroy = nullptr;
+    decltype(&hiprtcGetErrorString) errstr = nullptr;
+};
+
+const RtcApi &rtc()
+{
+    static RtcApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = nullptr;
+        for (const char *name : {"libhiprtc.so.7", "libhiprtc.so"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) {
+            const char *e = dlerror();
+            api.err = std::string("cannot load libhiprtc: ") + (e ? e : "?");
+            return;
+        }
+        bool all = true;
+        auto sym = [&](auto &fp, const char *name) {
+            fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+            all = all && fp;
+        };
+        sym(api.create, "hiprtcCreateProgram");
+        sym(api.compile, "hiprtcCompileProgram");
+        sym(api.log_size, "hiprtcGetProgramLogSize");
+        sym(api.get_log, "hiprtcGetProgramLog");
+        sym(api.code_size, "hiprtcGetCodeSize");
+        sym(api.get_code, "hiprtcGetCode");
+        sym(api.destroy, "hiprtcDestroyProgram");
+        sym(api.errstr, "hiprtcGetErrorString");
+        api.ok = all;
+        if (!all) api.err = "libhiprtc lacks an entry point";
+    });
+    return api;
+}
+
 const char *const kJitOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
 constexpr int kJitNOpts = 3;
-constexpr int kJitCacheFormat = 2;  // bump when the cache key or file layout changes
+constexpr int kJitCacheFormat = 3;  // bump when the cache key or file layout changes
 
-// Cache key: the generated source, the compile options, the hipRTC version
-// and the cache format.  A code object built by another toolchain or with
-// other options therefore lands under another name.
+// Cache key: the generated source, the compile options, the ROCm release
+// (the HIP runtime's version, which hipRTC ships with -- asking hipRTC itself
+// would load it on every run) and the cache format.  A code object built by
+// another toolchain or with other options therefore lands under another name.
 uint64_t jit_key(const std::string &src)
 {
-    int major = 0, minor = 0;
-    (void)hiprtcVersion(&major, &minor);
+    int rt = 0;
+    (void)hipRuntimeGetVersion(&rt);
     std::string k = src;
     k += '\0';
     for (const char *o : kJitOpts) (k += o) += ' ';
-    k += "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " format " + std::to_string(kJitCacheFormat);
+    k += "hip " + std::to_string(rt) + " headers " + std::to_string(HIP_VERSION) + " format " +
+         std::to_string(kJitCacheFormat);
     return fnv1a(k);
 }
 
 // Cache files are the code object followed by a 16-byte trailer: "MDPJ", the
 // format, and the 64-bit key it was compiled for.  A file whose trailer does
-// not name this key (a foreign or planted object, another format) is a miss.
+// not name this key (a stale or corrupted file, another format, another
+// key's object under this name) is a miss.  The trailer is a staleness and
+// corruption check, not an authentication: the key is also the file name.
+// What keeps other users' objects out is the directory check
+// (cache_dir_private).
 constexpr char kTrailerMagic[4] = {'M', 'D', 'P', 'J'};
 
 void add_trailer(std::vector<char> &c, uint64_t key)
@@ -1404,35 +1130,40 @@ int mdp_jit_compile(const std::string &src, std::vector<char> &code, std::string
     snprintf(name, sizeof name, "fwd_%016llx.co", (unsigned long long)key);
     const std::string dir = cache_dir();
     const std::string path = dir + "/" + name;
-    if (!fresh && !getenv("MDP_JIT_NOCACHE") && read_file(path, code) && strip_trailer(code, key) &&
-        plausible_code_object(code)) {
+    if (!fresh && !getenv("MDP_JIT_NOCACHE") && cache_dir_private(dir) && read_file(path, code) &&
+        strip_trailer(code, key) && plausible_code_object(code)) {
         std::lock_guard<std::mutex> lk(g_mu);
         g_code[key] = code;
         return 0;
     }
+    const RtcApi &R = rtc();
+    if (!R.ok) {
+        log = R.err;
+        return -1;
+    }
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "mdp_fwd_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    if (R.create(&prog, src.c_str(), "mdp_fwd_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         log = "hiprtcCreateProgram failed";
         return -1;
     }
-    const hiprtcResult r = hiprtcCompileProgram(prog, kJitNOpts, kJitOpts);
+    const hiprtcResult r = R.compile(prog, kJitNOpts, kJitOpts);
     size_t ls = 0;
-    hiprtcGetProgramLogSize(prog, &ls);
+    R.log_size(prog, &ls);
     if (ls > 1) {
         std::vector<char> lb(ls + 1, 0);
-        hiprtcGetProgramLog(prog, lb.data());
+        R.get_log(prog, lb.data());
         log = lb.data();
     }
     if (r != HIPRTC_SUCCESS) {
-        hiprtcDestroyProgram(&prog);
-        if (log.empty()) log = hiprtcGetErrorString(r);
+        R.destroy(&prog);
+        if (log.empty()) log = R.errstr(r);
         return -1;
     }
     size_t cs = 0;
-    hiprtcGetCodeSize(prog, &cs);
+    R.code_size(prog, &cs);
     code.resize(cs);
-    hiprtcGetCode(prog, code.data());
-    hiprtcDestroyProgram(&prog);
+    R.get_code(prog, code.data());
+    R.destroy(&prog);
     {
         std::lock_guard<std::mutex> lk(g_mu);
         g_code[key] = code;

@@ -23,38 +23,15 @@ struct MdpJitPlan {
     // register kernels: one copy of the forward per ratio form (the t-form
     // copy without g^d factors); false: one copy for both
     bool split_forms = true;
-    // the per-point set-up (ratio, power tables, start vector) before the
-    // prologue rather than after it
-    bool early_w = false;  // neutral on config 2, config 3 forward 43.1-43.7 vs 44.3-44.5 us with it
-    // fused prologue: Z rows, Q entries and items on disjoint threads
-    bool bal = false;  // measured slower (ph2 2.4 k -> 2.7 k cycles)
-    // fused Q sums and their index loads unconditional (zero slot padding)
-    bool qflat = true;
-    // fused prologue's Z-independent phase in issue-first form (all
-    // first-level LDS loads of items, Q entries and Z rows in flight together)
-    bool ph2flat = false;  // measured slower (ph2 + ph3 3.5 k vs 2.8 k cycles)
     // several columns per workgroup: each column's lanes rotated by half a
     // block (SIMD balance of the ratio forms)
     bool rot = true;
-    // fused prologue: one lane per item / Q entry / Z row for all the
-    // workgroup's columns, per-column values interleaved in LDS
-    bool cmerge = false;
-    // fused prologue reads the column tables from HBM / L2 where used
-    // instead of staging them in LDS first
-    bool direct = false;  // measured slower (phase 2 4.3 k vs 2.4 k cycles: twice the VALU chain per lane)
     int hack = 0;  // diag build only (MDP_JIT_HACK; results wrong): 1 = no log, no stores; 2 = no stores
     uint32_t nj = 0, nvar = 0, nitems = 0, ncoef = 0, nqi = 0;
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
     // items, qstart, qitem, the Z-row series coefficients [nj][8], then
     // zs[kmax][nj] (the explicit "large" columns)
     uint32_t off_it = 0, off_qs = 0, off_qi = 0, off_zc = 0, off_zs = 0;
-    // S-build layout (sbuild): instead of the var-column S and the zs image,
-    // the var columns' dispersal rows Mv[nvar][n] (off_mv), each row's
-    // explicit column list [kzmax][nj] (u8 for n < 255, else u16; off_zl)
-    // and each row's hidden state j (off_rj); the kernel builds S itself
-    bool sbuild = false;  // measured slower on config 2 (10.4 vs 9.2-9.4 us): off by default
-    uint32_t off_mv = 0, off_zl = 0, off_rj = 0, n = 0;
-    std::vector<uint32_t> var_cols;
     uint32_t kzmax = 0;    // zs rows compiled in (grids with |c| <= 1; larger ones use k_qrows)
     bool zpad = false;     // the fused image always holds kzmax zs rows (zero past kmax)
     uint32_t qmaxlen = 0;  // most items of one Q entry
@@ -100,6 +77,22 @@ int mdp_jit_default_epl(const std::vector<uint32_t> &udesc);
 // The pending exponent of B after the plan's years, starting from plan.e0
 // (the next chunk's e0).
 uint32_t mdp_jit_end_exp(const MdpJitPlan &plan);
+
+// The ratio forms' algorithmic FP64 work per grid point,
+// from the plan's enumeration alone (np, udesc, e0): per point of each form
+// the set-up (y = 1 - x, the ratio's division, the power tables of B and g
+// beyond their first powers), every distinct Q group's Horner chain once
+// (2 nX), g^d once per distinct (group, d > 0) on s-form points, each
+// year's state update npc (2 npp - 1), the source pre-scales (1 per source
+// above the year's minimum |A|), the flushes of the deferred exponent (npc
+// multiplies + the power B^E by squaring), and the end: the prior sum
+// (np_last), B^final and log (1 each).
+struct MdpRatioWork {
+    double setup_s = 0, setup_t = 0;  // per s-form / t-form point
+    double use_s = 0, use_t = 0;      // transitions, state updates, pre-scales, flushes
+    double final_pt = 0;              // prior sum, final exponent, log
+};
+MdpRatioWork mdp_jit_ratio_work(const MdpJitPlan &plan);
 
 // HIP source of `mdp_fwd_jit` for this plan; sets plan.epl when it was 0.
 std::string mdp_jit_forward_source(MdpJitPlan &plan);

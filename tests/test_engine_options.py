@@ -6,7 +6,10 @@
   the default library; the diag library (libmidaspom_diag.so) accepts them.
 * A cached code object is used only if its trailer names the cache key of
   the source being compiled (source, compile options, hipRTC version): a
-  planted or foreign file under the key is rebuilt, not loaded.
+  stale, corrupted or foreign file under the key is rebuilt, not loaded (a
+  staleness / corruption check).  The cache directory itself is used only
+  while it is private to this user (0700-created, owned by the user, not
+  group- or world-writable), which is what keeps other users' objects out.
 
 Each case runs in a subprocess (the library is loaded once per process)."""
 from __future__ import annotations
@@ -63,10 +66,21 @@ assert rc == -5, (rc, msg)
 # MDP_JIT_HACK in the environment is not read by the library
 rc, msg = create(None, c_plain=True)
 assert rc == -5, (rc, msg)
-# ... while the Python layer forwards it as an option, which the default
-# library refuses instead of building kernels with wrong results
+# ... and the Python layer does not forward it from the environment to the
+# default library (a warning, then the plain engine: no device here) ...
+import warnings
+with warnings.catch_warnings(record=True) as w:
+    warnings.simplefilter("always")
+    try:
+        mdp.Engine(model)
+    except mdp.MidaspomError as ex:
+        assert "MDP_ENODEV" in str(ex), ex
+    else:
+        raise SystemExit("no device, yet created")
+assert any("measurement-only" in str(x.message) for x in w), [str(x.message) for x in w]
+# ... while an explicit option of that name is refused
 try:
-    mdp.Engine(model)
+    mdp.Engine(model, options="MDP_JIT_HACK=1")
 except mdp.MidaspomError as ex:
     assert "measurement-only" in str(ex), ex
 else:
@@ -89,7 +103,7 @@ print("ok")
 
 
 @pytest.mark.skipif(gpu_available(), reason="offline compile check runs on CPU-only hosts")
-def test_jit_cache_rejects_planted_and_foreign_objects(tmp_path):
+def test_jit_cache_rejects_stale_and_foreign_objects(tmp_path):
     """Compile config 1's forward kernels into an empty cache; then replace
     every cached file by garbage, by a bare gfx950 ELF without our trailer,
     and by another key's (valid) file: each time the engine recompiles, and
@@ -120,3 +134,74 @@ print("ok")
         assert "ok" in run(code, env)
         for f in files:
             assert f.read_bytes() == good[f], f.name
+
+
+def _gpu_option_cases():
+    import ast
+    tree = ast.parse((ROOT / "tests" / "test_gpu_options.py").read_text())
+    vals = {}
+    for node in tree.body:
+        if isinstance(node, ast.Assign) and isinstance(node.targets[0], ast.Name) \
+                and node.targets[0].id in ("VARIANTS", "TOOLING"):
+            vals[node.targets[0].id] = ast.literal_eval(node.value)
+    return vals["VARIANTS"], vals["TOOLING"]
+
+
+def test_every_accepted_option_has_a_parity_case():
+    """Every option name the default library accepts (the Python mirror
+    ENGINE_OPTION_NAMES, checked against the C list below) is set by some
+    case of tests/test_gpu_options.py (oracle parity on the GPU), or is a
+    tooling option that selects no kernel."""
+    from midaspom_amd import _lib
+    variants, tooling = _gpu_option_cases()
+    used = set()
+    for opts, _ in variants:
+        for kv in opts.split(";"):
+            used.add(kv.split("=")[0])
+    accepted = [n for n in _lib.ENGINE_OPTION_NAMES if n not in _lib.DIAG_OPTION_NAMES]
+    missing = [n for n in accepted if n not in used and n not in tooling]
+    assert not missing, f"options with no GPU parity case: {missing}"
+    assert used <= set(accepted), used - set(accepted)
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks option parsing up to the device probe (CPU hosts)")
+def test_c_library_accepts_exactly_the_python_list():
+    """The C library's option list equals _lib.ENGINE_OPTION_NAMES: each
+    name passes the parser (then: no device), and the round-4 measured-off
+    variants (removed in round 5) are unknown."""
+    out = run(r"""
+for name in _lib.ENGINE_OPTION_NAMES:
+    if name in _lib.DIAG_OPTION_NAMES:
+        continue
+    rc, msg = create((name + "=1").encode())
+    assert rc == -5, (name, rc, msg)
+for name in ("MDP_FUSED_SBUILD", "MDP_FUSED_BAL", "MDP_FUSED_PH2FLAT", "MDP_FUSED_CMERGE", "MDP_FUSED_DIRECT",
+             "MDP_JIT_EARLYW", "MDP_FUSED_QFLAT"):
+    rc, msg = create((name + "=1").encode())
+    assert rc == -1 and "unknown engine option" in msg, (name, rc, msg)
+print("ok")
+""")
+    assert "ok" in out
+
+
+@pytest.mark.skipif(gpu_available(), reason="offline compile check runs on CPU-only hosts")
+def test_jit_cache_ignores_a_shared_directory(tmp_path):
+    """A cache directory that others can write to is neither read nor
+    written: the engine compiles, the directory stays empty; made private
+    again, the cache fills."""
+    cache = tmp_path / "shared"
+    cache.mkdir()
+    os.chmod(cache, 0o777)
+    code = r"""
+import os
+os.environ.pop("MDP_JIT_NOCACHE", None)
+rc, msg = create(b"MDP_JIT_CHECK=1")
+assert rc == -5 and "forward kernels compiled" in msg, msg
+print("ok")
+"""
+    env = {"MDP_JIT_CACHE": str(cache)}
+    assert "ok" in run(code, env)
+    assert not list(cache.iterdir())
+    os.chmod(cache, 0o700)
+    assert "ok" in run(code, env)
+    assert len(list(cache.glob("fwd_*.co"))) == 2

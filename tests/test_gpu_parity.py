@@ -589,13 +589,26 @@ def test_grid_dropping_columns_then_full_grid(monkeypatch, fused):
 @pytest.mark.parametrize("fname", ["config2_64x50.txt", "config3_256x200.txt", "occupancies.txt"])
 def test_work_fact_per_point_terms_from_the_model(golden, fname):
     """mdp_engine_work_fact's per-point terms restated from the enumerated
-    model alone: every use (k -> l between consecutive years)
-    costs 2 |A&B| + 3, the weight table 2 maxA + one product per W[|A|][m]
-    used, the prior sum 2 np_last - 1; flop = nc per-c + ne nc per-point."""
+    model alone.  Ratio forms (the numerator, ABI 8): per
+    point the set-up (1 - x, the division, the B and g power tables past
+    their first powers), each distinct Q group (A & B, B) once (2 |A & B|),
+    g^d once per distinct (group, d = |A| - |A & B| > 0) on s-form points,
+    the state updates npc (2 npp - 1), one pre-scale per source above the
+    year's minimum |A|, the deferred-exponent flushes (E >= 192: npc + the
+    power by squaring), the end (np_last + 1 + the final power).  Legacy
+    direct form: every use 2 |A&B| + 3, the weight table 2 maxA + one
+    product per W[|A|][m] used, the prior sum 2 np_last - 1."""
     model = mdp.Model.load(golden / fname)
     ids, ss = model.year_ids, model.short_state
     use, use_min, mmax, seen = 0.0, 0.0, {}, set()
+    groups, gd, yr, dp, dg = set(), set(), 0.0, 0, 0
+    E, flushes = 0, []
+
+    def powcost(x):
+        return 0 if x <= 1 else x.bit_length() - 1 + bin(x).count("1") - 1
+
     for t in range(1, model.tmax):
+        a_src = [bin(int(ss[a])).count("1") for a in ids[t - 1]]
         for b in ids[t]:
             for a in ids[t - 1]:
                 A, B = int(ss[a]), int(ss[b])
@@ -605,18 +618,40 @@ def test_work_fact_per_point_terms_from_the_model(golden, fname):
                     seen.add((A & B, B, nA))
                     use_min += 2 * nX + 1
                 mmax[nA] = max(mmax.get(nA, -1), nX)
+                if (A & B, B) not in groups:
+                    groups.add((A & B, B))
+                    yr += 2 * nX
+                if nA > nX:
+                    dg = max(dg, nA - nX)
+                    if (A & B, B, nA - nX) not in gd:
+                        gd.add((A & B, B, nA - nX))
         use_min += len(ids[t]) * (2 * len(ids[t - 1]) - 1)  # the state updates of year t
+        amin = min(a_src)
+        dp = max(dp, max(a_src) - amin)
+        yr += len(ids[t]) * (2 * len(ids[t - 1]) - 1) + sum(1 for a in a_src if a > amin)
+        E += amin
+        if E >= 192:
+            yr += len(ids[t]) + powcost(E)
+            E = 0
     maxA = max(mmax) if mmax else 0
     weight = 2 * maxA + sum(m + 1 for m in mmax.values())
     final = 2 * len(ids[-1]) - 1
-    g, _ = mdp.grid(8)
+    setup_t = 2 + max(dp - 1, 0)
+    setup_s = setup_t + max(dg - 1, 0)
+    use_s, use_t = yr + len(gd), yr
+    final_r = len(ids[-1]) + 1 + (powcost(E) + 1 if E else 0)
+    g, _ = mdp.grid(8)  # e = i/7: rows 0-3 s-form (x < 1/2), 4-7 t-form
     with mdp.Engine(model) as eng:
         eng.set_grid(g, g)
         w = eng.work_fact(8, 8)
     assert (w["use_pt"], w["use_pt_min"], w["weight_pt"], w["final_pt"]) == (use, use_min, weight, final)
     per_c = w["z_c"] + w["pc_c"] + w["item_c"] + w["q_c"]
     assert w["flop"] == 8 * per_c + 64 * (use + weight + final)
-    assert w["flop_min"] == 8 * per_c + 64 * (use_min + weight + final)
+    assert w["flop_min_direct"] == 8 * per_c + 64 * (use_min + weight + final)
+    assert w["setup_pt"] == pytest.approx(0.5 * (setup_s + setup_t))
+    assert w["use_pt_ratio"] == pytest.approx(0.5 * (use_s + use_t))
+    assert w["final_pt_ratio"] == final_r
+    assert w["flop_min"] == pytest.approx(8 * per_c + 64 * (0.5 * (setup_s + use_s + setup_t + use_t) + final_r))
 
 
 def test_wide_single_year():
