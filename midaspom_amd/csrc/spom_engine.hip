@@ -1122,72 +1122,82 @@ __global__ __launch_bounds__(kBlock) void k_wq(uint32_t c0, uint32_t nitems, con
 }
 
 // Wide years on the matrix cores (FP64 MFMA, v_mfma_f64_16x16x4_f64).  For
-// one column c and a block of kMmaPts points, year t's new state vector is
+// one column c and a block of PTS points, year t's new state vector is
 //     n[p][l] = sum_(k, m) W[p][(k, m)] C[(k, m)][l],
 //     W[p][(k, m)] = v[p][k] x_p^(|A_k| - m) y_p^m,   C[(k, m)][l] = Q_kl[m]
 // (0 past the transition's nX): the transition P[k][l] = sum_m Q_kl[m]
 // x^(|A|-m) y^m of the wide kernels (direct weights, as k_fwd_wide), summed
 // over K = every source's (k, m <= |A_k|) -- one GEMM per year of M = the
 // points, N = the new states, K = sum_k (|A_k| + 1), on the matrix cores with
-// the states of the block's points in LDS.  C's fragments are gathered from
-// the column's Q row: a lane's K entry (k, |A_k|, m; staged in LDS two years
-// ahead) names the transition descriptor (k, l) (host table, c-independent:
-// the Q-row offset of the transition's coefficients and its nX), and m <= nX
-// picks the slot.  W's are formed from the states and per-point power tables
-// in LDS.
-// 16 waves, one work item each per year: (column tile, pair of row tiles,
-// slice of the year's K chunks) -- with 16 / (2 ncol) slices in years of 16,
-// 32 or 64 states, so that every wave is busy; later slices leave their
-// partial products in the state buffer's rows past the year's column tiles
-// and the first adds them in slice order.  A wave's gathers run one chunk of
-// kMmaU steps ahead (descriptors two), and its first chunks of year t + 1 are
-// issued before year t's closing barriers.  The products sum in another
+// the states of the block's points in LDS.  Each MFMA computes the transposed
+// tile n^T = C^T W^T (A operand: the gathered C values, states x K; B: the
+// W values, K x points), so a lane's accumulators are 4 states of one point
+// and the year's stores are rows of 16 consecutive points (conflict-free).
+// C's fragments are gathered from the column's Q row: a lane's K entry (k, m,
+// the LDS rows of v_k, x^(|A_k|-m) and y^m) names the transition descriptor
+// (k, l) (host table, c-independent: the Q-row offset of the transition's
+// coefficients and its nX), and m <= nX picks the slot, else the zero slot.
+// 16 waves, one work item each per year: (column tile, every row tile, slice
+// of the year's K chunks) -- with S = min(16 / ncol, room, nch / 2) slices, so
+// that up to 16 waves are busy in a year of any size.  Slice 1 leaves its
+// partial products in the year's own destination rows, later slices in the
+// state buffer's rows past the year's column tiles; slice 0 adds them in
+// slice order (deterministic).  Each lane's K entries run three chunks ahead
+// in a ring of four register slots (loaded once: from LDS, staged two years
+// ahead, or with KG from the global table when three years do not fit), the
+// transition descriptors two and the C gathers one; the loop body is
+// unrolled four times so the slots are fixed.  The products sum in another
 // order than k_fwd_wide's (positive terms: ~1e-15 relative).
-constexpr uint32_t kMmaPts = 64;        // points per workgroup (4 row tiles of 16)
 constexpr uint32_t kMmaThreads = 1024;  // 16 waves
 constexpr uint32_t kMmaU = 2;           // K steps (of 4) per pipeline chunk: years padded to 8 entries
-constexpr uint32_t kMmaNone = 0x80000000u;  // descriptor of a padded column (l >= the year's states)
-constexpr uint32_t kMmaRows = 128;      // state buffer rows (also the K slices' partial sums)
-constexpr uint32_t kMmaPS = 80;         // power-table row stride: rows r, r + 1 on different bank halves
-constexpr uint32_t kMmaRT = 4;         // row tiles a wave takes (2 or 4)
-constexpr uint32_t kMmaKtRegs = 4;      // K entries per thread staged per year (<= 4096)
+constexpr uint32_t kMmaKtRegs = 4;      // K entries per thread staged per year (LDS staging: <= 4096)
+constexpr uint32_t kMmaDummy = 1u << 21; // K-entry field of the descriptor row k (bits 21-28)
+// the kernel's shape for NPM states a year (padded to 16): points per block,
+// state buffer rows (>= 128, for the slices' partial sums), power-table row
+// stride (rows r and r + 1 on different LDS bank halves)
+constexpr uint32_t mma_pts(uint32_t npm) { return npm > 128 ? 32u : 64u; }
+constexpr uint32_t mma_rows(uint32_t npm) { return npm > 128 ? npm : 128u; }
+constexpr uint32_t mma_ps(uint32_t npm) { return mma_pts(npm) + 16u; }
 typedef double mdp_d4 __attribute__((ext_vector_type(4)));
-template <int NPM>  // states per year, padded to 16 (64 or 128)
+template <int NPM, bool KG>  // NPM: states per year, padded (64, 128 or 256); KG: K entries read from HBM
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint2 *__restrict__ kt,
     const uint32_t *__restrict__ kbase, const uint32_t *__restrict__ desc, const uint32_t *__restrict__ dbase,
     uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne, uint32_t c0, uint32_t maxA,
     uint32_t ktmax, uint32_t zslot, double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
 {
-    static_assert(NPM <= (int)kMmaRows, "state rows");
+    constexpr uint32_t PTS = mma_pts(NPM), ROWS = mma_rows(NPM), PS = mma_ps(NPM), RT = PTS / 16;
+    static_assert(NPM <= (int)ROWS && NPM <= 256, "state rows");
     extern __shared__ __attribute__((aligned(16))) double mlds[];
-    double *Va = mlds, *Vb = mlds + (size_t)kMmaRows * kMmaPts;      // [state][point]
-    double *xp = Vb + (size_t)kMmaRows * kMmaPts, *yp = xp + (size_t)(maxA + 1) * kMmaPS;  // [r][point]
-    uint2 *Kl = (uint2 *)(yp + (size_t)(maxA + 1) * kMmaPS);  // [3][ktmax]: year t's K entries at t % 3
+    double *Va = mlds, *Vb = mlds + (size_t)ROWS * PTS;  // [state][point]
+    double *xp = Vb + (size_t)ROWS * PTS, *yp = xp + (size_t)(maxA + 1) * PS;  // [r][point]
+    uint2 *Kl = (uint2 *)(yp + (size_t)(maxA + 1) * PS);  // (LDS staging) [3][ktmax]: year t's at t % 3
     const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
-    const uint32_t p0 = blockIdx.x * kMmaPts, ic = c0 + blockIdx.y;
-    if (threadIdx.x < kMmaPts) {
+    const uint32_t p0 = blockIdx.x * PTS, ic = c0 + blockIdx.y;
+    if (threadIdx.x < PTS) {
         const uint32_t ie = p0 + threadIdx.x;
         const double e = ie < ne ? evals[ie] : 0.0;
         const double x = e > 1.0 ? 1.0 : e, y = 1.0 - x;
         double a = 1.0, b = 1.0;
         for (uint32_t r = 0; r <= maxA; ++r) {
-            xp[r * kMmaPS + threadIdx.x] = a;
-            yp[r * kMmaPS + threadIdx.x] = b;
+            xp[r * PS + threadIdx.x] = a;
+            yp[r * PS + threadIdx.x] = b;
             a *= x;
             b *= y;
         }
     }
     const uint32_t np0 = np[0];
-    for (uint32_t i = threadIdx.x; i < (uint32_t)NPM * kMmaPts; i += kMmaThreads) Va[i] = i / kMmaPts < np0 ? 1.0 : 0.0;
-    for (uint32_t t = 1; t < 3 && t < tmax; ++t)
-        for (uint32_t i = threadIdx.x; i < kbase[t + 1] - kbase[t]; i += kMmaThreads) Kl[(t % 3) * ktmax + i] = kt[kbase[t] + i];
+    for (uint32_t i = threadIdx.x; i < (uint32_t)NPM * PTS; i += kMmaThreads) Va[i] = i / PTS < np0 ? 1.0 : 0.0;
+    if (!KG)
+        for (uint32_t t = 1; t < 3 && t < tmax; ++t)
+            for (uint32_t i = threadIdx.x; i < kbase[t + 1] - kbase[t]; i += kMmaThreads)
+                Kl[(t % 3) * ktmax + i] = kt[kbase[t] + i];
     __syncthreads();
     const double *q = Q + (size_t)ic * ldQ;
     const uint32_t kk = lane >> 4, col = lane & 15u;
     // this wave's work item of year t
     struct Item {
-        uint32_t npc, npcp, nch, nit, S, item, ks, cb, ce, lc, r0;
+        uint32_t npc, npcp, nch, nit, S, item, ks, cb, ce, sh, lc4;
         bool active;
         const uint2 *kl;
         const uint32_t *dt;
@@ -1198,127 +1208,156 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         const uint32_t ncol = (it.npc + 15) / 16;
         it.npcp = ncol * 16;
         it.nch = (kbase[t + 1] - kbase[t]) / (4 * kMmaU);
-        it.nit = ncol * (4 / kMmaRT);
-        // slices of at least two chunks; a wave has at most one item a year
-        it.S = 16 % it.nit == 0 ? min(min(16 / it.nit, 8 / ncol), max(1u, it.nch / 2)) : 1;
+        it.nit = ncol;
+        // slices: at most 16 waves; slice 1 in the destination rows, later
+        // ones in the (ROWS - npcp) rows past them; at least two chunks each
+        const uint32_t room = 2 + (ROWS - it.npcp) / it.npcp;
+        it.S = min(min(16 / ncol, room), max(1u, it.nch / 2));
         it.active = wv < it.nit * it.S;
         it.item = wv % it.nit;
         it.ks = wv / it.nit;
         it.cb = it.nch * it.ks / it.S;
         it.ce = it.nch * (it.ks + 1) / it.S;
-        it.lc = (it.item / (4 / kMmaRT)) * 16 + col;
-        it.r0 = (it.item % (4 / kMmaRT)) * kMmaRT;
-        it.kl = Kl + (t % 3) * ktmax;
-        it.dt = desc + __builtin_amdgcn_readfirstlane(dbase[t]);  // [k][npcp]
+        // descriptor rows [k][2^sh >= npcp] (row npp: the padded entries')
+        it.sh = 32u - (uint32_t)__builtin_clz(it.npcp - 1u);
+        it.lc4 = (it.item * 16 + col) << 2;
+        it.kl = KG ? kt + __builtin_amdgcn_readfirstlane(kbase[t]) : Kl + (t % 3) * ktmax;
+        it.dt = desc + __builtin_amdgcn_readfirstlane(dbase[t]);
         return it;
     };
+    // the lane's K entry (kk) of step u of chunk ch (clamped into the year)
     auto kent = [&](const Item &it, uint32_t ch, uint32_t u) {
-        return it.kl[((ch < it.nch ? ch : it.nch - 1) * kMmaU + u) * 4 + kk];
+        const uint32_t c = ch < it.nch ? ch : it.nch - 1;
+        return it.kl[(c * kMmaU + u) * 4 + kk];
     };
     // (32-bit byte offsets from uniform bases: the loads take the scalar-base
     // form, with no 64-bit address arithmetic per lane)
     auto dsc = [&](const Item &it, uint2 en) {
-        return *(const uint32_t *)((const char *)it.dt + ((((en.y >> 24) & 0x7fu) * it.npcp + it.lc) << 2));
+        const uint32_t k = (en.y >> 21) & 0xffu;
+        return *(const uint32_t *)((const char *)it.dt + ((k << (it.sh + 2)) + it.lc4));
     };
-    // C[(k, m)][l]: the slot of Q_kl[m], or the Q row's zero slot (ldQ > ncoef)
+    // C[(k, m)][l]: the slot of Q_kl[m], or the Q row's zero slot (ldQ > ncoef;
+    // absent transitions' descriptors name it with nX = 0)
     auto cval = [&](uint2 en, uint32_t d) {
-        const uint32_t m = (en.y >> 16) & 0xffu;
-        const bool ok = (en.y >> 31) != 0u && (d >> 31) == 0u && m <= ((d >> kOffBits) & 31u);
-        return *(const double *)((const char *)q + ((ok ? (d & kOffMask) + m : zslot) << 3));
+        const uint32_t m = (en.y >> 16) & 31u;
+        return *(const double *)((const char *)q + ((m <= ((d >> kOffBits) & 31u) ? (d & kOffMask) + m : zslot) << 3));
     };
-    // ring slots by chunk parity (relative to the item's first chunk): the
-    // descriptors of chunks ch + 1 and ch + 2, the C values of ch and ch + 1;
-    // the loop body runs twice per pass with the slots fixed, so nothing moves
+    // rings by chunk position j = ch - cb (mod 4 / mod 2): K entries of ch ..
+    // ch + 3, descriptors of ch + 1 and ch + 2, C values of ch and ch + 1
+    uint2 ee[4][kMmaU];
     uint32_t dd[2][kMmaU];
     double bb[2][kMmaU];
-    auto issue_d = [&](const Item &it, uint32_t ch, uint32_t sl) {
-#pragma unroll
-        for (uint32_t u = 0; u < kMmaU; ++u) dd[sl][u] = dsc(it, kent(it, ch, u));
-    };
-    auto issue_b = [&](const Item &it, uint32_t ch, uint32_t sl) {
-#pragma unroll
-        for (uint32_t u = 0; u < kMmaU; ++u) bb[sl][u] = cval(kent(it, ch, u), dd[sl][u]);
-    };
     auto prime = [&](const Item &it) {
-        issue_d(it, it.cb, 0);
-        issue_d(it, it.cb + 1, 1);
-        issue_b(it, it.cb, 0);
+#pragma unroll
+        for (uint32_t u = 0; u < kMmaU; ++u) {
+            ee[0][u] = kent(it, it.cb, u);
+            ee[1][u] = kent(it, it.cb + 1, u);
+            ee[2][u] = kent(it, it.cb + 2, u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kMmaU; ++u) {
+            dd[0][u] = dsc(it, ee[0][u]);
+            dd[1][u] = dsc(it, ee[1][u]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kMmaU; ++u) bb[0][u] = cval(ee[0][u], dd[0][u]);
     };
     Item cur = plan(tmax > 1 ? 1u : 0u);
     if (tmax > 1 && cur.active) prime(cur);
     for (uint32_t t = 1; t < tmax; ++t) {
-        // year t + 2's K entries: loaded now, stored before the year's barrier
+        // (LDS staging) year t + 2's K entries: loaded now, stored before the year's barrier
         uint2 nk[kMmaKtRegs];
-        const uint32_t kn0 = t + 2 < tmax ? kbase[t + 2] : 0u, kn = t + 2 < tmax ? kbase[t + 3] - kn0 : 0u;
+        const uint32_t kn0 = !KG && t + 2 < tmax ? kbase[t + 2] : 0u, kn = !KG && t + 2 < tmax ? kbase[t + 3] - kn0 : 0u;
+        if (!KG)
 #pragma unroll
-        for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
-            const uint32_t i = threadIdx.x + r * kMmaThreads;
-            nk[r] = i < kn ? kt[kn0 + i] : make_uint2(0u, 0u);
-        }
-        mdp_d4 acc[kMmaRT];
+            for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
+                const uint32_t i = threadIdx.x + r * kMmaThreads;
+                nk[r] = i < kn ? kt[kn0 + i] : make_uint2(0u, 0u);
+            }
+        mdp_d4 acc[RT];
 #pragma unroll
-        for (uint32_t h = 0; h < kMmaRT; ++h) acc[h] = mdp_d4{0.0, 0.0, 0.0, 0.0};
-        // one chunk: the descriptors of ch + 2, the C values of ch + 1, then
-        // ch's products (W formed unconditionally: padded entries name row 0
-        // and meet C = 0)
-        auto chunk = [&](uint32_t ch, uint32_t sl) {
-            issue_d(cur, ch + 2, sl);
-            issue_b(cur, ch + 1, sl ^ 1u);
+        for (uint32_t h = 0; h < RT; ++h) acc[h] = mdp_d4{0.0, 0.0, 0.0, 0.0};
+        // one chunk at ring position j: the K entries of ch + 3, the
+        // descriptors of ch + 2, the C values of ch + 1, then ch's products (W
+        // formed unconditionally: padded entries name row 0 and meet C = 0)
+        auto chunk = [&](uint32_t ch, auto jc) {
+            constexpr uint32_t j = decltype(jc)::value;
+#pragma unroll
+            for (uint32_t u = 0; u < kMmaU; ++u) ee[(j + 3) & 3][u] = kent(cur, ch + 3, u);
+#pragma unroll
+            for (uint32_t u = 0; u < kMmaU; ++u) dd[j & 1][u] = dsc(cur, ee[(j + 2) & 3][u]);
+#pragma unroll
+            for (uint32_t u = 0; u < kMmaU; ++u) bb[(j + 1) & 1][u] = cval(ee[(j + 1) & 3][u], dd[(j + 1) & 1][u]);
 #pragma unroll
             for (uint32_t u = 0; u < kMmaU; ++u) {
-                const uint2 en = kent(cur, ch, u);
+                const uint2 en = ee[j][u];
 #pragma unroll
-                for (uint32_t h = 0; h < kMmaRT; ++h) {
-                    const uint32_t pb = ((cur.r0 + h) * 16 + col) * 8u;
+                for (uint32_t h = 0; h < RT; ++h) {
+                    const uint32_t pb = (h * 16 + col) * 8u;
                     const double wt = *(const double *)((const char *)xp + (en.x >> 16) + pb) *
                                       *(const double *)((const char *)yp + (en.y & 0xffffu) + pb);
                     const double av = *(const double *)((const char *)Va + (en.x & 0xffffu) + pb) * wt;
-                    acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bb[sl][u], acc[h], 0, 0, 0);
+                    acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(bb[j & 1][u], av, acc[h], 0, 0, 0);
                 }
             }
         };
         if (cur.active)
-            for (uint32_t ch = cur.cb; ch < cur.ce; ch += 2) {
-                chunk(ch, 0);
-                if (ch + 1 < cur.ce) chunk(ch + 1, 1);
+            for (uint32_t ch = cur.cb; ch < cur.ce; ch += 4) {
+                chunk(ch, std::integral_constant<uint32_t, 0>{});
+                if (ch + 1 < cur.ce) chunk(ch + 1, std::integral_constant<uint32_t, 1>{});
+                if (ch + 2 < cur.ce) chunk(ch + 2, std::integral_constant<uint32_t, 2>{});
+                if (ch + 3 < cur.ce) chunk(ch + 3, std::integral_constant<uint32_t, 3>{});
             }
         // next year's first chunks in flight across this year's barriers
         // (its K entries were staged a year ago)
         const Item nxt = plan(t + 1 < tmax ? t + 1 : t);
         if (t + 1 < tmax && nxt.active) prime(nxt);
-        // n[p][l]: lane holds column l = lc, rows kk + 4 r of each tile; slice
-        // j > 0's partials: (S - 1) x 2 ncol x 512 doubles past row npcp, at
-        // most the (kMmaRows - npcp) x kMmaPts the buffer has
+        // the lane's accumulators: states item * 16 + kk + 4 r of point
+        // h * 16 + col; slice 1 stores them in place, slice j >= 2 past row
+        // npcp ((S - 2) x ncol x 16 PTS doubles at most, within the buffer)
+        double *dst = Vb + (size_t)(cur.item * 16 + kk) * PTS + col;
         auto part = [&](uint32_t j) {
-            return Vb + (size_t)cur.npcp * kMmaPts + (size_t)((j - 1) * cur.nit + cur.item) * (kMmaRT * 256) + lane;
+            return Vb + (size_t)cur.npcp * PTS + (size_t)((j - 2) * cur.nit + cur.item) * (RT * 256) + lane;
         };
-        if (cur.active && cur.ks > 0) {
+        if (cur.active && cur.ks == 1)
+#pragma unroll
+            for (uint32_t h = 0; h < RT; ++h)
+#pragma unroll
+                for (uint32_t r = 0; r < 4; ++r) dst[(size_t)(4 * r) * PTS + h * 16] = acc[h][r];
+        if (cur.active && cur.ks >= 2) {
             double *pk = part(cur.ks);
 #pragma unroll
-            for (uint32_t h = 0; h < kMmaRT; ++h)
+            for (uint32_t h = 0; h < RT; ++h)
 #pragma unroll
                 for (uint32_t r = 0; r < 4; ++r) pk[(h * 4 + r) * 64] = acc[h][r];
         }
         if (cur.S > 1) __syncthreads();
         if (cur.active && cur.ks == 0) {
-            for (uint32_t j = 1; j < cur.S; ++j) {
+            if (cur.S > 1)
+#pragma unroll
+                for (uint32_t h = 0; h < RT; ++h)
+#pragma unroll
+                    for (uint32_t r = 0; r < 4; ++r) acc[h][r] = acc[h][r] + dst[(size_t)(4 * r) * PTS + h * 16];
+            for (uint32_t j = 2; j < cur.S; ++j) {
                 const double *pj = part(j);
 #pragma unroll
-                for (uint32_t h = 0; h < kMmaRT; ++h)
+                for (uint32_t h = 0; h < RT; ++h)
 #pragma unroll
                     for (uint32_t r = 0; r < 4; ++r) acc[h][r] = acc[h][r] + pj[(h * 4 + r) * 64];
             }
-            if (cur.lc < cur.npc)
+            // (padded states l >= npc hold 0: their C values are the zero slot)
 #pragma unroll
-                for (uint32_t h = 0; h < kMmaRT; ++h)
+            for (uint32_t h = 0; h < RT; ++h)
 #pragma unroll
-                    for (uint32_t r = 0; r < 4; ++r) Vb[cur.lc * kMmaPts + (cur.r0 + h) * 16 + kk + 4 * r] = acc[h][r];
+                for (uint32_t r = 0; r < 4; ++r) dst[(size_t)(4 * r) * PTS + h * 16] = acc[h][r];
         }
-        uint2 *kw = Kl + ((t + 2) % 3) * ktmax;
+        if (!KG) {
+            uint2 *kw = Kl + ((t + 2) % 3) * ktmax;
 #pragma unroll
-        for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
-            const uint32_t i = threadIdx.x + r * kMmaThreads;
-            if (i < kn) kw[i] = nk[r];
+            for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
+                const uint32_t i = threadIdx.x + r * kMmaThreads;
+                if (i < kn) kw[i] = nk[r];
+            }
         }
         __syncthreads();
         double *tv = Va;
@@ -1326,10 +1365,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         Vb = tv;
         cur = nxt;
     }
-    if (threadIdx.x < kMmaPts) {
+    if (threadIdx.x < PTS) {
         const uint32_t ie = p0 + threadIdx.x, npl = np[tmax - 1];
         double L = 0.0;
-        for (uint32_t l = 0; l < npl; ++l) L += Va[l * kMmaPts + threadIdx.x] * prior0;
+        for (uint32_t l = 0; l < npl; ++l) L += Va[l * PTS + threadIdx.x] * prior0;
         if (ie < ne) out[(size_t)ie * ld_out + (size_t)ic * out_cs] = log(L);
     }
 }
@@ -1530,7 +1569,7 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
     "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_JIT_SPLIT", "MDP_JIT_ROT",
-    "MDP_WIDE_MMA"};
+    "MDP_WIDE_MMA", "MDP_WIDE_MMA_KG"};
 const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
@@ -1626,7 +1665,7 @@ struct mdp_engine {
     // k_fwd_mma (wide years on the matrix cores): per year t its K entries
     // (k | |A_k| << 8 | m << 16 | valid << 31, padded to 4) from kbase[t],
     // and the Q-row slot of each (K entry, new state l) from gbase[t]
-    bool mma = false;
+    bool mma = false, mma_kg = false;  // kg: K entries read from HBM, not staged in LDS
     uint32_t mma_npm = 0;
     std::vector<uint2> mma_kt;  // per year its K entries: LDS byte offsets of the W rows, m, k
     std::vector<uint32_t> mma_kbase, mma_desc, mma_dbase;
@@ -1958,12 +1997,31 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
 // plus the FP64 work per grid point of k_fwd_wide (every use a (nX+1)-term
 // dot product with a weight multiply per term, one FMA into the state
 // vector; the per-lane power tables; the final prior sum).
-// k_fwd_mma: two state buffers and the power tables of kMmaPts points, three
-// years' K entries
+// k_fwd_mma: two state buffers and the power tables of the block's points,
+// and (LDS staging) three years' K entries
 size_t mma_lds(const mdp_engine *eng)
 {
-    return (2 * (size_t)kMmaRows * kMmaPts + 2 * ((size_t)eng->maxA + 1) * kMmaPS) * sizeof(double) +
-           3 * (size_t)eng->mma_ktmax * sizeof(uint2);
+    const uint32_t npm = eng->mma_npm;
+    return (2 * (size_t)mma_rows(npm) * mma_pts(npm) + 2 * ((size_t)eng->maxA + 1) * mma_ps(npm)) * sizeof(double) +
+           (eng->mma_kg ? 0 : 3 * (size_t)eng->mma_ktmax * sizeof(uint2));
+}
+
+// the k_fwd_mma instantiation of the engine's plan
+const void *mma_kernel(const mdp_engine *eng)
+{
+    if (eng->mma_npm == 64) return eng->mma_kg ? (const void *)k_fwd_mma<64, true> : (const void *)k_fwd_mma<64, false>;
+    if (eng->mma_npm == 128) return eng->mma_kg ? (const void *)k_fwd_mma<128, true> : (const void *)k_fwd_mma<128, false>;
+    return (const void *)k_fwd_mma<256, true>;
+}
+
+// the device's LDS per workgroup (the current device; 160 KiB on gfx950)
+size_t device_lds_max()
+{
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && v > 0)
+        return (size_t)v;
+    return 160 * 1024;
 }
 
 int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
@@ -1976,15 +2034,20 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
     double f = 2.0 * (eng->maxA + 1) + 2.0 * eng->np[eng->tmax - 1];
     for (uint32_t d : eng->udesc_d) f += 3.0 * (((d >> kOffBits) & 31u) + 1.0) + 2.0;
     eng->wide_flops_pt = f;
-    // k_fwd_mma's tables (c-independent): years of at most 128 states, at
-    // most 24 occupied patches a state (its per-point power tables); per
-    // year its K entries (k, |A_k|, m), padded to whole pipeline chunks, and
-    // the transition descriptors [k][l] (Q-row offset | nX << kOffBits)
+    // k_fwd_mma's tables (c-independent): years of at most 256 states; per
+    // year its K entries (k, |A_k|, m), padded to whole pipeline chunks with
+    // entries naming the descriptor row npp (every transition absent), and the
+    // transition descriptors [k][2^sh >= npcp] (Q-row offset | nX << kOffBits;
+    // an absent transition names the zero slot with nX = 0)
     eng->mma = false;
-    if (eng->npmax <= 128 && eng->maxA <= 24) {
+    eng->mma_kg = false;
+    if (eng->npmax <= 256 && eng->maxA <= 24) {
         const char *mv = eng->opts.get("MDP_WIDE_MMA");
         if (!mv || atoi(mv) != 0) {
-            eng->mma_npm = eng->npmax <= 64 ? 64u : 128u;
+            const uint32_t npm = eng->npmax <= 64 ? 64u : eng->npmax <= 128 ? 128u : 256u;
+            const uint32_t pts = mma_pts(npm), ps = mma_ps(npm);
+            const uint32_t none = (uint32_t)eng->ncoef_d;  // the zero slot, nX = 0
+            eng->mma_npm = npm;
             eng->mma_kt.clear();
             eng->mma_desc.clear();
             eng->mma_kbase.assign(eng->tmax + 1, 0u);
@@ -1993,20 +2056,22 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
             size_t ub = 0;
             for (uint32_t t = 1; t < eng->tmax; ++t) {
                 const uint32_t npp = eng->np[t - 1], npc = eng->np[t], npcp = (npc + 15) / 16 * 16;
+                uint32_t ld = 16;
+                while (ld < npcp) ld *= 2;
                 eng->mma_kbase[t] = (uint32_t)eng->mma_kt.size();
                 eng->mma_dbase[t] = (uint32_t)eng->mma_desc.size();
                 for (uint32_t k = 0; k < npp; ++k) {
                     const uint32_t a = eng->udesc_d[ub + k] >> 27;  // |A_k| (any use from k; l = 0)
-                    for (uint32_t m = 0; m <= a; ++m)  // Va row k, xp row a - m, yp row m (bytes); m; k; valid
-                        eng->mma_kt.push_back(make_uint2((k * kMmaPts * 8u) | (((a - m) * kMmaPS * 8u) << 16),
-                                                         (m * kMmaPS * 8u) | (m << 16) | (k << 24) | (1u << 31)));
+                    for (uint32_t m = 0; m <= a; ++m)  // Va row k, xp row a - m, yp row m (bytes); m; k
+                        eng->mma_kt.push_back(make_uint2((k * pts * 8u) | (((a - m) * ps * 8u) << 16),
+                                                         (m * ps * 8u) | (m << 16) | (k * kMmaDummy)));
                 }
-                while (eng->mma_kt.size() % (4 * kMmaU)) eng->mma_kt.push_back(make_uint2(0u, 0u));
+                while (eng->mma_kt.size() % (4 * kMmaU)) eng->mma_kt.push_back(make_uint2(0u, npp * kMmaDummy));
                 eng->mma_ktmax = std::max<uint32_t>(eng->mma_ktmax, (uint32_t)eng->mma_kt.size() - eng->mma_kbase[t]);
-                for (uint32_t k = 0; k < npp; ++k)
-                    for (uint32_t l = 0; l < npcp; ++l) {
-                        uint32_t dv = kMmaNone;
-                        if (l < npc) {
+                for (uint32_t k = 0; k <= npp; ++k)
+                    for (uint32_t l = 0; l < ld; ++l) {
+                        uint32_t dv = none;
+                        if (k < npp && l < npc) {
                             const uint32_t dsc = eng->udesc_d[ub + (size_t)l * npp + k];
                             dv = (dsc & kOffMask) | (((dsc >> kOffBits) & 31u) << kOffBits);
                         }
@@ -2016,11 +2081,17 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
             }
             eng->mma_kbase[eng->tmax] = (uint32_t)eng->mma_kt.size();
             eng->mma_dbase[eng->tmax] = (uint32_t)eng->mma_desc.size();
-            if (eng->mma_kt.empty()) eng->mma_kt.push_back(make_uint2(0u, 0u));
-            if (eng->mma_desc.empty()) eng->mma_desc.push_back(kMmaNone);
-            // the next year's K entries are staged through kMmaKtRegs registers
-            // a thread, and everything must fit the LDS
-            eng->mma = eng->mma_ktmax <= kMmaKtRegs * kMmaThreads && mma_lds(eng) <= 160 * 1024;
+            // (chunk reads past a year's entries are clamped into it; one
+            // chunk of slack keeps the last year's clamp in the table)
+            for (uint32_t i = 0; i < 4 * kMmaU; ++i) eng->mma_kt.push_back(make_uint2(0u, 0u));
+            if (eng->mma_desc.empty()) eng->mma_desc.push_back(none);
+            // three years' K entries staged in LDS (through kMmaKtRegs
+            // registers a thread) where they fit, else read from HBM (KG);
+            // 256-state years always read them from HBM
+            const size_t lmax = device_lds_max();
+            eng->mma_kg = npm > 128 || eng->mma_ktmax > kMmaKtRegs * kMmaThreads || mma_lds(eng) > lmax;
+            if (const char *kv = eng->opts.get("MDP_WIDE_MMA_KG"); kv && atoi(kv) != 0) eng->mma_kg = true;
+            eng->mma = mma_lds(eng) <= lmax && none <= kOffMask;
         }
     }
     return MDP_OK;
@@ -2409,8 +2480,7 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
                  (rc = dev_upload(&d.mma_desc, eng->mma_desc)) || (rc = dev_upload(&d.mma_dbase, eng->mma_dbase))))
                 return rc;
             if (eng->mma)
-                HIP_TRY(hipFuncSetAttribute(eng->mma_npm == 64 ? (const void *)k_fwd_mma<64> : (const void *)k_fwd_mma<128>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)mma_lds(eng)));
+                HIP_TRY(hipFuncSetAttribute(mma_kernel(eng), hipFuncAttributeMaxDynamicSharedMemorySize, (int)mma_lds(eng)));
             HIP_TRY(hipFuncSetAttribute((const void *)k_fwd_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)wide_lds(eng)));
             return MDP_OK;
@@ -2757,14 +2827,19 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
         uint32_t se = os.se, sc = os.sc;
         for (uint32_t c0 = 0; c0 < d.nc; c0 += 65535) {
             const uint32_t n = std::min(65535u, d.nc - c0);
-            const dim3 g((d.ne + kMmaPts - 1) / kMmaPts, n);
-            note_launch(eng, "k_fwd_mma<%u>", eng->mma_npm);
-#define MDP_MMA(NPM) \
-    hipLaunchKernelGGL((k_fwd_mma<NPM>), g, dim3(kMmaThreads), mma_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.np_d, \
+            const uint32_t pts = mma_pts(eng->mma_npm);
+            const dim3 g((d.ne + pts - 1) / pts, n);
+            if (eng->mma_kg && eng->mma_npm <= 128) note_launch(eng, "k_fwd_mma<%u,kg>", eng->mma_npm);
+            else note_launch(eng, "k_fwd_mma<%u>", eng->mma_npm);
+#define MDP_MMA(NPM, KG) \
+    hipLaunchKernelGGL((k_fwd_mma<NPM, KG>), g, dim3(kMmaThreads), mma_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.np_d, \
                        d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, \
                        eng->mma_ktmax, eng->ncoef_d, out, se, sc)
-            if (eng->mma_npm == 64) MDP_MMA(64);
-            else MDP_MMA(128);
+            if (eng->mma_npm == 64 && !eng->mma_kg) MDP_MMA(64, false);
+            else if (eng->mma_npm == 64) MDP_MMA(64, true);
+            else if (eng->mma_npm == 128 && !eng->mma_kg) MDP_MMA(128, false);
+            else if (eng->mma_npm == 128) MDP_MMA(128, true);
+            else MDP_MMA(256, true);
 #undef MDP_MMA
         }
     } else {

@@ -243,19 +243,29 @@ def _wide_engine_run(model, e, c, path, monkeypatch):
     """Run on the named path and check it ran: "default" (years of 17-64
     states: the specialised kernel with its states in LDS; more: the wide
     kernels), "wide" (MDP_WIDE=1: k_witems + k_wq + the matrix-core forward
-    k_fwd_mma) or "wide-plain" (the same with k_fwd_wide, MDP_WIDE_MMA=0)."""
+    k_fwd_mma), "wide-kg" (the same with its K entries read from HBM instead
+    of staged in LDS, MDP_WIDE_MMA_KG=1) or "wide-plain" (k_fwd_wide,
+    MDP_WIDE_MMA=0)."""
     monkeypatch.delenv("MDP_WIDE", raising=False)
     monkeypatch.delenv("MDP_WIDE_MMA", raising=False)
+    monkeypatch.delenv("MDP_WIDE_MMA_KG", raising=False)
     if path.startswith("wide"):
         monkeypatch.setenv("MDP_WIDE", "1")
     if path == "wide-plain":
         monkeypatch.setenv("MDP_WIDE_MMA", "0")
+    if path == "wide-kg":
+        monkeypatch.setenv("MDP_WIDE_MMA_KG", "1")
     with mdp.Engine(model) as eng:
         got = eng.loglik_grid(e, c)
         launched, info = eng.launched(), eng.info()
     if path.startswith("wide") or model.npstates.max() > 64:
-        mma = path != "wide-plain" and model.npstates.max() <= 128
-        want = f"k_fwd_mma<{64 if model.npstates.max() <= 64 else 128}>" if mma else "k_fwd_wide"
+        npm = model.npstates.max()
+        mma = path != "wide-plain" and npm <= 256
+        want = f"k_fwd_mma<{64 if npm <= 64 else 128 if npm <= 128 else 256}" if mma else "k_fwd_wide"
+        if mma and npm <= 128:
+            want += ",kg>" if path == "wide-kg" else ">"
+        elif mma:
+            want += ">"
         assert info["variant"] >= 20000 and want in launched, launched
     else:
         assert 10000 <= info["variant"] < 20000, info
@@ -263,14 +273,16 @@ def _wide_engine_run(model, e, c, path, monkeypatch):
     return got
 
 
-@pytest.mark.parametrize("path", ["default", "wide", "wide-plain"])
-@pytest.mark.parametrize("missing", [{0: 5}, {3: 5}, {2: 6}, {4: 6}, {0: 8}, {3: 8}, {1: 5, 2: 6}, {0: 6, 4: 7}])
+@pytest.mark.parametrize("path", ["default", "wide", "wide-kg", "wide-plain"])
+@pytest.mark.parametrize("missing", [{0: 5}, {3: 5}, {2: 6}, {4: 6}, {0: 8}, {3: 8}, {1: 5, 2: 6}, {0: 6, 4: 7},
+                                     {1: 8, 2: 7}, {2: 7, 3: 8}])
 def test_wide_years_vs_oracle(missing, path, monkeypatch):
     """Years with more than 4 missing patches (> 16 states), in year 0, in
     later years, in consecutive years: the reference expands 2^k states for
     any k (main_MIDASPOM.c:225-251) and propagates them (:371-384); up to 64
     states the specialised kernel keeps them in LDS, beyond that (and forced)
-    the wide kernels run."""
+    the wide kernels run -- k_fwd_mma<64|128|256> on the matrix cores (256
+    states: 32 points a block, K entries from HBM)."""
     rng = np.random.default_rng(sum(100 * y + k for y, k in missing.items()))
     obs = _wide_obs(rng, 12, 5, missing)
     model = mdp.Model.from_obs(obs)
@@ -297,7 +309,7 @@ def test_random_wide_problems(seed, monkeypatch):
     e, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.2])))
     c, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.5])))
     ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c, threads=16)
-    for path, cb in (("default", None), ("wide", None), ("wide-plain", None), ("wide", "1")):
+    for path, cb in (("default", None), ("wide", None), ("wide-kg", None), ("wide-plain", None), ("wide", "1")):
         if cb:
             monkeypatch.setenv("MDP_WIDE_CB", cb)
         got = _wide_engine_run(model, e, c, path, monkeypatch)
@@ -343,6 +355,26 @@ def test_wide_survey_series_128_states(tmp_path, path, monkeypatch):
     ie[:4], ic[:4] = [0, 129, 0, 129], [0, 0, 69, 69]
     ref = oracle.OracleModel.load(f).loglik_points(e[ie], c[ic], threads=16)
     assert np.isfinite(ref).sum() >= 16
+    assert_loglik_close(got[ie, ic], ref)
+
+
+def test_wide_survey_series_256_states(tmp_path, monkeypatch):
+    """A 75 %-unvisited survey series (three years of 256 states, 257 024
+    uses per point): k_fwd_mma<256> (32 points a block, K entries from HBM)
+    on a 70 x 40 grid (three 32-point blocks, the last partial), sampled
+    against the oracle."""
+    cfg = dict(synth.CONFIG2, pmiss=0.75, seed=5, T=30)
+    f = synth.write(tmp_path / "wide75.txt", **cfg)
+    model = mdp.Model.load(f)
+    assert model.npstates.max() == 256
+    e, _ = mdp.grid(70)
+    c, _ = mdp.grid(40)
+    got = _wide_engine_run(model, e, c, "default", monkeypatch)
+    rng = np.random.default_rng(6)
+    ie, ic = rng.integers(0, 70, 16), rng.integers(0, 40, 16)
+    ie[:4], ic[:4] = [0, 69, 0, 69], [0, 0, 39, 39]
+    ref = oracle.OracleModel.load(f).loglik_points(e[ie], c[ic], threads=16)
+    assert np.isfinite(ref).sum() >= 10
     assert_loglik_close(got[ie, ic], ref)
 
 
