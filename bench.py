@@ -159,16 +159,25 @@ def cli_walls(cfg_inputs, tmpdir):
             # steady state after it
             env = dict(os.environ, MDP_JIT_CACHE=str(cache / name), MIDASPOM_TIMING="1",
                        **({"AMD_COMGR_CACHE": "0"} if leg == "cold" else {}))
-            t0 = time.perf_counter()
+            t0 = time.monotonic()
             r = subprocess.run([str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", str(s), "-i", str(inp),
                                 "-o", str(Path(tmpdir) / f"{name}.post")], env=env, capture_output=True, text=True)
-            out[f"{name}_cli_{leg}_s"] = time.perf_counter() - t0 if r.returncode == 0 else None
+            t1 = time.monotonic()
+            out[f"{name}_cli_{leg}_s"] = t1 - t0 if r.returncode == 0 else None
             # the CLI's own split (MIDASPOM_TIMING): parse, HIP start-up,
             # engine set-up (hipRTC), grid, Ltot, write
             for ln in r.stderr.splitlines():
                 if ln.startswith("midaspom timing (s):"):
                     v = ln.split(":", 1)[1].split()
                     out[f"{name}_cli_{leg}_split_s"] = {v[i]: float(v[i + 1]) for i in range(0, len(v) - 1, 2)}
+                # main's entry and return on this process's clock (CLOCK_MONOTONIC):
+                # the wall before main (spawn, exec, loader, library
+                # constructors) and after it (exit handlers, runtime teardown)
+                if ln.startswith("midaspom clock (s):"):
+                    v = ln.split(":", 1)[1].split()
+                    st = {v[i]: float(v[i + 1]) for i in range(0, len(v) - 1, 2)}
+                    out[f"{name}_cli_{leg}_outside_s"] = {"before_main": st["main_entry"] - t0,
+                                                          "after_main": t1 - st["main_return"]}
     orc = ROOT / "oracle" / "_build" / "orc_main"
     if orc.exists() and "config1" in cfg_inputs:
         inp, s = cfg_inputs["config1"]

@@ -175,6 +175,10 @@ int main(int argc, char **argv)
     free(grid);
     free(lik);
     mdp_model_free(model);
+    /* absolute CLOCK_MONOTONIC stamps of main's entry and return: a parent
+     * timing the process on the same clock attributes the wall outside main
+     * (exec, loader, library constructors; exit handlers, runtime teardown) */
+    if (timing) fprintf(stderr, "midaspom clock (s): main_entry %.6f main_return %.6f\n", t_start, now_s());
     if (getenv("MIDASPOM_FAST_EXIT") && atoi(getenv("MIDASPOM_FAST_EXIT")) != 0) {
         /* measurement: leave without the HIP runtime's exit-time teardown */
         fflush(stdout);

@@ -2232,6 +2232,12 @@ int jit_build(mdp_engine *eng, bool fused)
         plan.epl = epl_r;
         plan.pro = 2;
     }
+    if (fused) {  // at most 1 024 threads a workgroup: fewer prologue threads, then fewer columns
+        const int fc = std::max(1, plan.fused_cols);
+        if (plan.kblock * fc * std::max(1, plan.pro) > 1024) plan.pro = 1;
+        if (plan.kblock * fc > 1024) plan.fused_cols = std::max(1, 1024 / std::max(1, plan.kblock));
+        eng->jit_plan.fused_cols = plan.fused_cols;  // the launch's columns per workgroup
+    }
     const std::string src = mdp_jit_forward_source(plan);
     if (fused) {
         eng->jit_epl_fused = plan.epl;

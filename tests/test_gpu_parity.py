@@ -144,7 +144,8 @@ def test_q5_impossible_transition(tmp_path):
 # ---------------------------------------------------------------------------
 # fuzzing: random problems covering every forward-kernel variant
 # ---------------------------------------------------------------------------
-@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic", "wide", "wide-chunked", "wide-plain"])
+@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic", "wide", "wide-chunked", "wide-kg",
+                        "wide-plain"])
 def engine_path(request, monkeypatch):
     """Every engine path: the direct one (the hipRTC-specialised forward
     kernel; on these small grids it computes its column's Q itself), the same
@@ -152,8 +153,10 @@ def engine_path(request, monkeypatch):
     transition cache and XCD ordering off (MDP_JIT_SLOTS=0, MDP_JIT_XCD=0), and
     the generic kernels (MDP_JIT=0), and the wide path that years with more
     than 16 states need (MDP_WIDE=1: its forward on the matrix cores,
-    k_fwd_mma; chunked: one c value per item launch; plain: k_fwd_wide)."""
-    for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB", "MDP_WIDE_MMA"):
+    k_fwd_mma; chunked: one c value per item launch; kg: k_fwd_mma with its K
+    entries read from HBM; plain: k_fwd_wide)."""
+    for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB", "MDP_WIDE_MMA",
+              "MDP_WIDE_MMA_KG"):
         monkeypatch.delenv(k, raising=False)
     if request.param.startswith("wide"):
         monkeypatch.setenv("MDP_WIDE", "1")
@@ -161,6 +164,8 @@ def engine_path(request, monkeypatch):
             monkeypatch.setenv("MDP_WIDE_CB", "1")
         if request.param == "wide-plain":
             monkeypatch.setenv("MDP_WIDE_MMA", "0")
+        if request.param == "wide-kg":
+            monkeypatch.setenv("MDP_WIDE_MMA_KG", "1")
     elif request.param == "generic":
         monkeypatch.setenv("MDP_JIT", "0")
     elif request.param == "direct-qrows":
@@ -218,6 +223,25 @@ def test_random_problems(seed, engine_path):
     model = mdp.Model.from_obs(obs, m=m, p=p, d=d)
     got = gpu_grid(model, e, c)
     ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c)
+    assert_loglik_close(got, ref)
+
+
+def test_structural_zeros_exact(golden, engine_path):
+    """Structural zeros (L = 0 exactly: an impossible transition, quirk Q5;
+    the e = 0 / e >= 1 / c = 0 borders of the shipped example, where some
+    year's change has probability 0) are -inf on every path -- not a small
+    subnormal, which assert_loglik_close would let through on the underflow
+    side and which a broken zero slot or padded gather would produce."""
+    obs = np.array([[0, 1, 1, 1], [0, 0, 0, 0], [0, 1, 0, 1]])
+    g, _ = mdp.grid(5)
+    assert np.isneginf(gpu_grid(mdp.Model.from_obs(obs), g)).all()
+    g, _ = mdp.grid(9, 0.0, 1.25)
+    model = mdp.Model.load(golden / "occupancies.txt")
+    got = gpu_grid(model, g)
+    ref = oracle.OracleModel.load(golden / "occupancies.txt", 400, 0.5, 100).loglik_grid(g, g)
+    zero = np.isneginf(ref)
+    assert zero.sum() >= 9 and (ref[~zero] > -700).all()  # borders only: no underflow here
+    assert np.array_equal(np.isneginf(got), zero)
     assert_loglik_close(got, ref)
 
 
