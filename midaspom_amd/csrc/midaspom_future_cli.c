@@ -196,5 +196,12 @@ int main(int argc, char **argv)
     free(lik);
     mdp_free(pend);
     mdp_free(post);
+    /* without the HIP runtime's exit-time teardown (midaspom_cli.c);
+     * MIDASPOM_FULL_EXIT=1 returns from main instead */
+    if (!(getenv("MIDASPOM_FULL_EXIT") && atoi(getenv("MIDASPOM_FULL_EXIT")) != 0)) {
+        fflush(stdout);
+        fflush(stderr);
+        _exit(0);
+    }
     return 0;
 }

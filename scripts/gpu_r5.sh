@@ -4,6 +4,9 @@
 #   bench  : the default bench line, and `--gpus 2 --backend gloo` (two ranks
 #            bench.py starts itself, sharing the one GPU)
 #   prof   : rocprofv3 kernel stats of configs 2 and 3
+#   wide   : scripts/wide_timing.py on the 45 %, 60 % and 75 %-unvisited series
+#   pmcw   : PMC passes of the 60 % series (k_fwd_mma)
+#   diag   : phase stamps of configs 2 and 3 (libmidaspom_diag.so, `make diag`)
 # Output: gpurun_out/r5/<mode>/
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -28,5 +31,13 @@ prof)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_cfg$CFG -o run -- python3 $R/bench.py --config $CFG $ARGS --no-cpu-baseline > $O/prof_bench_cfg$CFG.json 2> $O/prof_bench_cfg$CFG.err || { echo "prof cfg$CFG failed"; tail $O/prof_bench_cfg$CFG.err; exit 1; }
     echo "prof cfg$CFG ok"
   done ;;
+wide)
+  WIDE_PATHS=wide WIDE60_PATHS=default,widekg,wideplain WIDE75_PATHS=default,wideplain timeout -k 10 500 python scripts/wide_timing.py > $O/wide_timing.jsonl 2> $O/wide_timing.err || { echo "wide timing failed"; tail $O/wide_timing.err; exit 1; }
+  cat $O/wide_timing.jsonl ;;
+pmcw)
+  bash scripts/gpu_pmc_wide.sh r5/pmcw "" default ;;
+diag)
+  timeout -k 10 300 python scripts/sweep_forward.py --configs 2,3 --diag --variants "MDP_JIT=1" --steps 30 > $O/diag.txt 2>&1 || { echo "diag failed"; tail $O/diag.txt; exit 1; }
+  cat $O/diag.txt ;;
 *) echo "mode?"; exit 2 ;;
 esac

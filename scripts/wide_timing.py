@@ -27,8 +27,8 @@ PATHS = {  # path name -> engine knobs
     "wide": {"MDP_WIDE": "1"}, "wideplain": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "0"},
     "epl2": {"MDP_VLDS_EPL": "2"}, "widekg": {"MDP_WIDE": "1", "MDP_WIDE_MMA_KG": "1"},
 }
-CASES = [(0.45, 30, 512, p) for p in os.environ.get("WIDE_PATHS", "default,nosplit,wide").split(",")]
-CASES += [(0.6, 50, 256, p) for p in os.environ.get("WIDE60_PATHS", "default").split(",")]
+CASES = [(0.45, 30, 512, p) for p in os.environ.get("WIDE_PATHS", "default,nosplit,wide").split(",") if p]
+CASES += [(0.6, 50, 256, p) for p in os.environ.get("WIDE60_PATHS", "default").split(",") if p]
 CASES += [(0.75, 30, 256, p) for p in os.environ.get("WIDE75_PATHS", "default").split(",") if p]
 for pmiss, T, s, path in CASES:
     for k in [k for k in os.environ if k.startswith("MDP_")]:
