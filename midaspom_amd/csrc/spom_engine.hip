@@ -1163,8 +1163,9 @@ template <int NPM, bool KG>  // NPM: states per year, padded (64, 128 or 256); K
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint2 *__restrict__ kt,
     const uint32_t *__restrict__ kbase, const uint32_t *__restrict__ desc, const uint32_t *__restrict__ dbase,
-    uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne, uint32_t c0, uint32_t maxA,
-    uint32_t ktmax, uint32_t zslot, double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
+    const uint2 *__restrict__ wplan, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
+    uint32_t c0, uint32_t maxA, uint32_t ktmax, uint32_t zslot, double *__restrict__ out, uint32_t ld_out,
+    uint32_t out_cs)
 {
     constexpr uint32_t PTS = mma_pts(NPM), ROWS = mma_rows(NPM), PS = mma_ps(NPM), RT = PTS / 16;
     static_assert(NPM <= (int)ROWS && NPM <= 256, "state rows");
@@ -1202,6 +1203,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         const uint2 *kl;
         const uint32_t *dt;
     };
+    // (the host's work split, mma_wave_plan: one scalar load, no divisions)
     auto plan = [&](uint32_t t) {
         Item it;
         it.npc = np[t];
@@ -1209,15 +1211,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         it.npcp = ncol * 16;
         it.nch = (kbase[t + 1] - kbase[t]) / (4 * kMmaU);
         it.nit = ncol;
-        // slices: at most 16 waves; slice 1 in the destination rows, later
-        // ones in the (ROWS - npcp) rows past them; at least two chunks each
-        const uint32_t room = 2 + (ROWS - it.npcp) / it.npcp;
-        it.S = min(min(16 / ncol, room), max(1u, it.nch / 2));
-        it.active = wv < it.nit * it.S;
-        it.item = wv % it.nit;
-        it.ks = wv / it.nit;
-        it.cb = it.nch * it.ks / it.S;
-        it.ce = it.nch * (it.ks + 1) / it.S;
+        const uint2 wp = wplan[t * 16 + wv];
+        it.cb = wp.x & 0xffffu;
+        it.ce = wp.x >> 16;
+        it.item = wp.y & 0xffu;
+        it.ks = (wp.y >> 8) & 0xffu;
+        it.S = (wp.y >> 16) & 0xffu;
+        it.active = (wp.y >> 24) != 0u;
         // descriptor rows [k][2^sh >= npcp] (row npp: the padded entries')
         it.sh = 32u - (uint32_t)__builtin_clz(it.npcp - 1u);
         it.lc4 = (it.item * 16 + col) << 2;
@@ -1247,7 +1247,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     uint2 ee[4][kMmaU];
     uint32_t dd[2][kMmaU];
     double bb[2][kMmaU];
-    auto prime = [&](const Item &it) {
+    // an item's first chunks, in two parts: the K entries and descriptors
+    // (prime_a), the first C gathers once the descriptors are in (prime_b)
+    auto prime_a = [&](const Item &it) {
 #pragma unroll
         for (uint32_t u = 0; u < kMmaU; ++u) {
             ee[0][u] = kent(it, it.cb, u);
@@ -1259,11 +1261,16 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
             dd[0][u] = dsc(it, ee[0][u]);
             dd[1][u] = dsc(it, ee[1][u]);
         }
+    };
+    auto prime_b = [&]() {
 #pragma unroll
         for (uint32_t u = 0; u < kMmaU; ++u) bb[0][u] = cval(ee[0][u], dd[0][u]);
     };
     Item cur = plan(tmax > 1 ? 1u : 0u);
-    if (tmax > 1 && cur.active) prime(cur);
+    if (tmax > 1 && cur.active) {
+        prime_a(cur);
+        prime_b();
+    }
     for (uint32_t t = 1; t < tmax; ++t) {
         // (LDS staging) year t + 2's K entries: loaded now, stored before the year's barrier
         uint2 nk[kMmaKtRegs];
@@ -1309,9 +1316,11 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
                 if (ch + 3 < cur.ce) chunk(ch + 3, std::integral_constant<uint32_t, 3>{});
             }
         // next year's first chunks in flight across this year's barriers
-        // (its K entries were staged a year ago)
+        // (its K entries were staged a year ago): descriptors now, C values
+        // after the partial sums
         const Item nxt = plan(t + 1 < tmax ? t + 1 : t);
-        if (t + 1 < tmax && nxt.active) prime(nxt);
+        const bool pnext = t + 1 < tmax && nxt.active;
+        if (pnext) prime_a(nxt);
         // the lane's accumulators: states item * 16 + kk + 4 r of point
         // h * 16 + col; slice 1 stores them in place, slice j >= 2 past row
         // npcp ((S - 2) x ncol x 16 PTS doubles at most, within the buffer)
@@ -1351,6 +1360,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
 #pragma unroll
                 for (uint32_t r = 0; r < 4; ++r) dst[(size_t)(4 * r) * PTS + h * 16] = acc[h][r];
         }
+        if (pnext) prime_b();
         if (!KG) {
             uint2 *kw = Kl + ((t + 2) % 3) * ktmax;
 #pragma unroll
@@ -1543,7 +1553,7 @@ struct DevCtx {
     double *Pg = nullptr, *V = nullptr;
     size_t cap_pg = 0, cap_v = 0;
     uint32_t *np_d = nullptr, *udesc_w = nullptr;
-    uint2 *mma_kt = nullptr;
+    uint2 *mma_kt = nullptr, *mma_wplan = nullptr;
     uint32_t *mma_kbase = nullptr, *mma_desc = nullptr, *mma_dbase = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
@@ -1668,6 +1678,7 @@ struct mdp_engine {
     bool mma = false, mma_kg = false;  // kg: K entries read from HBM, not staged in LDS
     uint32_t mma_npm = 0;
     std::vector<uint2> mma_kt;  // per year its K entries: LDS byte offsets of the W rows, m, k
+    std::vector<uint2> mma_wplan;  // per (year, wave) its work item (chunk range, column tile, slice)
     std::vector<uint32_t> mma_kbase, mma_desc, mma_dbase;
     uint32_t mma_ktmax = 16;
     uint32_t qslot_lglmax = 0;      // log2 of the widest lane segment
@@ -2081,6 +2092,23 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
             }
             eng->mma_kbase[eng->tmax] = (uint32_t)eng->mma_kt.size();
             eng->mma_dbase[eng->tmax] = (uint32_t)eng->mma_desc.size();
+            // per year and wave its work item (k_fwd_mma): column tile, K
+            // slice of S (at most 16 waves; slice 1 in the destination rows,
+            // later ones in the rows past the year's column tiles; at least
+            // two chunks each), chunk range
+            eng->mma_wplan.assign((size_t)(eng->tmax + 1) * 16, make_uint2(0u, 0u));
+            for (uint32_t t = 1; t < eng->tmax; ++t) {
+                const uint32_t ncol = (eng->np[t] + 15) / 16, npcp = ncol * 16;
+                const uint32_t nch = (eng->mma_kbase[t + 1] - eng->mma_kbase[t]) / (4 * kMmaU);
+                const uint32_t room = 2 + (mma_rows(npm) - npcp) / npcp;
+                const uint32_t S = std::min(std::min(16 / ncol, room), std::max(1u, nch / 2));
+                for (uint32_t wv = 0; wv < 16; ++wv) {
+                    const uint32_t item = wv % ncol, ks = wv / ncol;
+                    const uint32_t cb = nch * ks / S, ce = nch * (ks + 1) / S;
+                    eng->mma_wplan[(size_t)t * 16 + wv] =
+                        make_uint2(cb | ce << 16, item | ks << 8 | S << 16 | (wv < ncol * S ? 1u : 0u) << 24);
+                }
+            }
             // (chunk reads past a year's entries are clamped into it; one
             // chunk of slack keeps the last year's clamp in the table)
             for (uint32_t i = 0; i < 4 * kMmaU; ++i) eng->mma_kt.push_back(make_uint2(0u, 0u));
@@ -2483,6 +2511,7 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
             if ((rc = dev_upload(&d.np_d, eng->np)) || (rc = dev_upload(&d.udesc_w, eng->udesc_d))) return rc;
             if (eng->mma &&
                 ((rc = dev_upload(&d.mma_kt, eng->mma_kt)) || (rc = dev_upload(&d.mma_kbase, eng->mma_kbase)) ||
+                 (rc = dev_upload(&d.mma_wplan, eng->mma_wplan)) ||
                  (rc = dev_upload(&d.mma_desc, eng->mma_desc)) || (rc = dev_upload(&d.mma_dbase, eng->mma_dbase))))
                 return rc;
             if (eng->mma)
@@ -2522,7 +2551,7 @@ void free_device(DevCtx &d)
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
                     d.zs, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
                     d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot,
-                    d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase,
+                    d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -2839,7 +2868,7 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
             else note_launch(eng, "k_fwd_mma<%u>", eng->mma_npm);
 #define MDP_MMA(NPM, KG) \
     hipLaunchKernelGGL((k_fwd_mma<NPM, KG>), g, dim3(kMmaThreads), mma_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.np_d, \
-                       d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, \
+                       d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, \
                        eng->mma_ktmax, eng->ncoef_d, out, se, sc)
             if (eng->mma_npm == 64 && !eng->mma_kg) MDP_MMA(64, false);
             else if (eng->mma_npm == 64) MDP_MMA(64, true);
