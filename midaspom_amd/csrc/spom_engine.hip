@@ -1579,7 +1579,7 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
     "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_JIT_SPLIT", "MDP_JIT_ROT",
-    "MDP_WIDE_MMA", "MDP_WIDE_MMA_KG"};
+    "MDP_WIDE_MMA", "MDP_WIDE_MMA_KG", "MDP_JIT_STAGE", "MDP_JIT_ROWP"};
 const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
@@ -2218,9 +2218,11 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     const size_t kimg = pl.zpad ? std::max<size_t>(kmax, std::max<uint32_t>(8u, pl.kzmax)) : kmax;
     const size_t ct = ((size_t)pl.off_zs + kimg * nj + 127) & ~(size_t)127;
     std::vector<double> img(ct, 0.0);
-    for (uint32_t js = 0; js < nj; ++js)
+    for (uint32_t js = 0; js < nj; ++js)  // (the columns of j marked -1: pressure 1.0)
         for (uint32_t b = 0; b < eng->nvar; ++b)
-            img[(size_t)js * eng->nvar + b] = eng->Sj[(size_t)js * n + eng->var_cols[b]];
+            img[(size_t)js * eng->nvar + b] = ((eng->cj_bits[js] >> (eng->nvar - 1 - b)) & 1u)
+                                                   ? -1.0
+                                                   : eng->Sj[(size_t)js * n + eng->var_cols[b]];
     uint2 *it = (uint2 *)(img.data() + pl.off_it);
     for (uint32_t i = 0; i < eng->nitems; ++i) {
         const uint32_t r = eng->itemRow[i];
@@ -2230,6 +2232,10 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     memcpy(img.data() + pl.off_zc, zc.data(), (size_t)nj * kZTerms * sizeof(double));
     if (!eng->qitem.empty())
         memcpy(img.data() + pl.off_qi, eng->qitem.data(), eng->qitem.size() * sizeof(uint32_t));
+    {
+        const std::vector<uint32_t> rq = mdp_jit_reversed_index(pl.udesc, pl.ldQ);
+        memcpy(img.data() + pl.off_rq, rq.data(), rq.size() * sizeof(uint32_t));
+    }
     for (size_t k = 0; k < kmax; ++k)  // zs pairs (k, k+1) of a row adjacent: one ds_read_b128
         for (uint32_t js = 0; js < nj; ++js) img[pl.off_zs + ((k / 2) * nj + js) * 2 + (k & 1)] = zs[k * nj + js];
     if ((rc = dev_reserve(&d.coltab, &d.cap_coltab, ct))) return rc;
@@ -2414,7 +2420,8 @@ int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 size_t fused_lds(const mdp_engine *eng, size_t ct_len)
 {
     const size_t fc = (size_t)eng->jit_plan.fused_cols;
-    return (ct_len + 2 + fc * (eng->nj + eng->nitems + 2 * eng->ldQ)) * sizeof(double);  // + staging scratch
+    return (ct_len + 2 + fc * (eng->nj + eng->nitems + 2 * eng->ldQ) + fc * eng->nj * ((eng->nvar + 1) & ~1u)) *
+           sizeof(double);  // + staging scratch, per-row pressures
 }
 
 constexpr size_t kWidePgBytes = 256ull << 20;  // wide path: item-factor chunk
@@ -3268,6 +3275,12 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
             plan.qmaxlen = 0;
             for (size_t q = 0; q + 1 < eng->qstart.size(); ++q)
                 plan.qmaxlen = std::max(plan.qmaxlen, eng->qstart[q + 1] - eng->qstart[q]);
+            // the fused kernel's staged prologue (spom_jit.cpp StageLists)
+            plan.qstart = eng->qstart;
+            plan.qitem = eng->qitem;
+            plan.item_row = eng->itemRow;
+            if (const char *sv = eng->opts.get("MDP_JIT_STAGE")) plan.stage_frac = atof(sv);
+            if (const char *sv = eng->opts.get("MDP_JIT_ROWP")) plan.rowp = atoi(sv) != 0;
             auto even = [](size_t v) { return (uint32_t)((v + 1) & ~(size_t)1); };
             if (const char *sv = eng->opts.get("MDP_JIT_SPLIT")) plan.split_forms = atoi(sv) != 0;
             if (const char *sv = eng->opts.get("MDP_JIT_ROT")) plan.rot = atoi(sv) != 0;
@@ -3275,7 +3288,8 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
                 plan.off_it = even((size_t)eng->nj * eng->nvar);
                 plan.off_qs = even(plan.off_it + eng->nitems);
                 plan.off_qi = even(plan.off_qs + (eng->ncoef_d + 2) / 2);
-                plan.off_zc = even(plan.off_qi + (eng->qitem.size() + 1) / 2);
+                plan.off_rq = even(plan.off_qi + (eng->qitem.size() + 1) / 2);
+                plan.off_zc = even(plan.off_rq + (eng->ldQ + 1) / 2);
                 plan.off_zs = even(plan.off_zc + (size_t)eng->nj * kZTerms);
                 const size_t kmax_max = plan.kzmax;
                 plan.ct_max = (uint32_t)std::min<size_t>(((plan.off_zs + kmax_max * eng->nj) + 127) & ~(size_t)127,

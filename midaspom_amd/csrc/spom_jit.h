@@ -31,10 +31,24 @@ struct MdpJitPlan {
     // column-table layout (offsets in doubles): var-column S [nj][nvar] at 0,
     // items, qstart, qitem, the Z-row series coefficients [nj][8], then
     // zs[kmax][nj] (the explicit "large" columns)
-    uint32_t off_it = 0, off_qs = 0, off_qi = 0, off_zc = 0, off_zs = 0;
+    // ... and the reversed-copy slot of every Q-row slot (u32 [ldQ], at off_rq)
+    uint32_t off_it = 0, off_qs = 0, off_qi = 0, off_rq = 0, off_zc = 0, off_zs = 0;
     uint32_t kzmax = 0;    // zs rows compiled in (grids with |c| <= 1; larger ones use k_qrows)
     bool zpad = false;     // the fused image always holds kzmax zs rows (zero past kmax)
     uint32_t qmaxlen = 0;  // most items of one Q entry
+    // fused variant, staged prologue (PRO 2, one kernel): the Q entries first
+    // used in the forward's first years (a share stage_frac of the uses) are
+    // formed by the forward's own waves, the rest by the prologue's extra
+    // waves while the forward runs; the forward waits for them (an LDS
+    // counter) at the first year that needs them.  0: one stage.  Needs the
+    // entries' item lists (qstart / qitem, ascending j) and the items' rows.
+    double stage_frac = 0.0;
+    // fused variant: the Z phase forms each row's var-column pressures (the
+    // column-table image marks the columns of j with S = -1) and the Pc phase
+    // each item's factors from them (k_qrows' phases 1-2); false: every item
+    // forms its own pressures before the Z phase
+    bool rowp = false;
+    std::vector<uint32_t> qstart, qitem, item_row;
     uint32_t ct_max = 0;  // largest column-table image (doubles), for the register staging
     int epl = 0;                  // grid points per lane (0: 2 unless the weight table is large)
     int kblock = 256;             // threads per column (256 or 512)
@@ -93,6 +107,11 @@ struct MdpRatioWork {
     double final_pt = 0;              // prior sum, final exponent, log
 };
 MdpRatioWork mdp_jit_ratio_work(const MdpJitPlan &plan);
+
+// The slot of each Q-row slot in the reversed copy the t-form lanes read:
+// within each group (offset, nX + 1 coefficients) slot off + k holds
+// coefficient off + nX - k; slots of no group map to themselves.
+std::vector<uint32_t> mdp_jit_reversed_index(const std::vector<uint32_t> &udesc, size_t ldq);
 
 // HIP source of `mdp_fwd_jit` for this plan; sets plan.epl when it was 0.
 std::string mdp_jit_forward_source(MdpJitPlan &plan);
