@@ -1579,7 +1579,7 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
     "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_JIT_SPLIT", "MDP_JIT_ROT",
-    "MDP_WIDE_MMA", "MDP_WIDE_MMA_KG", "MDP_JIT_STAGE", "MDP_JIT_ROWP"};
+    "MDP_WIDE_MMA", "MDP_WIDE_MMA_KG"};
 const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
@@ -2420,8 +2420,7 @@ int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
 size_t fused_lds(const mdp_engine *eng, size_t ct_len)
 {
     const size_t fc = (size_t)eng->jit_plan.fused_cols;
-    return (ct_len + 2 + fc * (eng->nj + eng->nitems + 2 * eng->ldQ) + fc * eng->nj * ((eng->nvar + 1) & ~1u)) *
-           sizeof(double);  // + staging scratch, per-row pressures
+    return (ct_len + 2 + fc * (eng->nj + eng->nitems + 2 * eng->ldQ)) * sizeof(double);  // + staging scratch
 }
 
 constexpr size_t kWidePgBytes = 256ull << 20;  // wide path: item-factor chunk
@@ -3275,12 +3274,6 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
             plan.qmaxlen = 0;
             for (size_t q = 0; q + 1 < eng->qstart.size(); ++q)
                 plan.qmaxlen = std::max(plan.qmaxlen, eng->qstart[q + 1] - eng->qstart[q]);
-            // the fused kernel's staged prologue (spom_jit.cpp StageLists)
-            plan.qstart = eng->qstart;
-            plan.qitem = eng->qitem;
-            plan.item_row = eng->itemRow;
-            if (const char *sv = eng->opts.get("MDP_JIT_STAGE")) plan.stage_frac = atof(sv);
-            if (const char *sv = eng->opts.get("MDP_JIT_ROWP")) plan.rowp = atoi(sv) != 0;
             auto even = [](size_t v) { return (uint32_t)((v + 1) & ~(size_t)1); };
             if (const char *sv = eng->opts.get("MDP_JIT_SPLIT")) plan.split_forms = atoi(sv) != 0;
             if (const char *sv = eng->opts.get("MDP_JIT_ROT")) plan.rot = atoi(sv) != 0;

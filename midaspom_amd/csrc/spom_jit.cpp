@@ -369,7 +369,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
           << pl.off_rq << "\n#define OFF_ZC "
           << pl.off_zc << "\n#define OFF_ZS "
           << pl.off_zs << "\n#define KZ " << std::max<uint32_t>(8u, pl.kzmax) << "\n#define ZPAD " << (pl.zpad ? 1 : 0)
-          << "\n#define NVP " << ((pl.nvar + 1) & ~1u) << "\n#define QML "
+          << "\n#define QML "
           << std::max<uint32_t>(1u, pl.qmaxlen) << "\n#define QUN " << std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)
           << "\n#define NSTG "
           << std::max<uint32_t>(1u, (pl.ct_max / 2 + (uint32_t)(pl.kblock * pl.fused_cols * std::max(1, pl.pro)) - 1) /
@@ -385,80 +385,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     const int PRO = pl.fused && pl.pro > 1 ? pl.pro : 1;
     o << "#define FC " << FC << "\n#define SPL " << SPL << "\n#define NTF (KBLOCK * FC * SPL)\n#define NT (NTF * "
       << PRO << ")\n";
-    // Staged prologue (fused, PRO 2): group 0 (the forward's own waves,
-    // threads [0, NTF)) forms the Z rows, items and Q entries the years up to
-    // t_split use, group 1 (the extra waves) the rest, each group with its own
-    // LDS-counter barriers; the forward starts as soon as group 0's entries
-    // exist and waits for group 1's at year t_split + 1.  Rows and items that
-    // both stages use belong to group 0; group 1 waits for group 0's Z and Pc
-    // phases before reading them.  Every value is computed by the same
-    // expression as in the one-stage prologue: the same bits.
-    struct StageLists {
-        std::vector<uint32_t> rows, items, qs;
-    };
-    StageLists stg[2];
-    size_t t_split = 0;
-    bool staged = pl.fused && PRO == 2 && SPL == 1 && !pl.vlds && !gather && pl.first && pl.last &&
-                  pl.stage_frac > 0.0 && pl.qstart.size() == (size_t)pl.ncoef + 1 && pl.item_row.size() == pl.nitems &&
-                  ((pl.kblock > 0 ? pl.kblock : 256) * FC % 64) == 0;
-    if (staged) {
-        // first year using each Q slot, and the split year: the first
-        // t_split years hold at least stage_frac of the uses
-        std::vector<size_t> first(ldq_local, SIZE_MAX);
-        size_t u = 0, total = pl.udesc.size(), acc = 0;
-        for (size_t t = 1; t < pl.np.size(); ++t) {
-            const size_t n = (size_t)pl.np[t - 1] * pl.np[t];
-            for (size_t j = 0; j < n; ++j, ++u) {
-                const uint32_t d = pl.udesc[u], off = d & ((1u << 22) - 1u), nX = (d >> 22) & 31u;
-                for (uint32_t m = 0; m <= nX && off + m < ldq_local; ++m) first[off + m] = std::min(first[off + m], t);
-            }
-            acc += n;
-            if (!t_split && (double)acc >= pl.stage_frac * (double)total) t_split = t;
-        }
-        std::vector<int> row_g(pl.nj, -1), item_g(pl.nitems, -1);
-        for (size_t q = 0; q < ldq_local; ++q) {
-            const int g = q < pl.ncoef && first[q] <= t_split ? 0 : 1;
-            stg[g].qs.push_back((uint32_t)q);
-            if (q >= pl.ncoef) continue;
-            for (uint32_t i = pl.qstart[q]; i < pl.qstart[q + 1]; ++i) {
-                const uint32_t it = pl.qitem[i];
-                if (item_g[it] < 0 || g < item_g[it]) item_g[it] = g;
-            }
-        }
-        for (uint32_t it = 0; it < pl.nitems; ++it)
-            if (item_g[it] >= 0) {
-                stg[item_g[it]].items.push_back(it);
-                const uint32_t r = pl.item_row[it];
-                if (row_g[r] < 0 || item_g[it] < row_g[r]) row_g[r] = item_g[it];
-            }
-        for (uint32_t r = 0; r < pl.nj; ++r)
-            if (row_g[r] >= 0) stg[row_g[r]].rows.push_back(r);
-        staged = t_split + 1 < pl.np.size() && !stg[0].qs.empty() && !stg[1].qs.empty();
-    }
-    if (staged) {
-        o << "#define NWG (NTF / 64)\n";
-        for (int g = 0; g < 2; ++g) {
-            const std::vector<uint32_t> *ls[3] = {&stg[g].rows, &stg[g].items, &stg[g].qs};
-            const char *nm[3] = {"R", "I", "Q"};
-            for (int k = 0; k < 3; ++k) {
-                o << "#define N" << nm[k] << g << " " << ls[k]->size() << "\n__constant__ const unsigned short SL_"
-                  << nm[k] << g << "[" << std::max<size_t>(1, ls[k]->size()) << "] = {";
-                for (size_t i = 0; i < ls[k]->size(); ++i) o << (i ? (i % 32 ? "," : ",\n") : "") << (*ls[k])[i];
-                if (ls[k]->empty()) o << "0";
-                o << "};\n";
-            }
-        }
-        // a wave's arrival at a group barrier (its LDS stores complete first)
-        // and the wait for a count of arrivals
-        o << "__device__ __forceinline__ void mdp_arrive(u32 *c)\n{\n"
-             "    __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\");\n"
-             "    if ((threadIdx.x & 63u) == 0u) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
-             "}\n"
-             "__device__ __forceinline__ void mdp_wait(u32 *c, u32 v)\n{\n"
-             "    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);\n"
-             "    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"workgroup\");\n"
-             "}\n";
-    }
     {   // slot of each coefficient in the reversed copy (see the ratio forms)
         const std::vector<uint32_t> rev = reversed_index(pl.udesc, ldq_local);
         o << "__constant__ const " << (ldq_local <= 65536 ? "unsigned short" : "unsigned int") << " REVQ[" << ldq_local + 2
@@ -624,7 +550,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    __shared__ double Zl[FC * NJ];\n"
              "#define PLS (NITEMS + 1)\n"  // a column's items, then its zero slot (the flat Q sums' padding)
              "    __shared__ double Pl[FC * PLS];\n"
-          << (staged ? "    __shared__ u32 msync[2];\n    if (threadIdx.x < 2) msync[threadIdx.x] = 0u;\n" : "") <<
+          <<
              "    const uint2 *Itl = (const uint2 *)(ct + OFF_IT);\n"
              "    const u32 *Qsl = (const u32 *)(ct + OFF_QS);\n"
              "    const u32 *Qil = (const u32 *)(ct + OFF_QI);\n"
@@ -657,266 +583,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    }\n"
              "    __syncthreads();\n"
           << stamp(4);
-        if (staged) {
-            // the two groups' prologues (see StageLists): per group g its
-            // items' F and Z slots and its entries' item lists before its Z
-            // rows, then Pc, then the Q sums, each phase closed by the group's
-            // own barrier (an LDS counter, NWG waves a group)
-            auto group = [&](int g) {
-                const std::string G = std::to_string(g), cnt = "&msync[" + G + "]";
-                std::ostringstream w;
-                w << "        const u32 gt = threadIdx.x - " << g << "u * NTF;\n"
-                     "        constexpr int KPC = (FC * NI" << G << " + NTF - 1) / NTF;\n"
-                     "        constexpr int KQ = (FC * NQ" << G << " + NTF - 1) / NTF;\n"
-                     "        constexpr int KZR = (FC * NR" << G << " + NTF - 1) / NTF;\n"
-                     "        double Fp[KPC > 0 ? KPC : 1];\n"
-                     "        u32 zi[KPC > 0 ? KPC : 1], pi[KPC > 0 ? KPC : 1];\n"
-                     "#pragma unroll\n"
-                     "        for (int k = 0; k < KPC; ++k) {\n"
-                     "            const u32 w = k * NTF + gt;\n"
-                     "            Fp[k] = 0.0;\n"
-                     "            zi[k] = 0u;\n"
-                     "            pi[k] = ~0u;\n"
-                     "            if (w >= FC * NI" << G << ") continue;\n"
-                     "            const u32 col = w % FC, it = SL_I" << G << "[w / FC];\n"
-                     "            const double c = cc[col];\n"
-                     "            const uint2 t = Itl[it];\n"
-                     "            const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
-                     "            double f[NVAR];\n"
-                     "            const u32 nB = ~B;\n"
-                     "#pragma unroll\n"
-                     "            for (int b = 0; b < NVAR; ++b) {\n"
-                     "                const u32 bit = NVAR - 1 - b;\n"
-                     "                const double pcv = c * Svl[r * NVAR + b];\n"
-                     "                const double p = (pcv > 1.0) | ((j >> bit) & 1u) ? 1.0 : pcv;\n"
-                     "                const double sg = __hiloint2double((int)(0x3ff00000u | ((nB << (31 - bit)) & 0x80000000u)), 0);\n"
-                     "                f[b] = fma(sg, p, fma(-0.5, sg, 0.5));\n"
-                     "            }\n"
-                     "#pragma unroll\n"
-                     "            for (int s = 1; s < NVAR; s *= 2)\n"
-                     "#pragma unroll\n"
-                     "                for (int b = 0; b + s < NVAR; b += 2 * s) f[b] *= f[b + s];\n"
-                     "            Fp[k] = f[0];\n"
-                     "            zi[k] = col * NJ + r;\n"
-                     "            pi[k] = col * PLS + it;\n"
-                     "        }\n"
-                     "        u32 qb[KQ > 0 ? KQ : 1], qn[KQ > 0 ? KQ : 1], qx[KQ > 0 ? KQ : 1][QUN], qw[KQ > 0 ? KQ : 1];\n"
-                     "#pragma unroll\n"
-                     "        for (int k = 0; k < KQ; ++k) {\n"
-                     "            const u32 w = k * NTF + gt;\n"
-                     "            const bool in = w < FC * NQ" << G << ";\n"
-                     "            const u32 col = w % FC, q = in ? SL_Q" << G << "[w / FC] : 0u;\n"
-                     "            const bool live = in && q < NCOEF;\n"
-                     "            const u32 q0 = live ? Qsl[q] : 0u, q1 = live ? Qsl[q + 1] : 0u;\n"
-                     "            qb[k] = q0;\n"
-                     "            qn[k] = q1 - q0;\n"
-                     "            qw[k] = in ? col * LDQ + q : ~0u;\n"
-                     "#pragma unroll\n"
-                     "            for (int u = 0; u < QUN; ++u) { const u32 t_ = Qil[q0 + u]; qx[k][u] = (u32)u < qn[k] ? t_ : (u32)NITEMS; }\n"
-                     "        }\n"
-                     "#pragma unroll\n"
-                     "        for (int k = 0; k < KZR; ++k) {\n"
-                     "            const u32 w = k * NTF + gt;\n"
-                     "            if (w < FC * NR" << G << ") {\n"
-                     "                const u32 col = w % FC, r = SL_R" << G << "[w / FC];\n"
-                     "                const double c = cc[col];\n"
-                     "                double sk[KZ];\n"
-                     "#pragma unroll\n"
-                     "                for (u32 kk = 0; kk < KZ; kk += 2) {\n"
-                     "                    const double2 t2 = ((const double2 *)zl)[(ZPAD || kk < kmax ? kk : kk % 8u) / 2 * NJ + r];\n"
-                     "                    sk[kk] = t2.x;\n"
-                     "                    sk[kk + 1] = t2.y;\n"
-                     "                }\n"
-                     "                double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
-                     "#pragma unroll\n"
-                     "                for (u32 kk = 0; kk < KZ; kk += 8) {\n"
-                     "                    const bool in = ZPAD || kk < kmax;\n"
-                     "#pragma unroll\n"
-                     "                    for (int u = 0; u < 8; ++u) sk[kk + u] = in ? sk[kk + u] : 0.0;\n"
-                     "                    za *= fma(-c, sk[kk + 0], 1.0) * fma(-c, sk[kk + 4], 1.0);\n"
-                     "                    zb *= fma(-c, sk[kk + 1], 1.0) * fma(-c, sk[kk + 5], 1.0);\n"
-                     "                    zc *= fma(-c, sk[kk + 2], 1.0) * fma(-c, sk[kk + 6], 1.0);\n"
-                     "                    zd *= fma(-c, sk[kk + 3], 1.0) * fma(-c, sk[kk + 7], 1.0);\n"
-                     "                }\n"
-                     "                double z = (za * zb) * (zc * zd);\n"
-                     "                if (kmax && !(fma(-c, sk[0], 1.0) > 0.0)) z = 0.0;\n"
-                     "                {\n"
-                     "                    const double2 *zq = (const double2 *)(zcl + r * 8);\n"
-                     "                    const double2 p01 = zq[0], p23 = zq[1], p45 = zq[2], p67 = zq[3];\n"
-                     "                    double q = p67.y;\n"
-                     "                    q = fma(q, c, p67.x);\n"
-                     "                    q = fma(q, c, p45.y);\n"
-                     "                    q = fma(q, c, p45.x);\n"
-                     "                    q = fma(q, c, p23.y);\n"
-                     "                    q = fma(q, c, p23.x);\n"
-                     "                    q = fma(q, c, p01.y);\n"
-                     "                    q = fma(q, c, p01.x);\n"
-                     "                    z *= exp(-(q * c));\n"
-                     "                }\n"
-                     "                Zl[col * NJ + r] = z;\n"
-                     "            }\n"
-                     "        }\n"
-                     "        mdp_arrive(" << cnt << ");\n"
-                     "        mdp_wait(" << cnt << ", NWG);\n"
-                  << (g ? "        mdp_wait(&msync[0], NWG);\n" : stamp(5)) <<  // group 0's Z rows
-                     "#pragma unroll\n"
-                     "        for (int k = 0; k < KPC; ++k)\n"
-                     "            if (pi[k] != ~0u) Pl[pi[k]] = Zl[zi[k]] * Fp[k];\n"
-                  << (g ? "" : "        if (gt < FC) Pl[gt * PLS + NITEMS] = 0.0;\n") <<
-                     "        mdp_arrive(" << cnt << ");\n"
-                     "        mdp_wait(" << cnt << ", 2 * NWG);\n"
-                  << (g ? "        mdp_wait(&msync[0], 2 * NWG);\n" : stamp(1)) <<  // group 0's items and zero slots
-                     "#pragma unroll\n"
-                     "        for (int k = 0; k < KQ; ++k) {\n"
-                     "            if (qw[k] != ~0u) {\n"
-                     "                const double *pl = Pl + (qw[k] / LDQ) * PLS;\n"
-                  << qsum_flat_code(std::max<uint32_t>(1u, pl.qmaxlen), std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)) <<
-                     "                Ql[qw[k]] = a;\n"
-                     "                Ql[FC * LDQ + (qw[k] / LDQ) * LDQ + Rql[qw[k] % LDQ]] = a;\n"
-                     "            }\n"
-                     "        }\n"
-                     "        mdp_arrive(" << cnt << ");\n";
-                return w.str();
-            };
-            o << "    if (threadIdx.x < NTF) {\n" << group(0) << "        mdp_wait(&msync[0], 3 * NWG);\n"
-              << "    } else {\n" << group(1) << "        return;\n    }\n";
-        } else if (pl.rowp) {
-            // Per-row pressures: the Z phase also forms each (column, row)'s
-            // var-column pressures p_b = min(1, c S[j][b]) (exactly 1.0 for
-            // the columns of j, marked -1 in the image) -- k_qrows' phase 1 --
-            // and the Pc phase folds each item's factors fma(s_b, p_b, n_b),
-            // (s_b, n_b) = (1, 0) where B_b, (-1, 1) where not, from them: the
-            // pressures are formed once per row instead of once per item (3.7
-            // items a row on config 2), and the items' work leaves the Z phase
-            o << "    __shared__ __attribute__((aligned(16))) double Prl[FC * NJ * NVP];\n"
-                 "    constexpr int KPC = (FC * NITEMS + NT - 1) / NT;\n"
-                 "    constexpr int KQ = (FC * LDQ + NT - 1) / NT;\n"
-                 "#define ITEM_W(k) ((k) * NT + threadIdx.x)\n"
-                 // Z rows from the last thread down: the waves that form them
-                 // are not the ones reading the Q entries' item lists
-                 "#define ZW(k) ((k) * NT + (NT - 1 - threadIdx.x))\n#define QW(k) ((k) * NT + threadIdx.x)\n"
-                 "    u32 zi[KPC], nBk[KPC];\n"
-                 "#pragma unroll\n"
-                 "    for (int k = 0; k < KPC; ++k) {\n"
-                 "        const u32 w = ITEM_W(k);\n"
-                 "        zi[k] = ~0u;\n"
-                 "        nBk[k] = 0u;\n"
-                 "        if (w >= FC * NITEMS) continue;\n"
-                 "        const u32 col = w % FC, it = w / FC;\n"
-                 "        const uint2 t = Itl[it];\n"
-                 "        zi[k] = col * NJ + ((t.x >> 24) | ((t.y >> 24) << 8));\n"
-                 "        nBk[k] = ~(t.x & 0xffffffu);\n"
-                 "    }\n"
-                 "    u32 qb[KQ], qn[KQ], qx[KQ][QUN];\n"
-                 "#pragma unroll\n"
-                 "    for (int k = 0; k < KQ; ++k) {\n"
-                 "        const u32 w = QW(k), q = w % LDQ;\n"
-                 "        const bool live = w < FC * LDQ && q < NCOEF;\n"
-                 "        const u32 q0 = live ? Qsl[q] : 0u, q1 = live ? Qsl[q + 1] : 0u;\n"
-                 "        qb[k] = q0;\n"
-                 "        qn[k] = q1 - q0;\n"
-                 "#pragma unroll\n"
-                 "        for (int u = 0; u < QUN; ++u) { const u32 t_ = Qil[q0 + u]; qx[k][u] = (u32)u < qn[k] ? t_ : (u32)NITEMS; }\n"
-                 "    }\n"
-                 "#pragma unroll\n"
-                 "    for (int k = 0; k < (FC * NJ + NT - 1) / NT; ++k) {\n"
-                 "        const u32 w = ZW(k);\n"
-                 "        if (w < FC * NJ) {\n"
-                 "            const u32 col = w % FC, r = w / FC;\n"
-                 "            const double c = cc[col];\n"
-                 "            double sk[KZ];\n"
-                 "#pragma unroll\n"
-                 "            for (u32 kk = 0; kk < KZ; kk += 2) {\n"
-                 "                const double2 t2 = ((const double2 *)zl)[(ZPAD || kk < kmax ? kk : kk % 8u) / 2 * NJ + r];\n"
-                 "                sk[kk] = t2.x;\n"
-                 "                sk[kk + 1] = t2.y;\n"
-                 "            }\n"
-                 "            double sb[NVP];\n"
-                 "#pragma unroll\n"
-                 "            for (int b = 0; b < NVAR; ++b) sb[b] = Svl[r * NVAR + b];\n"
-                 "            double za = 1.0, zb = 1.0, zc = 1.0, zd = 1.0;\n"
-                 "#pragma unroll\n"
-                 "            for (u32 kk = 0; kk < KZ; kk += 8) {\n"
-                 "                const bool in = ZPAD || kk < kmax;\n"
-                 "#pragma unroll\n"
-                 "                for (int u = 0; u < 8; ++u) sk[kk + u] = in ? sk[kk + u] : 0.0;\n"
-                 "                za *= fma(-c, sk[kk + 0], 1.0) * fma(-c, sk[kk + 4], 1.0);\n"
-                 "                zb *= fma(-c, sk[kk + 1], 1.0) * fma(-c, sk[kk + 5], 1.0);\n"
-                 "                zc *= fma(-c, sk[kk + 2], 1.0) * fma(-c, sk[kk + 6], 1.0);\n"
-                 "                zd *= fma(-c, sk[kk + 3], 1.0) * fma(-c, sk[kk + 7], 1.0);\n"
-                 "            }\n"
-                 "            double z = (za * zb) * (zc * zd);\n"
-                 "            if (kmax && !(fma(-c, sk[0], 1.0) > 0.0)) z = 0.0;\n"
-                 "            {\n"
-                 "                const double2 *zq = (const double2 *)(zcl + r * 8);\n"
-                 "                const double2 p01 = zq[0], p23 = zq[1], p45 = zq[2], p67 = zq[3];\n"
-                 "                double q = p67.y;\n"
-                 "                q = fma(q, c, p67.x);\n"
-                 "                q = fma(q, c, p45.y);\n"
-                 "                q = fma(q, c, p45.x);\n"
-                 "                q = fma(q, c, p23.y);\n"
-                 "                q = fma(q, c, p23.x);\n"
-                 "                q = fma(q, c, p01.y);\n"
-                 "                q = fma(q, c, p01.x);\n"
-                 "                z *= exp(-(q * c));\n"
-                 "            }\n"
-                 "            Zl[col * NJ + r] = z;\n"
-                 // min(1, c S) as the reference clamps it (:355-357): NaN stays
-                 // NaN; exactly 1.0 for the columns of j (S marked -1) and the
-                 // padded slot
-                 "            double pr[NVP];\n"
-                 "#pragma unroll\n"
-                 "            for (int b = 0; b < NVP; ++b) {\n"
-                 "                const double s_ = b < NVAR ? sb[b] : -1.0, t_ = c * s_;\n"
-                 "                pr[b] = s_ < 0.0 || t_ > 1.0 ? 1.0 : t_;\n"
-                 "            }\n"
-                 "            double2 *pd = (double2 *)(Prl + (col * NJ + r) * NVP);\n"
-                 "#pragma unroll\n"
-                 "            for (int b = 0; b < NVP / 2; ++b) pd[b] = make_double2(pr[2 * b], pr[2 * b + 1]);\n"
-                 "        }\n"
-                 "    }\n"
-                 "    __syncthreads();\n"
-              << stamp(5) <<
-                 // Pc per item: its factors from its row's pressures, the
-                 // fused kernel's pairwise tree over NVAR, times Z
-                 "#pragma unroll\n"
-                 "    for (int k = 0; k < KPC; ++k) {\n"
-                 "        const u32 w = ITEM_W(k);\n"
-                 "        if (zi[k] == ~0u) continue;\n"
-                 "        const double2 *ps = (const double2 *)(Prl + zi[k] * NVP);\n"
-                 "        double f[NVP];\n"
-                 "#pragma unroll\n"
-                 "        for (int b = 0; b < NVP / 2; ++b) {\n"
-                 "            const double2 p2 = ps[b];\n"
-                 "            f[2 * b] = p2.x;\n"
-                 "            f[2 * b + 1] = p2.y;\n"
-                 "        }\n"
-                 "#pragma unroll\n"
-                 "        for (int b = 0; b < NVAR; ++b) {\n"
-                 "            const u32 bit = NVAR - 1 - b;\n"
-                 "            const double sg = __hiloint2double((int)(0x3ff00000u | ((nBk[k] << (31 - bit)) & 0x80000000u)), 0);\n"
-                 "            f[b] = fma(sg, f[b], fma(-0.5, sg, 0.5));\n"
-                 "        }\n"
-                 "#pragma unroll\n"
-                 "        for (int s = 1; s < NVAR; s *= 2)\n"
-                 "#pragma unroll\n"
-                 "            for (int b = 0; b + s < NVAR; b += 2 * s) f[b] *= f[b + s];\n"
-                 "        Pl[(w % FC) * PLS + w / FC] = Zl[zi[k]] * f[0];\n"
-                 "    }\n"
-                 "    if (threadIdx.x < FC) Pl[threadIdx.x * PLS + NITEMS] = 0.0;\n"
-                 "    __syncthreads();\n"
-              << stamp(1) <<
-                 "#pragma unroll\n"
-                 "    for (int k = 0; k < KQ; ++k) {\n"
-                 "        const u32 w = QW(k);\n"
-                 "        if (w < FC * LDQ) {\n"
-                 "            const double *pl = Pl + (w / LDQ) * PLS;\n"
-              << qsum_flat_code(std::max<uint32_t>(1u, pl.qmaxlen), std::min<uint32_t>(std::max<uint32_t>(1u, pl.qmaxlen), 16u)) <<
-                 "            Ql[w] = a;\n"
-                 "            Ql[FC * LDQ + (w / LDQ) * LDQ + Rql[w % LDQ]] = a;\n"
-                 "        }\n"
-                 "    }\n";
-        } else
         o <<
              // operands of the Pc and Q phases that do not depend on Z, read
              // and combined before the Z phase: per item its Z slot and the
@@ -1045,13 +711,10 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    }\n";
     }
     o << wblock;
-    if (staged)  // (group 1 has left; group 0's entries are in)
-        o << stamp(2);
-    else
-        o << "    __syncthreads();\n"
-          << stamp(2)
-          // the prologue's extra threads (PRO > 1) are done: the forward runs on NTF
-          << (PRO > 1 ? "    if (threadIdx.x >= NTF) return;\n" : "");
+    o << "    __syncthreads();\n"
+      << stamp(2)
+      // the prologue's extra threads (PRO > 1) are done: the forward runs on NTF
+      << (PRO > 1 ? "    if (threadIdx.x >= NTF) return;\n" : "");
     // H for point i: the Horner chain of a Q group (offset, nX) over the
     // lane's copy of the coefficients (stored order for s-form lanes,
     // reversed for t-form ones).  Transitions of one group (same A & B and B)
@@ -1190,10 +853,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
     size_t u = 0;
     for (size_t t = 1; t < pl.np.size(); ++t) {
         const uint32_t npp = pl.np[t - 1], npc = pl.np[t];
-        if (staged && t == t_split + 1) {  // the second stage's Q entries
-            o << "    }}\n    mdp_wait(&msync[1], 3 * NWG);\n" << guard;
-            since = 0;
-        }
         if (npp == 1 && npc == 1 && !pl.vlds) {
             std::string pre;
             const std::string e = use_expr(u++, pre);

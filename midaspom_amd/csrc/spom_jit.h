@@ -36,19 +36,6 @@ struct MdpJitPlan {
     uint32_t kzmax = 0;    // zs rows compiled in (grids with |c| <= 1; larger ones use k_qrows)
     bool zpad = false;     // the fused image always holds kzmax zs rows (zero past kmax)
     uint32_t qmaxlen = 0;  // most items of one Q entry
-    // fused variant, staged prologue (PRO 2, one kernel): the Q entries first
-    // used in the forward's first years (a share stage_frac of the uses) are
-    // formed by the forward's own waves, the rest by the prologue's extra
-    // waves while the forward runs; the forward waits for them (an LDS
-    // counter) at the first year that needs them.  0: one stage.  Needs the
-    // entries' item lists (qstart / qitem, ascending j) and the items' rows.
-    double stage_frac = 0.0;
-    // fused variant: the Z phase forms each row's var-column pressures (the
-    // column-table image marks the columns of j with S = -1) and the Pc phase
-    // each item's factors from them (k_qrows' phases 1-2); false: every item
-    // forms its own pressures before the Z phase
-    bool rowp = false;
-    std::vector<uint32_t> qstart, qitem, item_row;
     uint32_t ct_max = 0;  // largest column-table image (doubles), for the register staging
     int epl = 0;                  // grid points per lane (0: 2 unless the weight table is large)
     int kblock = 256;             // threads per column (256 or 512)

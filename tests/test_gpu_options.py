@@ -46,10 +46,6 @@ VARIANTS = [
     ("MDP_QROWS_XCD=0", "tall"),
     ("MDP_JIT_SPLIT=0", "cfg2"),
     ("MDP_JIT_ROT=0", "cfg2"),
-    ("MDP_JIT_STAGE=0.3", "cfg2"),
-    ("MDP_JIT_STAGE=0.6", "cfg1"),
-    ("MDP_JIT_ROWP=1", "cfg2"),
-    ("MDP_JIT_ROWP=1", "cfg1"),
     ("MDP_FAST_LOG=0", "cfg1"),
     ("MDP_JIT=0", "cfg2"),
     ("MDP_JIT=0;MDP_FWD=scalar", "cfg1"),
