@@ -2415,13 +2415,6 @@ int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
     return MDP_OK;
 }
 
-// The fused kernel's column-table capacity (g_ct, doubles; the kernel
-// stages all of it: CT_CAP in spom_jit.cpp)
-uint32_t fused_ct_cap(const mdp_engine *eng)
-{
-    return (std::max<uint32_t>(2u, eng->jit_plan.ct_max) + 1u) & ~1u;
-}
-
 // The fused forward kernel keeps its column's tables (ct_len doubles,
 // dynamic LDS), Z, Pc and Q in LDS.
 size_t fused_lds(const mdp_engine *eng, size_t ct_len)
@@ -2606,40 +2599,6 @@ std::vector<uint32_t> point_list(const double *e, uint32_t ne, uint32_t epl)
     return pl;
 }
 
-// The fused kernel's module globals for this grid: the column tables
-// (g_ct, from the device image) and each workgroup's c values (g_cb, by
-// hardware workgroup index, in the kernel's XCD-aware block order: the
-// column group ic0 of logical block lb, spom_jit.cpp)
-int fused_globals(const mdp_engine *eng, DevCtx &d, const double *c, uint32_t nc, uint32_t ne)
-{
-    // the fused launch's e blocks per column (its own shape: launch_forward)
-    const uint32_t kb = eng->jit_kblock_fused, epl = (uint32_t)eng->jit_epl_fused;
-    const uint32_t nl = epl > 1 ? d.nlist : ne;
-    const uint32_t gy = (nl + kb * epl - 1) / (kb * epl);
-    hipModule_t m = d.jit_mod[1];
-    if (!m) return mdp_set_error(MDP_EHIP, "fused forward kernel not loaded");
-    hipDeviceptr_t gct = nullptr, gcb = nullptr;
-    size_t nct = 0, ncb_bytes = 0;
-    HIP_TRY(hipModuleGetGlobal(&gct, &nct, m, "g_ct"));
-    HIP_TRY(hipModuleGetGlobal(&gcb, &ncb_bytes, m, "g_cb"));
-    if (nct < (size_t)d.ct_len * sizeof(double))
-        return mdp_set_error(MDP_EHIP, "fused kernel's column-table global too small (%zu < %u doubles)",
-                             nct / sizeof(double), d.ct_len);
-    HIP_TRY(hipMemcpy(gct, d.coltab, (size_t)d.ct_len * sizeof(double), hipMemcpyDeviceToDevice));
-    const uint32_t fc = (uint32_t)std::max(1, eng->jit_plan.fused_cols), ncb = (nc + fc - 1) / fc;
-    const uint32_t nb = gy * ncb, full = nb & ~7u;
-    std::vector<double> cb((size_t)nb * fc, 0.0);
-    for (uint32_t b = 0; b < nb; ++b) {
-        const uint32_t lb = eng->jit_plan.xcd && b < full ? (b & 7u) * (full >> 3) + (b >> 3) : b;
-        const uint32_t ic0 = eng->jit_plan.efast ? lb / gy * fc : lb % ncb * fc;
-        for (uint32_t f = 0; f < fc; ++f) cb[(size_t)b * fc + f] = ic0 + f < nc ? c[ic0 + f] : 0.0;
-    }
-    if (cb.size() * sizeof(double) > ncb_bytes)
-        return mdp_set_error(MDP_EUNSUPPORTED, "%u fused workgroups exceed the kernel's c table", nb);
-    HIP_TRY(hipMemcpy(gcb, cb.data(), cb.size() * sizeof(double), hipMemcpyHostToDevice));
-    return MDP_OK;
-}
-
 int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const double *c,
                  uint32_t nc)
 {
@@ -2706,13 +2665,9 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         // chunked series or Q rows built in HBM
         const uint32_t nl = eng->jit_epl > 1 ? d.nlist : ne;
         const uint32_t gy = (nl + eng->jit_kblock * eng->jit_epl - 1) / (eng->jit_kblock * eng->jit_epl);
-        const uint32_t fc = (uint32_t)std::max(1, eng->jit_plan.fused_cols);
-        d.fused = eng->chunks.empty() && !eng->qglobal && !eng->jit_plan.vlds &&
-                  fused_lds(eng, fused_ct_cap(eng)) <= kFusedLdsMax && d.ct_len <= fused_ct_cap(eng) &&
-                  d.zs_kmax <= eng->jit_plan.kzmax && (size_t)gy * ((nc + fc - 1) / fc) * fc <= kMdpJitCbCap &&
-                  (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
+        d.fused = eng->chunks.empty() && !eng->qglobal && !eng->jit_plan.vlds && fused_lds(eng, d.ct_len) <= kFusedLdsMax &&
+                  d.zs_kmax <= eng->jit_plan.kzmax && (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
         if ((rc = jit_load(eng, d, d.fused))) return rc;
-        if (d.fused && (rc = fused_globals(eng, d, c, nc, ne))) return rc;
         if (!eng->chunks.empty()) {  // the state vectors handed between chunks
             d.ldv = gy * eng->jit_kblock * (uint32_t)eng->jit_epl;
             uint32_t nb = 1;  // most states at a chunk boundary
@@ -2836,7 +2791,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, OutStrid
                         eng->chunks[0].qidx.empty() ? "" : ",gather");
             return MDP_OK;
         }
-        const uint32_t dyn = d.fused ? (fused_ct_cap(eng) + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch
+        const uint32_t dyn = d.fused ? (d.ct_len + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch
         HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kb * fc * spl * pro), 1, 1, kb * fc * spl * pro, 1, 1, dyn,
                                          s, args,
                                          nullptr, t_kev.start, t_kev.stop, 0));

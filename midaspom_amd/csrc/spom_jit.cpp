@@ -395,15 +395,6 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
         for (size_t q = 0; q < all.size(); ++q) o << (q ? (q % 32 ? "," : ",\n") : "") << all[q];
         o << "};\n";
     }
-    if (pl.fused)
-        // the column tables and each workgroup's c values in module globals
-        // (written by the host per grid, mdp_jit_fused_globals): their
-        // addresses are PC-relative, so the staging loads issue at entry
-        // instead of one kernel-argument round trip later
-        o << "#define CT_CAP " << ((std::max<uint32_t>(2u, pl.ct_max) + 1) & ~1u) << "\n#define CB_CAP "
-          << kMdpJitCbCap << "\n"
-             "__device__ __attribute__((aligned(16))) double g_ct[CT_CAP];\n"
-             "__device__ double g_cb[CB_CAP];\n";
     o << "extern \"C\" __global__ __launch_bounds__(NT) "
       << (pl.wpe > 0 ? "__attribute__((amdgpu_waves_per_eu(" + std::to_string(pl.wpe) + "))) " : std::string())
       << "void mdp_fwd_jit(\n"
@@ -571,11 +562,11 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "    const double *zl = ct + OFF_ZS;\n"
              "    double cc[FC];\n"
              "#pragma unroll\n"
-             "    for (int f = 0; f < FC; ++f) cc[f] = g_cb[blockIdx.x * FC + f];\n"
+             "    for (int f = 0; f < FC; ++f) cc[f] = ic0 + f < nc ? cvals[ic0 + f] : 0.0;\n"
              "    {\n"
-             "        const double2 *src = (const double2 *)g_ct;\n"
+             "        const double2 *src = (const double2 *)coltab;\n"
              "        double2 *dst = (double2 *)ct;\n"
-             "        constexpr u32 n2 = CT_CAP / 2;\n"
+             "        const u32 n2 = ct_len / 2;\n"
              "        double2 t[NSTG];\n"
              "#pragma unroll\n"
              "        for (int k = 0; k < NSTG; ++k) {\n"

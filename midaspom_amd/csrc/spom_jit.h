@@ -71,11 +71,6 @@ struct MdpJitPlan {
     size_t ldq_row = 0;           // Q row stride when gathering (the k_qrows row)
 };
 
-// The fused kernel's module globals: g_ct (the column tables, ct_max doubles)
-// and g_cb (each workgroup's FC c values, by hardware workgroup index; at
-// most kMdpJitCbCap doubles -- larger grids run the reading variant).
-constexpr uint32_t kMdpJitCbCap = 65536;
-
 // Grid points per lane for a program of these uses (2, or 1 when the weight
 // table is large); chunks of one series share it, as they share a scratch.
 int mdp_jit_default_epl(const std::vector<uint32_t> &udesc);
