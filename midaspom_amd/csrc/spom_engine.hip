@@ -1143,14 +1143,13 @@ __global__ __launch_bounds__(kBlock) void k_wq(uint32_t c0, uint32_t nitems, con
 // partial products in the year's own destination rows, later slices in the
 // state buffer's rows past the year's column tiles; slice 0 adds them in
 // slice order (deterministic).  Each lane's K entries run three chunks ahead
-// in a ring of four register slots (loaded once: from LDS, staged two years
-// ahead, or with KG from the global table when three years do not fit), the
+// in a ring of four register slots (loaded once, straight from the table in
+// HBM: staging three years of them in LDS was 1-5 % slower), the
 // transition descriptors two and the C gathers one; the loop body is
 // unrolled four times so the slots are fixed.  The products sum in another
 // order than k_fwd_wide's (positive terms: ~1e-15 relative).
 constexpr uint32_t kMmaThreads = 1024;  // 16 waves
 constexpr uint32_t kMmaU = 2;           // K steps (of 4) per pipeline chunk: years padded to 8 entries
-constexpr uint32_t kMmaKtRegs = 4;      // K entries per thread staged per year (LDS staging: <= 4096)
 constexpr uint32_t kMmaDummy = 1u << 21; // K-entry field of the descriptor row k (bits 21-28)
 // the kernel's shape for NPM states a year (padded to 16): points per block,
 // state buffer rows (>= 128, for the slices' partial sums), power-table row
@@ -1159,7 +1158,7 @@ constexpr uint32_t mma_pts(uint32_t npm) { return npm > 128 ? 32u : 64u; }
 constexpr uint32_t mma_rows(uint32_t npm) { return npm > 128 ? npm : 128u; }
 constexpr uint32_t mma_ps(uint32_t npm) { return mma_pts(npm) + 16u; }
 typedef double mdp_d4 __attribute__((ext_vector_type(4)));
-template <int NPM, bool KG>  // NPM: states per year, padded (64, 128 or 256); KG: K entries read from HBM
+template <int NPM>  // states per year, padded (64, 128 or 256)
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint2 *__restrict__ kt,
     const uint32_t *__restrict__ kbase, const uint32_t *__restrict__ desc, const uint32_t *__restrict__ dbase,
@@ -1172,7 +1171,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     extern __shared__ __attribute__((aligned(16))) double mlds[];
     double *Va = mlds, *Vb = mlds + (size_t)ROWS * PTS;  // [state][point]
     double *xp = Vb + (size_t)ROWS * PTS, *yp = xp + (size_t)(maxA + 1) * PS;  // [r][point]
-    uint2 *Kl = (uint2 *)(yp + (size_t)(maxA + 1) * PS);  // (LDS staging) [3][ktmax]: year t's at t % 3
     const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const uint32_t p0 = blockIdx.x * PTS, ic = c0 + blockIdx.y;
     if (threadIdx.x < PTS) {
@@ -1189,10 +1187,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     }
     const uint32_t np0 = np[0];
     for (uint32_t i = threadIdx.x; i < (uint32_t)NPM * PTS; i += kMmaThreads) Va[i] = i / PTS < np0 ? 1.0 : 0.0;
-    if (!KG)
-        for (uint32_t t = 1; t < 3 && t < tmax; ++t)
-            for (uint32_t i = threadIdx.x; i < kbase[t + 1] - kbase[t]; i += kMmaThreads)
-                Kl[(t % 3) * ktmax + i] = kt[kbase[t] + i];
     __syncthreads();
     const double *q = Q + (size_t)ic * ldQ;
     const uint32_t kk = lane >> 4, col = lane & 15u;
@@ -1221,7 +1215,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         // descriptor rows [k][2^sh >= npcp] (row npp: the padded entries')
         it.sh = 32u - (uint32_t)__builtin_clz(it.npcp - 1u);
         it.lc4 = (it.item * 16 + col) << 2;
-        it.kl = KG ? kt + __builtin_amdgcn_readfirstlane(kbase[t]) : Kl + (t % 3) * ktmax;
+        it.kl = kt + __builtin_amdgcn_readfirstlane(kbase[t]);
         it.dt = desc + __builtin_amdgcn_readfirstlane(dbase[t]);
         return it;
     };
@@ -1272,15 +1266,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
         prime_b();
     }
     for (uint32_t t = 1; t < tmax; ++t) {
-        // (LDS staging) year t + 2's K entries: loaded now, stored before the year's barrier
-        uint2 nk[kMmaKtRegs];
-        const uint32_t kn0 = !KG && t + 2 < tmax ? kbase[t + 2] : 0u, kn = !KG && t + 2 < tmax ? kbase[t + 3] - kn0 : 0u;
-        if (!KG)
-#pragma unroll
-            for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
-                const uint32_t i = threadIdx.x + r * kMmaThreads;
-                nk[r] = i < kn ? kt[kn0 + i] : make_uint2(0u, 0u);
-            }
         mdp_d4 acc[RT];
 #pragma unroll
         for (uint32_t h = 0; h < RT; ++h) acc[h] = mdp_d4{0.0, 0.0, 0.0, 0.0};
@@ -1361,14 +1346,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
                 for (uint32_t r = 0; r < 4; ++r) dst[(size_t)(4 * r) * PTS + h * 16] = acc[h][r];
         }
         if (pnext) prime_b();
-        if (!KG) {
-            uint2 *kw = Kl + ((t + 2) % 3) * ktmax;
-#pragma unroll
-            for (uint32_t r = 0; r < kMmaKtRegs; ++r) {
-                const uint32_t i = threadIdx.x + r * kMmaThreads;
-                if (i < kn) kw[i] = nk[r];
-            }
-        }
         __syncthreads();
         double *tv = Va;
         Va = Vb;
@@ -1579,7 +1556,7 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
     "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_JIT_SPLIT", "MDP_JIT_ROT",
-    "MDP_WIDE_MMA", "MDP_WIDE_MMA_KG"};
+    "MDP_WIDE_MMA"};
 const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
@@ -1675,7 +1652,7 @@ struct mdp_engine {
     // k_fwd_mma (wide years on the matrix cores): per year t its K entries
     // (k | |A_k| << 8 | m << 16 | valid << 31, padded to 4) from kbase[t],
     // and the Q-row slot of each (K entry, new state l) from gbase[t]
-    bool mma = false, mma_kg = false;  // kg: K entries read from HBM, not staged in LDS
+    bool mma = false;
     uint32_t mma_npm = 0;
     std::vector<uint2> mma_kt;  // per year its K entries: LDS byte offsets of the W rows, m, k
     std::vector<uint2> mma_wplan;  // per (year, wave) its work item (chunk range, column tile, slice)
@@ -2014,15 +1991,15 @@ size_t mma_lds(const mdp_engine *eng)
 {
     const uint32_t npm = eng->mma_npm;
     return (2 * (size_t)mma_rows(npm) * mma_pts(npm) + 2 * ((size_t)eng->maxA + 1) * mma_ps(npm)) * sizeof(double) +
-           (eng->mma_kg ? 0 : 3 * (size_t)eng->mma_ktmax * sizeof(uint2));
+           0;
 }
 
 // the k_fwd_mma instantiation of the engine's plan
 const void *mma_kernel(const mdp_engine *eng)
 {
-    if (eng->mma_npm == 64) return eng->mma_kg ? (const void *)k_fwd_mma<64, true> : (const void *)k_fwd_mma<64, false>;
-    if (eng->mma_npm == 128) return eng->mma_kg ? (const void *)k_fwd_mma<128, true> : (const void *)k_fwd_mma<128, false>;
-    return (const void *)k_fwd_mma<256, true>;
+    if (eng->mma_npm == 64) return (const void *)k_fwd_mma<64>;
+    if (eng->mma_npm == 128) return (const void *)k_fwd_mma<128>;
+    return (const void *)k_fwd_mma<256>;
 }
 
 // the device's LDS per workgroup (the current device; 160 KiB on gfx950)
@@ -2051,7 +2028,6 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
     // transition descriptors [k][2^sh >= npcp] (Q-row offset | nX << kOffBits;
     // an absent transition names the zero slot with nX = 0)
     eng->mma = false;
-    eng->mma_kg = false;
     if (eng->npmax <= 256 && eng->maxA <= 24) {
         const char *mv = eng->opts.get("MDP_WIDE_MMA");
         if (!mv || atoi(mv) != 0) {
@@ -2113,12 +2089,7 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
             // chunk of slack keeps the last year's clamp in the table)
             for (uint32_t i = 0; i < 4 * kMmaU; ++i) eng->mma_kt.push_back(make_uint2(0u, 0u));
             if (eng->mma_desc.empty()) eng->mma_desc.push_back(none);
-            // three years' K entries staged in LDS (through kMmaKtRegs
-            // registers a thread) where they fit, else read from HBM (KG);
-            // 256-state years always read them from HBM
             const size_t lmax = device_lds_max();
-            eng->mma_kg = npm > 128 || eng->mma_ktmax > kMmaKtRegs * kMmaThreads || mma_lds(eng) > lmax;
-            if (const char *kv = eng->opts.get("MDP_WIDE_MMA_KG"); kv && atoi(kv) != 0) eng->mma_kg = true;
             eng->mma = mma_lds(eng) <= lmax && none <= kOffMask;
         }
     }
@@ -2870,17 +2841,14 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
             const uint32_t n = std::min(65535u, d.nc - c0);
             const uint32_t pts = mma_pts(eng->mma_npm);
             const dim3 g((d.ne + pts - 1) / pts, n);
-            if (eng->mma_kg && eng->mma_npm <= 128) note_launch(eng, "k_fwd_mma<%u,kg>", eng->mma_npm);
-            else note_launch(eng, "k_fwd_mma<%u>", eng->mma_npm);
-#define MDP_MMA(NPM, KG) \
-    hipLaunchKernelGGL((k_fwd_mma<NPM, KG>), g, dim3(kMmaThreads), mma_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.np_d, \
+            note_launch(eng, "k_fwd_mma<%u>", eng->mma_npm);
+#define MDP_MMA(NPM) \
+    hipLaunchKernelGGL((k_fwd_mma<NPM>), g, dim3(kMmaThreads), mma_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, d.np_d, \
                        d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan, eng->tmax, eng->prior0, d.e, d.ne, c0, eng->maxA, \
                        eng->mma_ktmax, eng->ncoef_d, out, se, sc)
-            if (eng->mma_npm == 64 && !eng->mma_kg) MDP_MMA(64, false);
-            else if (eng->mma_npm == 64) MDP_MMA(64, true);
-            else if (eng->mma_npm == 128 && !eng->mma_kg) MDP_MMA(128, false);
-            else if (eng->mma_npm == 128) MDP_MMA(128, true);
-            else MDP_MMA(256, true);
+            if (eng->mma_npm == 64) MDP_MMA(64);
+            else if (eng->mma_npm == 128) MDP_MMA(128);
+            else MDP_MMA(256);
 #undef MDP_MMA
         }
     } else {

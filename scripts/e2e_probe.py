@@ -1,8 +1,10 @@
-"""Where the config-1 drop-in CLI's wall goes (GPU box): the bare HIP floor
-(scripts/ubench/hipinit_probe: device count, a context, normal exit or
-_exit), then the CLI cold (empty hipRTC cache) once and warm 5 times, with
-the CLI's own split (MIDASPOM_TIMING=1), normally and with
-MIDASPOM_FAST_EXIT=1 (no exit-time runtime teardown).  One JSON line."""
+"""Where the drop-in CLI's wall goes (GPU box): configs 1 (s = 50) and 2
+(s = 512) interleaved, warm (a filled code-object cache), each run timed
+from spawn to exit on CLOCK_MONOTONIC beside the CLI's own split
+(MIDASPOM_TIMING=1: parse, HIP start-up, set-up, grid, Ltot, write) and its
+main entry / return stamps -- the wall before main (exec, loader, library
+constructors) and after it (exit) -- with the default quick exit and with
+MIDASPOM_FULL_EXIT=1 (the HIP runtime's exit-time teardown).  One JSON line."""
 import json
 import os
 import subprocess
@@ -13,33 +15,39 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
-from midaspom_amd import _lib  # noqa: E402
+from midaspom_amd import _lib, synth  # noqa: E402
 
 tmp = Path(tempfile.mkdtemp())
-inp = ROOT / "tests" / "golden" / "occupancies.txt"
-s = int(sys.argv[1]) if len(sys.argv) > 1 else 50
-res = {"s": s}
+inputs = {"config1": (ROOT / "tests" / "golden" / "occupancies.txt", 50),
+          "config2": (synth.write(tmp / "c2.txt", **synth.CONFIG2), 512)}
+env = dict(os.environ, MDP_JIT_CACHE=str(tmp / "jit"), MIDASPOM_TIMING="1")
 
 
-def run(cmd, env):
-    t0 = time.perf_counter()
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True)
-    w = time.perf_counter() - t0
+def run(name, extra):
+    inp, s = inputs[name]
+    cmd = [str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", str(s), "-i", str(inp), "-o", str(tmp / "p.txt")]
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, env=dict(env, **extra), capture_output=True, text=True)
+    t1 = time.monotonic()
     assert r.returncode == 0, r.stderr[-800:]
-    split = None
+    out = {"wall": round(t1 - t0, 4)}
     for ln in r.stderr.splitlines():
-        if ln.startswith("midaspom timing (s):") or ln.startswith("hipinit_probe:"):
-            split = ln.split(":", 1)[1].strip()
-    return round(w, 4), split
+        if ln.startswith("midaspom timing (s):"):
+            v = ln.split(":", 1)[1].split()
+            out["split"] = {v[i]: float(v[i + 1]) for i in range(0, len(v) - 1, 2)}
+        if ln.startswith("midaspom clock (s):"):
+            v = ln.split(":", 1)[1].split()
+            st = {v[i]: float(v[i + 1]) for i in range(0, len(v) - 1, 2)}
+            out["before_main"] = round(st["main_entry"] - t0, 4)
+            out["after_main"] = round(t1 - st["main_return"], 4)
+    return out
 
 
-probe = str(ROOT / "scripts" / "ubench" / "hipinit_probe")
-for args in ([], ["fast"], ["ctx"], ["ctx", "fast"]):
-    res["probe_" + ("_".join(args) or "plain")] = [run([probe] + args, dict(os.environ)) for _ in range(3)]
-cmd = [str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", str(s), "-i", str(inp), "-o", str(tmp / "p.txt")]
-cache = tmp / "jit"
-env = dict(os.environ, MDP_JIT_CACHE=str(cache), MIDASPOM_TIMING="1")
-res["cold"] = run(cmd, dict(env, AMD_COMGR_CACHE="0"))
-res["warm"] = [run(cmd, env) for _ in range(5)]
-res["warm_fast_exit"] = [run(cmd, dict(env, MIDASPOM_FAST_EXIT="1")) for _ in range(5)]
+res = {}
+for name in ("config1", "config2"):  # fill the caches
+    run(name, {})
+for rep in range(3):
+    for name in ("config1", "config2"):
+        for mode, extra in (("quick", {}), ("full", {"MIDASPOM_FULL_EXIT": "1"})):
+            res.setdefault(f"{name}_{mode}", []).append(run(name, extra))
 print(json.dumps(res))

@@ -35,7 +35,7 @@ widetest)
   timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_highvar.py tests/test_gpu_options.py tests/test_gpu_layout.py -m gpu -x -q -k "wide or WIDE or structural" --timeout 180 --timeout-method thread -p no:cacheprovider > $O/pytest_wide.log 2>&1
   rc=$?; tail -3 $O/pytest_wide.log; [ $rc -eq 0 ] || exit $rc ;;
 wide)
-  WIDE_PATHS=wide WIDE60_PATHS=default,widekg,wideplain WIDE75_PATHS=default,wideplain timeout -k 10 500 python scripts/wide_timing.py > $O/wide_timing.jsonl 2> $O/wide_timing.err || { echo "wide timing failed"; tail $O/wide_timing.err; exit 1; }
+  WIDE_PATHS=wide WIDE60_PATHS=default,wideplain WIDE75_PATHS=default,wideplain timeout -k 10 500 python scripts/wide_timing.py > $O/wide_timing.jsonl 2> $O/wide_timing.err || { echo "wide timing failed"; tail $O/wide_timing.err; exit 1; }
   cat $O/wide_timing.jsonl ;;
 pmcw)
   bash scripts/gpu_pmc_wide.sh r5/pmcw "" default ;;

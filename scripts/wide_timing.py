@@ -25,7 +25,7 @@ tmp = Path(tempfile.mkdtemp())
 PATHS = {  # path name -> engine knobs
     "default": {}, "nosplit": {"MDP_VSPLIT": "1"}, "split2": {"MDP_VSPLIT": "2"}, "split4": {"MDP_VSPLIT": "4"},
     "wide": {"MDP_WIDE": "1"}, "wideplain": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "0"},
-    "epl2": {"MDP_VLDS_EPL": "2"}, "widekg": {"MDP_WIDE": "1", "MDP_WIDE_MMA_KG": "1"},
+    "epl2": {"MDP_VLDS_EPL": "2"},
 }
 CASES = [(0.45, 30, 512, p) for p in os.environ.get("WIDE_PATHS", "default,nosplit,wide").split(",") if p]
 CASES += [(0.6, 50, 256, p) for p in os.environ.get("WIDE60_PATHS", "default").split(",") if p]

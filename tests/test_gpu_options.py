@@ -55,7 +55,6 @@ VARIANTS = [
     ("MDP_WIDE=1", "cfg1"),
     ("MDP_WIDE=1;MDP_WIDE_CB=3", "cfg1"),
     ("MDP_WIDE=1;MDP_WIDE_MMA=0", "cfg2"),
-    ("MDP_WIDE=1;MDP_WIDE_MMA_KG=1", "cfg2"),
     ("MDP_VSPLIT=1", "wide45"),
     ("MDP_VSPLIT=2", "wide45"),
     ("MDP_VLDS_EPL=2", "wide45"),

@@ -144,8 +144,7 @@ def test_q5_impossible_transition(tmp_path):
 # ---------------------------------------------------------------------------
 # fuzzing: random problems covering every forward-kernel variant
 # ---------------------------------------------------------------------------
-@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic", "wide", "wide-chunked", "wide-kg",
-                        "wide-plain"])
+@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic", "wide", "wide-chunked", "wide-plain"])
 def engine_path(request, monkeypatch):
     """Every engine path: the direct one (the hipRTC-specialised forward
     kernel; on these small grids it computes its column's Q itself), the same
@@ -153,10 +152,8 @@ def engine_path(request, monkeypatch):
     transition cache and XCD ordering off (MDP_JIT_SLOTS=0, MDP_JIT_XCD=0), and
     the generic kernels (MDP_JIT=0), and the wide path that years with more
     than 16 states need (MDP_WIDE=1: its forward on the matrix cores,
-    k_fwd_mma; chunked: one c value per item launch; kg: k_fwd_mma with its K
-    entries read from HBM; plain: k_fwd_wide)."""
-    for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB", "MDP_WIDE_MMA",
-              "MDP_WIDE_MMA_KG"):
+    k_fwd_mma; chunked: one c value per item launch; plain: k_fwd_wide)."""
+    for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB", "MDP_WIDE_MMA"):
         monkeypatch.delenv(k, raising=False)
     if request.param.startswith("wide"):
         monkeypatch.setenv("MDP_WIDE", "1")
@@ -164,8 +161,6 @@ def engine_path(request, monkeypatch):
             monkeypatch.setenv("MDP_WIDE_CB", "1")
         if request.param == "wide-plain":
             monkeypatch.setenv("MDP_WIDE_MMA", "0")
-        if request.param == "wide-kg":
-            monkeypatch.setenv("MDP_WIDE_MMA_KG", "1")
     elif request.param == "generic":
         monkeypatch.setenv("MDP_JIT", "0")
     elif request.param == "direct-qrows":
@@ -267,18 +262,13 @@ def _wide_engine_run(model, e, c, path, monkeypatch):
     """Run on the named path and check it ran: "default" (years of 17-64
     states: the specialised kernel with its states in LDS; more: the wide
     kernels), "wide" (MDP_WIDE=1: k_witems + k_wq + the matrix-core forward
-    k_fwd_mma), "wide-kg" (the same with its K entries read from HBM instead
-    of staged in LDS, MDP_WIDE_MMA_KG=1) or "wide-plain" (k_fwd_wide,
-    MDP_WIDE_MMA=0)."""
+    k_fwd_mma) or "wide-plain" (k_fwd_wide, MDP_WIDE_MMA=0)."""
     monkeypatch.delenv("MDP_WIDE", raising=False)
     monkeypatch.delenv("MDP_WIDE_MMA", raising=False)
-    monkeypatch.delenv("MDP_WIDE_MMA_KG", raising=False)
     if path.startswith("wide"):
         monkeypatch.setenv("MDP_WIDE", "1")
     if path == "wide-plain":
         monkeypatch.setenv("MDP_WIDE_MMA", "0")
-    if path == "wide-kg":
-        monkeypatch.setenv("MDP_WIDE_MMA_KG", "1")
     with mdp.Engine(model) as eng:
         got = eng.loglik_grid(e, c)
         launched, info = eng.launched(), eng.info()
@@ -286,9 +276,7 @@ def _wide_engine_run(model, e, c, path, monkeypatch):
         npm = model.npstates.max()
         mma = path != "wide-plain" and npm <= 256
         want = f"k_fwd_mma<{64 if npm <= 64 else 128 if npm <= 128 else 256}" if mma else "k_fwd_wide"
-        if mma and npm <= 128:
-            want += ",kg>" if path == "wide-kg" else ">"
-        elif mma:
+        if mma:
             want += ">"
         assert info["variant"] >= 20000 and want in launched, launched
     else:
@@ -297,7 +285,7 @@ def _wide_engine_run(model, e, c, path, monkeypatch):
     return got
 
 
-@pytest.mark.parametrize("path", ["default", "wide", "wide-kg", "wide-plain"])
+@pytest.mark.parametrize("path", ["default", "wide", "wide-plain"])
 @pytest.mark.parametrize("missing", [{0: 5}, {3: 5}, {2: 6}, {4: 6}, {0: 8}, {3: 8}, {1: 5, 2: 6}, {0: 6, 4: 7},
                                      {1: 8, 2: 7}, {2: 7, 3: 8}])
 def test_wide_years_vs_oracle(missing, path, monkeypatch):
@@ -306,7 +294,7 @@ def test_wide_years_vs_oracle(missing, path, monkeypatch):
     any k (main_MIDASPOM.c:225-251) and propagates them (:371-384); up to 64
     states the specialised kernel keeps them in LDS, beyond that (and forced)
     the wide kernels run -- k_fwd_mma<64|128|256> on the matrix cores (256
-    states: 32 points a block, K entries from HBM)."""
+    states: 32 points a block)."""
     rng = np.random.default_rng(sum(100 * y + k for y, k in missing.items()))
     obs = _wide_obs(rng, 12, 5, missing)
     model = mdp.Model.from_obs(obs)
@@ -333,7 +321,7 @@ def test_random_wide_problems(seed, monkeypatch):
     e, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.2])))
     c, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.5])))
     ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c, threads=16)
-    for path, cb in (("default", None), ("wide", None), ("wide-kg", None), ("wide-plain", None), ("wide", "1")):
+    for path, cb in (("default", None), ("wide", None), ("wide-plain", None), ("wide", "1")):
         if cb:
             monkeypatch.setenv("MDP_WIDE_CB", cb)
         got = _wide_engine_run(model, e, c, path, monkeypatch)
@@ -384,7 +372,7 @@ def test_wide_survey_series_128_states(tmp_path, path, monkeypatch):
 
 def test_wide_survey_series_256_states(tmp_path, monkeypatch):
     """A 75 %-unvisited survey series (three years of 256 states, 257 024
-    uses per point): k_fwd_mma<256> (32 points a block, K entries from HBM)
+    uses per point): k_fwd_mma<256> (32 points a block)
     on a 70 x 40 grid (three 32-point blocks, the last partial), sampled
     against the oracle."""
     cfg = dict(synth.CONFIG2, pmiss=0.75, seed=5, T=30)
