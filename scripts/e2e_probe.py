@@ -18,20 +18,35 @@ sys.path.insert(0, str(ROOT))
 from midaspom_amd import _lib, synth  # noqa: E402
 
 tmp = Path(tempfile.mkdtemp())
+c2 = synth.write(tmp / "c2.txt", **synth.CONFIG2)
 inputs = {"config1": (ROOT / "tests" / "golden" / "occupancies.txt", 50),
-          "config2": (synth.write(tmp / "c2.txt", **synth.CONFIG2), 512)}
+          "config2": (c2, 512),
+          # the same programs on the other grid size: is the exit cost the
+          # problem's or the grid's?
+          "config1_s512": (ROOT / "tests" / "golden" / "occupancies.txt", 512),
+          "config2_s50": (c2, 50)}
 env = dict(os.environ, MDP_JIT_CACHE=str(tmp / "jit"), MIDASPOM_TIMING="1")
 
 
-def run(name, extra):
+def run(name, extra, files=False):
+    """(files: stdout / stderr to files instead of pipes -- a process that
+    holds an inherited pipe open past the CLI's exit would delay a pipe's
+    EOF, not the exit)"""
     inp, s = inputs[name]
     cmd = [str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", str(s), "-i", str(inp), "-o", str(tmp / "p.txt")]
     t0 = time.monotonic()
-    r = subprocess.run(cmd, env=dict(env, **extra), capture_output=True, text=True)
-    t1 = time.monotonic()
-    assert r.returncode == 0, r.stderr[-800:]
+    if files:
+        with open(tmp / "o.txt", "w") as fo, open(tmp / "e.txt", "w") as fe:
+            rc = subprocess.run(cmd, env=dict(env, **extra), stdout=fo, stderr=fe).returncode
+        t1 = time.monotonic()
+        err = (tmp / "e.txt").read_text()
+    else:
+        r = subprocess.run(cmd, env=dict(env, **extra), capture_output=True, text=True)
+        t1 = time.monotonic()
+        rc, err = r.returncode, r.stderr
+    assert rc == 0, err[-800:]
     out = {"wall": round(t1 - t0, 4)}
-    for ln in r.stderr.splitlines():
+    for ln in err.splitlines():
         if ln.startswith("midaspom timing (s):"):
             v = ln.split(":", 1)[1].split()
             out["split"] = {v[i]: float(v[i + 1]) for i in range(0, len(v) - 1, 2)}
@@ -44,10 +59,11 @@ def run(name, extra):
 
 
 res = {}
-for name in ("config1", "config2"):  # fill the caches
+for name in inputs:  # fill the caches
     run(name, {})
 for rep in range(3):
-    for name in ("config1", "config2"):
+    for name in inputs:
         for mode, extra in (("quick", {}), ("full", {"MIDASPOM_FULL_EXIT": "1"})):
             res.setdefault(f"{name}_{mode}", []).append(run(name, extra))
+        res.setdefault(f"{name}_quick_files", []).append(run(name, {}, files=True))
 print(json.dumps(res))
