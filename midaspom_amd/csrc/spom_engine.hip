@@ -1294,12 +1294,21 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
             }
         };
         if (cur.active)
-            for (uint32_t ch = cur.cb; ch < cur.ce; ch += 4) {
+        {
+            // whole rounds of four chunks with no branch between them (a
+            // branch join made the compiler wait for every load in flight at
+            // each chunk), then the last one to three
+            uint32_t ch = cur.cb;
+            for (; ch + 4 <= cur.ce; ch += 4) {
                 chunk(ch, std::integral_constant<uint32_t, 0>{});
-                if (ch + 1 < cur.ce) chunk(ch + 1, std::integral_constant<uint32_t, 1>{});
-                if (ch + 2 < cur.ce) chunk(ch + 2, std::integral_constant<uint32_t, 2>{});
-                if (ch + 3 < cur.ce) chunk(ch + 3, std::integral_constant<uint32_t, 3>{});
+                chunk(ch + 1, std::integral_constant<uint32_t, 1>{});
+                chunk(ch + 2, std::integral_constant<uint32_t, 2>{});
+                chunk(ch + 3, std::integral_constant<uint32_t, 3>{});
             }
+            if (ch < cur.ce) chunk(ch, std::integral_constant<uint32_t, 0>{});
+            if (ch + 1 < cur.ce) chunk(ch + 1, std::integral_constant<uint32_t, 1>{});
+            if (ch + 2 < cur.ce) chunk(ch + 2, std::integral_constant<uint32_t, 2>{});
+        }
         // next year's first chunks in flight across this year's barriers
         // (its K entries were staged a year ago): descriptors now, C values
         // after the partial sums
