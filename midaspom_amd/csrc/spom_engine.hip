@@ -339,6 +339,16 @@ __global__ __launch_bounds__(kBlock) void k_zrows(const double *__restrict__ cva
 // occupied levels from the lowest up gives exactly that tree; so does a
 // butterfly of xor shuffles over an aligned power-of-two lane segment
 // holding the sums of aligned power-of-two blocks of groups (k_qrows).
+// A double from the lane DPP control CTRL names (quad_perm 0x00-0xff,
+// row_mirror 0x140, row_half_mirror 0x141): no LDS, no wait
+template <int CTRL>
+__device__ __forceinline__ double quad_dpp(double v)
+{
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
 constexpr uint32_t kQGroup = 8;  // config 3: 808 lanes, one pass of k_qrows, <= 3 shuffle levels
 constexpr int kQLevels = 24;
 constexpr uint32_t kQLanesMax = 64;  // k_qrows: lanes per entry (a power of two, <= a wave)
@@ -349,11 +359,11 @@ constexpr uint32_t kQrowsMaxC = 4;
 template <int NV, bool EXACT, int CB>  // EXACT: nvar == NV (no padded factor slots)
 __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     const double *__restrict__ cvals, uint32_t nc, uint32_t nvar, uint32_t nrows,
-    uint32_t kmax, const double *__restrict__ zsT, const double *__restrict__ zc, const double *__restrict__ sv,
+    uint32_t kmax, const double *__restrict__ zsq, const double *__restrict__ zc, const double *__restrict__ sv,
     uint32_t nitems, const uint2 *__restrict__ items, uint32_t ncoef, const uint32_t *__restrict__ qstart,
     uint32_t nqi, const uint32_t *__restrict__ qitem, double *__restrict__ Q, uint32_t ldQ,
     unsigned long long *__restrict__ stamps, uint32_t xcd, const uint2 *__restrict__ qslot, uint32_t nslot,
-    uint32_t lglmax)
+    uint32_t lglmax, const uint4 *__restrict__ qlane)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     MDP_RSTAMP(stamps, 6);
@@ -361,6 +371,14 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // phase 3's lane table does not depend on c: its first pass is loaded
     // now, its latency hidden under phases 0-2
     const uint2 sd0 = threadIdx.x < nslot ? qslot[threadIdx.x] : make_uint2(0xffffffffu, 0u);
+    // nvar <= 8: the lane's group of item indices too (qlane, at least 64
+    // lanes: the clamped index is in bounds)
+    uint4 qa0 = make_uint4(0u, 0u, 0u, 0u), qb0 = qa0;
+    if constexpr (NV == 8) {
+        const uint32_t l = min(threadIdx.x, max(nslot, 1u) - 1);
+        qa0 = qlane[2 * l];
+        qb0 = qlane[2 * l + 1];
+    }
     // XCD-aware: workgroups are dealt round-robin over the 8 XCDs, so XCD x
     // takes a contiguous eighth of the c range -- the columns the forward
     // kernel's XCD-aware order gives XCD x -- and the forward reads these Q
@@ -390,132 +408,165 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     double cv[CB];  // this workgroup's c values (the last one again past the grid: never stored)
 #pragma unroll
     for (int i = 0; i < CB; ++i) cv[i] = cvals[c0 + min((uint32_t)i, ncb - 1)];  // no load in a branch
-    // items and the Q CSR: every thread's loads of a pass in flight before
-    // its stores.  (Clamped indices and branch-free stores to a scratch slot
-    // shortened the staging, 2.3 k -> 1.8 k cycles on config 3, but phase 1
-    // as a whole went 8.7 k -> 9.3 k: its loads then queue behind the
-    // staging's.  Not kept.)
-    {
-        constexpr uint32_t kSt = 4;
-        const uint32_t nmax = max(max(nitems, ncoef + 1), nqi);
-        for (uint32_t i0 = threadIdx.x; i0 < nmax; i0 += kSt * kQrowsBlock) {
-            uint2 ti[kSt];
-            uint32_t ts[kSt], tq[kSt];
+    // 1. Z and pressures per row, one quad of lanes per row.  Lane q takes
+    // the row's product chain q (explicit columns k = q mod 4, k_zrows' chains
+    // and order) for all CB c values; the quad combines the chains as
+    // (za zb)(zc zd) (exact products commute, so every lane holds the same
+    // bits); lane q then finishes c value q (the clamp test against the row
+    // maximum, stored first; the small columns' series) and forms var columns
+    // [q NV/4, (q + 1) NV/4) of the pressures min(1, c S) of every c value
+    // (the columns of j, where sv holds -1, and padded slots select a factor
+    // of exactly 1.0 in phase 2 whatever is stored here).  Each row's tables
+    // cross the vector cache once per workgroup: threads over (row, c) read
+    // them CB times, 4x the bytes on config 3, and the cache's return rate
+    // bounded the phase.
+    const uint32_t kq = kmax / 4;  // chain length (kmax a multiple of 8)
+    constexpr uint32_t NB = NV / 4;  // var columns per lane
+    constexpr uint32_t kPre = 3;     // chain pairs loaded up front (kmax <= 24: all)
+    struct RowLd {
+        double2 t[kPre];  // the chain's first pairs
+        double2 zq2;      // the lane's two series coefficients
+        double sb[NB];    // the lane's var columns of S
+    };
+    auto rowload = [&](uint32_t w, RowLd &L) {
+        const uint32_t q = w & 3u, r = w >> 2;
+        const double2 *zr = (const double2 *)(zsq + (size_t)r * kmax + (size_t)q * kq);
 #pragma unroll
-            for (uint32_t u = 0; u < kSt; ++u) {
-                const uint32_t i = i0 + u * kQrowsBlock;
-                ti[u] = i < nitems ? items[i] : make_uint2(0u, 0u);
-                ts[u] = i <= ncoef ? qstart[i] : 0u;
-                tq[u] = i < nqi ? qitem[i] : 0u;
+        for (uint32_t u = 0; u < kPre; ++u) L.t[u] = zr[2 * u < kq ? u : 0];  // zsq padded: in bounds at kmax 0
+        L.zq2 = ((const double2 *)(zc + (size_t)r * kZTermsDev))[q];
+#pragma unroll
+        for (uint32_t i = 0; i < NB; ++i) {
+            const uint32_t b = q * NB + i;
+            const double x = sv[(size_t)r * nvar + (EXACT ? b : min(b, nvar - 1))];
+            L.sb[i] = (EXACT || b < nvar) ? x : -1.0;
+        }
+    };
+    auto rowwork = [&](uint32_t w, const RowLd &L) {
+        const uint32_t q = w & 3u, r = w >> 2;
+        const double2 *zr = (const double2 *)(zsq + (size_t)r * kmax + (size_t)q * kq);
+        double ch[CB];
+#pragma unroll
+        for (int i = 0; i < CB; ++i) ch[i] = 1.0;
+        auto pair = [&](const double2 p) {
+#pragma unroll
+            for (int i = 0; i < CB; ++i) ch[i] *= fma(-cv[i], p.x, 1.0) * fma(-cv[i], p.y, 1.0);
+        };
+#pragma unroll
+        for (uint32_t u = 0; u < kPre; ++u)
+            if (2 * u < kq) pair(L.t[u]);
+        for (uint32_t u = kPre; 2 * u < kq; u += 2) {  // longer rows (|c| > 1)
+            const double2 x = zr[u], y = 2 * u + 2 < kq ? zr[u + 1] : make_double2(0.0, 0.0);
+            pair(x);
+            if (2 * u + 2 < kq) pair(y);
+        }
+        // (za zb)(zc zd): lanes 0, 1 hold za zb, lanes 2, 3 zc zd
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+            ch[i] = ch[i] * quad_dpp<0xB1>(ch[i]);  // quad_perm [1,0,3,2]
+            ch[i] = ch[i] * quad_dpp<0x4E>(ch[i]);  // quad_perm [2,3,0,1]
+        }
+        // lane q: c value q
+        double c = cv[0], zz = ch[0];
+#pragma unroll
+        for (int i = 1; i < CB; ++i)
+            if (q == (uint32_t)i) c = cv[i], zz = ch[i];
+        const double first = quad_dpp<0x00>(L.t[0].x);  // column 0, the row maximum
+        if (kmax && !(fma(-c, first, 1.0) > 0.0)) zz = 0.0;
+        double zq[kZTermsDev];
+        zq[0] = quad_dpp<0x00>(L.zq2.x), zq[1] = quad_dpp<0x00>(L.zq2.y);
+        zq[2] = quad_dpp<0x55>(L.zq2.x), zq[3] = quad_dpp<0x55>(L.zq2.y);
+        zq[4] = quad_dpp<0xAA>(L.zq2.x), zq[5] = quad_dpp<0xAA>(L.zq2.y);
+        zq[6] = quad_dpp<0xFF>(L.zq2.x), zq[7] = quad_dpp<0xFF>(L.zq2.y);
+        zz *= zseries(zq, c);
+        if (q < (uint32_t)CB) Zl[pix(nrows, r, q)] = zz;
+        // min(1, c S) as the reference clamps it (:355-357): NaN stays NaN;
+        // exactly 1.0 for the columns of j (sv -1) and the padded slots, so
+        // that phase 2's fma(s, p, n) gives their factor 1.0 with no select
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+            double pr[NB];
+#pragma unroll
+            for (uint32_t j = 0; j < NB; ++j) {
+                const double tt = cv[i] * L.sb[j];
+                pr[j] = L.sb[j] < 0.0 || tt > 1.0 ? 1.0 : tt;
             }
+            double2 *pd = (double2 *)(Prl + (size_t)r * PRS + i * NV + q * NB);
 #pragma unroll
-            for (uint32_t u = 0; u < kSt; ++u) {
-                const uint32_t i = i0 + u * kQrowsBlock;
-                if (i < nitems) It[i] = ti[u];
+            for (uint32_t j = 0; j < NB / 2; ++j) pd[j] = make_double2(pr[2 * j], pr[2 * j + 1]);
+        }
+    };
+    // the first row's loads (index clamped: no load in a branch), then the
+    // first pass of the items and Q CSR staging, both in flight at once; the
+    // staging's stores wait until the row's work is done, so its latency
+    // hides under phase 1
+    const uint32_t nrw = nrows * 4;
+    RowLd L0;
+    rowload(min(threadIdx.x, nrw - 1), L0);
+    constexpr uint32_t kSt = 4;
+    uint2 ti[kSt];
+    uint32_t ts[kSt], tq[kSt];
+    auto stload = [&](uint32_t i0) {
+#pragma unroll
+        for (uint32_t u = 0; u < kSt; ++u) {
+            const uint32_t i = i0 + u * kQrowsBlock;
+            // clamped, not guarded: a guarded load sits in a branch, and the
+            // row's first use then waited for every staging load too
+            ti[u] = items[min(i, nitems - 1)];  // launched only with items
+            if constexpr (NV != 8) {  // nvar <= 8: phase 3 reads qlane instead
+                ts[u] = qstart[min(i, ncoef)];
+                tq[u] = nqi ? qitem[min(i, nqi - 1)] : 0u;
+            }
+        }
+    };
+    auto ststore = [&](uint32_t i0) {
+#pragma unroll
+        for (uint32_t u = 0; u < kSt; ++u) {
+            const uint32_t i = i0 + u * kQrowsBlock;
+            if (i < nitems) It[i] = ti[u];
+            if constexpr (NV != 8) {
                 if (i <= ncoef) Qs[i] = ts[u];
                 if (i < nqi) Qi[i] = tq[u];
             }
         }
+    };
+    stload(threadIdx.x);
+    if (threadIdx.x < nrw) rowwork(threadIdx.x, L0);
+    for (uint32_t w = threadIdx.x + kQrowsBlock; w < nrw; w += kQrowsBlock) {
+        RowLd L;
+        rowload(w, L);
+        rowwork(w, L);
     }
     MDP_STAMP(stamps, 4);
-    // 1. Z per (row, c): the row's explicit columns in k_zrows' four chains
-    // and order, the clamp test against the row maximum (stored first), the
-    // small columns' series; then the row's pressures min(1, c S) (the
-    // columns of j, where sv holds -1, and padded slots select a factor of
-    // exactly 1.0 in phase 2 whatever is stored here).  Measured slower and
-    // not kept (config 3, phase 1 8.7 k cycles): threads over rows with all
-    // CB c values each, so each row is read once, not CB times (9.3 k: the
-    // per-thread chains at one wave per SIMD); the series coefficients and S
-    // loaded with the first columns (9.8 k: the slowest wave later).
-    for (uint32_t w = threadIdx.x; w < nrows * CB; w += kQrowsBlock) {
-        const uint32_t cl = w % CB, r = w / CB;
-        double c = cv[0];
-#pragma unroll
-        for (int i = 1; i < CB; ++i) c = cl == (uint32_t)i ? cv[i] : c;
-        const double2 *zr = (const double2 *)(zsT + (size_t)r * kmax);
-        double za = 1.0, zb = 1.0, zcc = 1.0, zd = 1.0;
-        auto chunk = [&](const double *sk) {
-            za *= fma(-c, sk[0], 1.0) * fma(-c, sk[4], 1.0);
-            zb *= fma(-c, sk[1], 1.0) * fma(-c, sk[5], 1.0);
-            zcc *= fma(-c, sk[2], 1.0) * fma(-c, sk[6], 1.0);
-            zd *= fma(-c, sk[3], 1.0) * fma(-c, sk[7], 1.0);
-        };
-        double first = 0.0;
-        uint32_t k = 0;
-        for (; k + 16 <= kmax; k += 16) {
-            double sk[16];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const double2 t2 = zr[k / 2 + u];
-                sk[2 * u] = t2.x;
-                sk[2 * u + 1] = t2.y;
-            }
-            if (k == 0) first = sk[0];
-            chunk(sk);
-            chunk(sk + 8);
+    ststore(threadIdx.x);
+    {
+        const uint32_t nmax = NV == 8 ? nitems : max(max(nitems, ncoef + 1), nqi);
+        for (uint32_t i0 = threadIdx.x + kSt * kQrowsBlock; i0 < nmax; i0 += kSt * kQrowsBlock) {
+            stload(i0);
+            ststore(i0);
         }
-        if (k < kmax) {  // kmax is a multiple of 8
-            double sk[8];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const double2 t2 = zr[k / 2 + u];
-                sk[2 * u] = t2.x;
-                sk[2 * u + 1] = t2.y;
-            }
-            if (k == 0) first = sk[0];
-            chunk(sk);
-        }
-        double zz = (za * zb) * (zcc * zd);
-        if (kmax && !(fma(-c, first, 1.0) > 0.0)) zz = 0.0;
-        double zq[kZTermsDev];
-#pragma unroll
-        for (int i = 0; i < kZTermsDev; ++i) zq[i] = zc[(size_t)r * kZTermsDev + i];
-        zz *= zseries(zq, c);
-        Zl[pix(nrows, r, cl)] = zz;
-        // the row's pressures for this c: min(1, c S) (the columns of j, where
-        // sv holds -1, and padded slots select a factor of exactly 1.0 in
-        // phase 2 whatever is stored here)
-        double pr[NV];
-#pragma unroll
-        for (int b = 0; b < NV; ++b) {
-            // min(1, c S) as the reference clamps it (:355-357): NaN stays NaN;
-            // exactly 1.0 for the columns of j (sv -1) and the padded slots, so
-            // that phase 2's fma(s, p, n) gives their factor 1.0 with no select
-            const double sb = (EXACT || (uint32_t)b < nvar) ? sv[(size_t)r * nvar + b] : -1.0;
-            const double t = c * sb;
-            pr[b] = sb < 0.0 || t > 1.0 ? 1.0 : t;
-        }
-        double2 *pd = (double2 *)(Prl + (size_t)r * PRS + cl * NV);
-#pragma unroll
-        for (int b = 0; b < NV / 2; ++b) pd[b] = make_double2(pr[2 * b], pr[2 * b + 1]);
     }
     MDP_STAMP(stamps, 5);
     __syncthreads();
     MDP_STAMP(stamps, 1);
     // 2. Pc per item, its CB c values: Z times the product F of the
-    // var-column factors f_b = B_b ? pC_b : 1 - pC_b = fma(s_b, pC_b, n_b),
-    // (s_b, n_b) = (1, 0) or (-1, 1) from the bit (j <= B, so j's columns give
-    // pC = 1.0), in the pairwise tree over NV slots -- the fused kernel's
-    // tree over nvar (padded slots are 1.0)
+    // var-column factors f_b = B_b ? pC_b : 1 - pC_b (j <= B, so j's columns
+    // give pC = 1.0, a factor of exactly 1.0), in the pairwise tree over NV
+    // slots -- the fused kernel's tree over nvar (padded slots are 1.0).  A
+    // factor is |n_b - pC_b| with n_b = 1.0 where B_b is clear, 0.0 where set:
+    // the same bits as the fused kernel's fma(s_b, pC_b, n_b), s_b = -1 / +1
+    // (1 - p rounded once; |0 - p| = p exactly), with the bit converted once
+    // per item and the abs folded into the tree's first products.  (Building
+    // s_b and n_b as doubles cost 5 integer instructions a slot, a quarter-rate
+    // multiply among them: phase 2 is bound by VALU issue.)
     for (uint32_t it = threadIdx.x; it < nitems; it += kQrowsBlock) {
         const uint2 t = It[it];
-        const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), nB = ~t.x, J = t.y & 0xffffffu;
-        // per slot (s_b, n_b): (1, 0) where B_b, (-1, 1) where not, so f_b =
-        // fma(s_b, min(1, c S), n_b) is p or 1 - p; the columns of j and the
-        // padded slots select exactly 1.0 (a product 0 * p would turn an
-        // infinite pressure into NaN) -- the values (hence the bits) are the
-        // fused kernel's
-        // (the columns of j have B_b set, j <= B, and the padded slots are
-        // taken as set: their factor is fma(1, 1.0, 0) = 1.0 -- phase 1 stores
-        // pressure 1.0 there -- the value the select form gave)
-        double sg[NV], nb[NV];
-        (void)J;
+        const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), nB = ~t.x;
+        double nb[NV];
 #pragma unroll
         for (int b = 0; b < NV; ++b) {
             const uint32_t bit = EXACT ? (uint32_t)(NV - 1 - b) : nvar - 1 - (uint32_t)b;  // wraps past nvar
             const uint32_t nbit = !EXACT && (uint32_t)b >= nvar ? 0u : (nB >> bit) & 1u;
-            sg[b] = __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
-            nb[b] = __hiloint2double((int)(nbit * 0x3ff00000u), 0);
+            nb[b] = (double)nbit;
         }
         double zr[CB], pc[CB];
 #pragma unroll
@@ -527,11 +578,10 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
 #pragma unroll
             for (int b = 0; b < NV / 2; ++b) {
                 const double2 p2 = ps[b];
-                f[2 * b] = fma(sg[2 * b], p2.x, nb[2 * b]);
-                f[2 * b + 1] = fma(sg[2 * b + 1], p2.y, nb[2 * b + 1]);
+                f[2 * b] = fabs(nb[2 * b] - p2.x) * fabs(nb[2 * b + 1] - p2.y);
             }
 #pragma unroll
-            for (int sh = 1; sh < NV; sh *= 2)
+            for (int sh = 2; sh < NV; sh *= 2)
 #pragma unroll
                 for (int b = 0; b + sh < NV; b += 2 * sh) f[b] *= f[b + sh];
             pc[i] = zr[i] * f[0];
@@ -550,6 +600,60 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // butterfly of xor shuffles, and its first lane stores the entry.  The
     // chain per lane is a few gathers and log2 L shuffles instead of the
     // entry's whole item list (35 on config 3).
+    if constexpr (NV == 8) {
+        // nvar <= 8: one group per lane (an entry has at most C(8,4) = 70
+        // items, 9 groups), its item indices in registers since the kernel
+        // began (qlane: the group padded with the zero slot nitems, x + 0.0 =
+        // x for these non-negative, NaN or infinite values), so the gathers
+        // follow the barrier directly.  The butterfly runs on DPP: after
+        // level l every lane of an aligned 2^(l+1) block holds the same bits
+        // (the sums commute exactly), so any lane of the partner block will
+        // do -- quad_perm for levels 0-1, row_half_mirror and row_mirror for
+        // levels 2-3, an xor shuffle beyond.
+        for (uint32_t s0 = 0; s0 < nslot; s0 += kQrowsBlock) {
+            const uint32_t sl = s0 + threadIdx.x;
+            uint2 sd = sd0;
+            uint4 qa = qa0, qb = qb0;
+            if (s0 != 0) {
+                const uint32_t l = min(sl, nslot - 1);
+                sd = sl < nslot ? qslot[l] : make_uint2(0xffffffffu, 0u);
+                qa = qlane[2 * l];
+                qb = qlane[2 * l + 1];
+            }
+            const uint32_t q = sd.x, le = sd.y & 0xffu, lgL = (sd.y >> 8) & 0xfu;
+            const uint32_t itm[kQGroup] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+            double a[CB];
+#pragma unroll
+            for (int i = 0; i < CB; ++i) {
+                double x = Pl[pix(npl, itm[0], i)];
+#pragma unroll
+                for (uint32_t u = 1; u < kQGroup; ++u) x = x + Pl[pix(npl, itm[u], i)];
+                a[i] = x;
+            }
+            auto level = [&](uint32_t lv, auto part) {
+                if (lv >= lglmax) return;  // uniform
+#pragma unroll
+                for (int i = 0; i < CB; ++i) {
+                    const double o = part(a[i]), t = a[i] + o;
+                    a[i] = lv < lgL ? t : a[i];  // a select, not a branch per value
+                }
+            };
+            level(0, [](double v) { return quad_dpp<0xB1>(v); });   // quad_perm [1,0,3,2]
+            level(1, [](double v) { return quad_dpp<0x4E>(v); });   // quad_perm [2,3,0,1]
+            level(2, [](double v) { return quad_dpp<0x141>(v); });  // row_half_mirror
+            level(3, [](double v) { return quad_dpp<0x140>(v); });  // row_mirror
+            for (uint32_t lv = 4; lv < lglmax; ++lv)
+#pragma unroll
+                for (int i = 0; i < CB; ++i) {
+                    const double o = __shfl_xor(a[i], 1 << lv);
+                    if (lv < lgL) a[i] = a[i] + o;
+                }
+            if (q < ldQ && le == 0)
+#pragma unroll
+                for (int i = 0; i < CB; ++i)
+                    if ((uint32_t)i < ncb) Q[(size_t)(c0 + i) * ldQ + q] = a[i];
+        }
+    } else
     for (uint32_t s0 = 0; s0 < nslot; s0 += kQrowsBlock) {
         const uint32_t sl = s0 + threadIdx.x;
         const uint2 sd = s0 == 0 ? sd0 : sl < nslot ? qslot[sl] : make_uint2(0xffffffffu, 0u);
@@ -1510,12 +1614,14 @@ struct DevCtx {
     // direct path: k_zrows / k_qrows tables (zs, row-major [row][k], depends
     // on the grid's c range)
     double *zs = nullptr, *sv = nullptr, *Qrow = nullptr, *Zg = nullptr;
+    double *zsq = nullptr;  // zs chain-major, [row][k mod 4][k / 4] (k_qrows: a lane's chain contiguous)
     double *zc = nullptr;   // Z-row series coefficients [row][kZTerms]
     size_t cap_zc = 0;
     uint2 *items = nullptr;  // per item {B | row << 24, j | (row >> 8) << 24}
     uint2 *qslot = nullptr;  // k_qrows phase-3 lane table
+    uint32_t *qlane = nullptr;  // k_qrows phase-3 item indices per lane (nvar <= 8)
     uint32_t *itemB = nullptr, *qstart = nullptr, *qitem = nullptr;
-    size_t cap_zs = 0, cap_qrow = 0, cap_zg = 0;
+    size_t cap_zs = 0, cap_zsq = 0, cap_qrow = 0, cap_zg = 0;
     uint32_t zs_len = 0;    // doubles in zs = zs_kmax * nj
     double *coltab = nullptr;  // fused kernel's column tables (plan offsets, zs last), 1 KiB padded
     size_t cap_coltab = 0;
@@ -1658,6 +1764,7 @@ struct mdp_engine {
     std::vector<uint32_t> cj_bits, cj_item0, itemB, qstart, qitem, udesc_d, var_cols;
     std::vector<uint32_t> itemRow;  // row (j slot) of each item
     std::vector<uint2> qslot;       // k_qrows phase-3 lanes (build_direct_plan)
+    std::vector<uint32_t> qlane;    // their groups' item indices, kQGroup a lane (nvar <= 8)
     // k_fwd_mma (wide years on the matrix cores): per year t its K entries
     // (k | |A_k| << 8 | m << 16 | valid << 31, padded to 4) from kbase[t],
     // and the Q-row slot of each (K entry, new state l) from gbase[t]
@@ -1961,6 +2068,16 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
             for (uint32_t le = 0; le < (1u << en.lgL); ++le)
                 eng->qslot.push_back(make_uint2(en.q, le | (en.lgL << 8) | (en.lgG << 12)));
         while (eng->qslot.size() % 64) eng->qslot.push_back(make_uint2(0xffffffffu, 0u));
+        // nvar <= 8 (one group per lane): each lane's kQGroup item indices,
+        // the zero slot nitems past its entry; at least 64 lanes
+        eng->qlane.assign(std::max<size_t>(eng->qslot.size(), 64) * kQGroup, eng->nitems);
+        if (eng->nvar <= 8)
+            for (size_t sl = 0; sl < eng->qslot.size(); ++sl) {
+                const uint32_t q = eng->qslot[sl].x, le = eng->qslot[sl].y & 0xffu;
+                if ((size_t)q + 1 >= eng->qstart.size()) continue;  // padding lanes: q = ~0
+                const uint32_t j0 = eng->qstart[q] + le * kQGroup, i1 = eng->qstart[q + 1];
+                for (uint32_t u = 0; u < kQGroup && j0 + u < i1; ++u) eng->qlane[sl * kQGroup + u] = eng->qitem[j0 + u];
+            }
     }
     eng->udesc_d.clear();
     for (uint32_t pi : eng->use_pair) {
@@ -2185,6 +2302,12 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     int rc;
     if ((rc = dev_reserve(&d.zs, &d.cap_zs, zsT.size()))) return rc;
     HIP_TRY(hipMemcpy(d.zs, zsT.data(), zsT.size() * sizeof(double), hipMemcpyHostToDevice));
+    // k_qrows' copy: row js's product chain q (columns k = q mod 4) contiguous
+    std::vector<double> zsq(kmax * nj + 2, 0.0);  // + a double2 k_qrows may read at kmax 0
+    for (uint32_t js = 0; js < nj; ++js)
+        for (size_t k = 0; k < kmax; ++k) zsq[js * kmax + (k % 4) * (kmax / 4) + k / 4] = zsT[js * kmax + k];
+    if ((rc = dev_reserve(&d.zsq, &d.cap_zsq, zsq.size()))) return rc;
+    HIP_TRY(hipMemcpy(d.zsq, zsq.data(), zsq.size() * sizeof(double), hipMemcpyHostToDevice));
     if ((rc = dev_reserve(&d.zc, &d.cap_zc, zc.size()))) return rc;
     HIP_TRY(hipMemcpy(d.zc, zc.data(), zc.size() * sizeof(double), hipMemcpyHostToDevice));
     d.zs_cmax = cmax;
@@ -2491,7 +2614,7 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
         qitem.push_back(0u);
         if ((rc = dev_upload(&d.sv, sv)) || (rc = dev_upload(&d.items, items)) ||
             (rc = dev_upload(&d.qstart, eng->qstart)) || (rc = dev_upload(&d.qitem, qitem)) ||
-            (rc = dev_upload(&d.qslot, eng->qslot)))
+            (rc = dev_upload(&d.qslot, eng->qslot)) || (rc = dev_upload(&d.qlane, eng->qlane)))
             return rc;
         if (eng->wide) {
             if ((rc = dev_upload(&d.np_d, eng->np)) || (rc = dev_upload(&d.udesc_w, eng->udesc_d))) return rc;
@@ -2535,8 +2658,8 @@ void free_device(DevCtx &d)
     (void)hipSetDevice(d.device);
     void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog,
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
-                    d.zs, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
-                    d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot,
+                    d.zs, d.zsq, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
+                    d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot, d.qlane,
                     d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
@@ -2909,9 +3032,10 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, OutStrides os, h
     do {                                                                                                \
     note_launch(eng, "k_qrows<%d,%d,%d>", NV, (int)EX, CB);                                              \
     MDP_LAUNCH((k_qrows<NV, EX, CB>), grid, dim3(kQrowsBlock), lds, s, d.c, d.nc, eng->nvar, eng->nj,         \
-               d.zs_kmax, d.zs, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
+               d.zs_kmax, d.zsq, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
                (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1],                 \
-               (uint32_t)(eng->qrows_xcd ? 1u : 0u), d.qslot, (uint32_t)eng->qslot.size(), eng->qslot_lglmax); } while (0)
+               (uint32_t)(eng->qrows_xcd ? 1u : 0u), d.qslot, (uint32_t)eng->qslot.size(), eng->qslot_lglmax,   \
+               (const uint4 *)d.qlane); } while (0)
         // c values per workgroup: <= qrows_maxcb(nvar) (register budget at 1024 threads)
         if (eng->nvar == 8) {
             if (cb == 4) MDP_QROWS_CB(8, true, 4);
