@@ -1175,12 +1175,12 @@ __global__ __launch_bounds__(kBlock) void k_witems(const double *__restrict__ cv
         pcv = pcv > 1.0 ? 1.0 : pcv;
         const double p = sb < 0.0 ? 1.0 : pcv;
         const uint32_t nbit = (uint32_t)b < nvar ? (nB >> (nvar - 1 - (uint32_t)b)) & 1u : 0u;
-        const double sg = __hiloint2double((int)(0x3ff00000u | (nbit << 31)), 0);
-        const double nb = __hiloint2double((int)(nbit * 0x3ff00000u), 0);
-        f[b] = fma(sg, p, nb);
+        f[b] = (double)nbit - p;  // |n - p|: k_qrows' fold
     }
 #pragma unroll
-    for (int sh = 1; sh < NV; sh *= 2)
+    for (int b = 0; b < NV; b += 2) f[b] = fabs(f[b]) * fabs(f[b + 1]);
+#pragma unroll
+    for (int sh = 2; sh < NV; sh *= 2)
 #pragma unroll
         for (int b = 0; b + sh < NV; b += 2 * sh) f[b] *= f[b + sh];
     Pg[(size_t)cl * nitems + it] = Zg[(size_t)r * nc + c0 + cl] * f[0];

@@ -608,21 +608,25 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        const uint2 t = Itl[it];\n"
              "        const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
              // f_b = j_b ? 1 : B_b ? p_b : 1 - p_b with p_b = min(1, c S): one
-             // select for the clamp and j (j <= B, so B_b is set there), then
-             // fma(s, p, n) with (s, n) = (1, 0) or (-1, 1) from B_b -- the
-             // same bits as the select form (k_qrows uses the same fold)
+             // select for the clamp and j (the image marks j's columns -1; j <= B,
+             // so B_b is set there), then |n_b - p_b| with n_b = 1.0 where B_b
+             // is clear -- the same bits as fma(s, p, n), (s, n) = (1, 0) or
+             // (-1, 1) (1 - p rounded once, |0 - p| = p), with the abs moved to
+             // the product (k_qrows uses the same fold)
              "        double f[NVAR];\n"
              "        const u32 nB = ~B;\n"
+             "        (void)j;\n"
              "#pragma unroll\n"
              "        for (int b = 0; b < NVAR; ++b) {\n"
              "            const u32 bit = NVAR - 1 - b;\n"
-             "            const double pcv = c * Svl[r * NVAR + b];\n"
-             "            const double p = (pcv > 1.0) | ((j >> bit) & 1u) ? 1.0 : pcv;\n"
-             "            const double sg = __hiloint2double((int)(0x3ff00000u | ((nB << (31 - bit)) & 0x80000000u)), 0);\n"
-             "            f[b] = fma(sg, p, fma(-0.5, sg, 0.5));\n"
+             "            const double sv = Svl[r * NVAR + b], pcv = c * sv;\n"
+             "            const double p = (pcv > 1.0) | (sv < 0.0) ? 1.0 : pcv;\n"
+             "            f[b] = (double)((nB >> bit) & 1u) - p;\n"
              "        }\n"
              "#pragma unroll\n"
-             "        for (int s = 1; s < NVAR; s *= 2)\n"
+             "        for (int b = 0; b < NVAR; b += 2) f[b] = b + 1 < NVAR ? fabs(f[b]) * fabs(f[b + 1]) : fabs(f[b]);\n"
+             "#pragma unroll\n"
+             "        for (int s = 2; s < NVAR; s *= 2)\n"
              "#pragma unroll\n"
              "            for (int b = 0; b + s < NVAR; b += 2 * s) f[b] *= f[b + s];\n"
              "        Fp[k] = f[0];\n"
