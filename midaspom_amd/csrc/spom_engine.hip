@@ -402,12 +402,13 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // the padding phase 3's unconditional gathers read past an entry's end
     const uint32_t npl = nitems + 1;
     double *Pl = Prl + (size_t)nrows * PRS;            // [CB/CP][npl][CP]
-    uint2 *It = (uint2 *)(Pl + (size_t)npl * CB);      // [nitems] {B, j}, row in the top bytes
-    uint32_t *Qs = (uint32_t *)(It + nitems);          // [ncoef + 1]
+    uint32_t *Qs = (uint32_t *)(Pl + (size_t)npl * CB);  // [ncoef + 1] (nvar > 8)
     uint32_t *Qi = Qs + ncoef + 1;                     // [nqi]
     double cv[CB];  // this workgroup's c values (the last one again past the grid: never stored)
 #pragma unroll
     for (int i = 0; i < CB; ++i) cv[i] = cvals[c0 + min((uint32_t)i, ncb - 1)];  // no load in a branch
+    // phase 1's c value of this lane (lane q of a quad: c value q)
+    const double cq = cvals[c0 + min(threadIdx.x & 3u, ncb - 1)];
     // 1. Z and pressures per row, one quad of lanes per row.  Lane q takes
     // the row's product chain q (explicit columns k = q mod 4, k_zrows' chains
     // and order) for all CB c values; the quad combines the chains as
@@ -459,17 +460,28 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
             pair(x);
             if (2 * u + 2 < kq) pair(y);
         }
-        // (za zb)(zc zd): lanes 0, 1 hold za zb, lanes 2, 3 zc zd
+        // (za zb)(zc zd) for c value q in lane q
+        double c = cv[0], zz;
+        if constexpr (CB == 4) {
+            // reduce-scatter: the pairs (0,1), (2,3) each keep two c values
+            // (lane q those = q mod 2), then (0,2), (1,3) one
+            const bool b0 = q & 1u, b1 = q & 2u;
+            const double s0 = b0 ? ch[0] : ch[1], s1 = b0 ? ch[2] : ch[3];
+            const double k0 = (b0 ? ch[1] : ch[0]) * quad_dpp<0xB1>(s0);  // quad_perm [1,0,3,2]
+            const double k1 = (b0 ? ch[3] : ch[2]) * quad_dpp<0xB1>(s1);
+            zz = (b1 ? k1 : k0) * quad_dpp<0x4E>(b1 ? k0 : k1);  // quad_perm [2,3,0,1]
+            c = cq;
+        } else {
 #pragma unroll
-        for (int i = 0; i < CB; ++i) {
-            ch[i] = ch[i] * quad_dpp<0xB1>(ch[i]);  // quad_perm [1,0,3,2]
-            ch[i] = ch[i] * quad_dpp<0x4E>(ch[i]);  // quad_perm [2,3,0,1]
+            for (int i = 0; i < CB; ++i) {
+                ch[i] = ch[i] * quad_dpp<0xB1>(ch[i]);  // quad_perm [1,0,3,2]
+                ch[i] = ch[i] * quad_dpp<0x4E>(ch[i]);  // quad_perm [2,3,0,1]
+            }
+            zz = ch[0];
+#pragma unroll
+            for (int i = 1; i < CB; ++i)
+                if (q == (uint32_t)i) c = cv[i], zz = ch[i];
         }
-        // lane q: c value q
-        double c = cv[0], zz = ch[0];
-#pragma unroll
-        for (int i = 1; i < CB; ++i)
-            if (q == (uint32_t)i) c = cv[i], zz = ch[i];
         const double first = quad_dpp<0x00>(L.t[0].x);  // column 0, the row maximum
         if (kmax && !(fma(-c, first, 1.0) > 0.0)) zz = 0.0;
         double zq[kZTermsDev];
@@ -503,33 +515,32 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     RowLd L0;
     rowload(min(threadIdx.x, nrw - 1), L0);
     constexpr uint32_t kSt = 4;
-    uint2 ti[kSt];
+    uint2 ti[kSt];  // the items of this thread's first kSt phase-2 passes
     uint32_t ts[kSt], tq[kSt];
-    auto stload = [&](uint32_t i0) {
+    auto stload = [&](uint32_t i0, uint2 *pi, uint32_t *ps, uint32_t *pq) {
 #pragma unroll
         for (uint32_t u = 0; u < kSt; ++u) {
             const uint32_t i = i0 + u * kQrowsBlock;
             // clamped, not guarded: a guarded load sits in a branch, and the
             // row's first use then waited for every staging load too
-            ti[u] = items[min(i, nitems - 1)];  // launched only with items
+            if (pi) pi[u] = items[min(i, nitems - 1)];  // launched only with items
             if constexpr (NV != 8) {  // nvar <= 8: phase 3 reads qlane instead
-                ts[u] = qstart[min(i, ncoef)];
-                tq[u] = nqi ? qitem[min(i, nqi - 1)] : 0u;
+                ps[u] = qstart[min(i, ncoef)];
+                pq[u] = nqi ? qitem[min(i, nqi - 1)] : 0u;
             }
         }
     };
-    auto ststore = [&](uint32_t i0) {
+    auto ststore = [&](uint32_t i0, const uint32_t *ps, const uint32_t *pq) {
+        if constexpr (NV != 8) {
 #pragma unroll
-        for (uint32_t u = 0; u < kSt; ++u) {
-            const uint32_t i = i0 + u * kQrowsBlock;
-            if (i < nitems) It[i] = ti[u];
-            if constexpr (NV != 8) {
-                if (i <= ncoef) Qs[i] = ts[u];
-                if (i < nqi) Qi[i] = tq[u];
+            for (uint32_t u = 0; u < kSt; ++u) {
+                const uint32_t i = i0 + u * kQrowsBlock;
+                if (i <= ncoef) Qs[i] = ps[u];
+                if (i < nqi) Qi[i] = pq[u];
             }
         }
     };
-    stload(threadIdx.x);
+    stload(threadIdx.x, ti, ts, tq);
     if (threadIdx.x < nrw) rowwork(threadIdx.x, L0);
     for (uint32_t w = threadIdx.x + kQrowsBlock; w < nrw; w += kQrowsBlock) {
         RowLd L;
@@ -537,12 +548,12 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         rowwork(w, L);
     }
     MDP_STAMP(stamps, 4);
-    ststore(threadIdx.x);
-    {
-        const uint32_t nmax = NV == 8 ? nitems : max(max(nitems, ncoef + 1), nqi);
-        for (uint32_t i0 = threadIdx.x + kSt * kQrowsBlock; i0 < nmax; i0 += kSt * kQrowsBlock) {
-            stload(i0);
-            ststore(i0);
+    ststore(threadIdx.x, ts, tq);
+    if constexpr (NV != 8) {  // a longer Q CSR (items past kSt passes are read in phase 2)
+        for (uint32_t i0 = threadIdx.x + kSt * kQrowsBlock; i0 < max(ncoef + 1, nqi); i0 += kSt * kQrowsBlock) {
+            uint32_t ps[kSt], pq[kSt];
+            stload(i0, nullptr, ps, pq);
+            ststore(i0, ps, pq);
         }
     }
     MDP_STAMP(stamps, 5);
@@ -558,8 +569,9 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // per item and the abs folded into the tree's first products.  (Building
     // s_b and n_b as doubles cost 5 integer instructions a slot, a quarter-rate
     // multiply among them: phase 2 is bound by VALU issue.)
-    for (uint32_t it = threadIdx.x; it < nitems; it += kQrowsBlock) {
-        const uint2 t = It[it];
+    // the first kSt passes' items are still in this thread's staging
+    // registers (pass u's item is the one it loaded as ti[u])
+    auto pcitem = [&](uint32_t it, const uint2 t) {
         const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), nB = ~t.x;
         double nb[NV];
 #pragma unroll
@@ -588,7 +600,11 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         }
 #pragma unroll
         for (int i = 0; i < CB; ++i) Pl[pix(npl, it, i)] = pc[i];
-    }
+    };
+#pragma unroll
+    for (uint32_t u = 0; u < kSt; ++u)
+        if (threadIdx.x + u * kQrowsBlock < nitems) pcitem(threadIdx.x + u * kQrowsBlock, ti[u]);
+    for (uint32_t it = threadIdx.x + kSt * kQrowsBlock; it < nitems; it += kQrowsBlock) pcitem(it, items[it]);
     if (threadIdx.x < CB) Pl[pix(npl, nitems, threadIdx.x)] = 0.0;
     __syncthreads();
     MDP_STAMP(stamps, 2);
@@ -2232,7 +2248,7 @@ size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
     const size_t nv = eng->nvar <= 8 ? 8 : eng->nvar <= 16 ? 16 : 24;  // k_qrows NV
     return ((((size_t)cb * eng->nj + 1) & ~(size_t)1) + (size_t)eng->nj * (cb * nv + 2) + (size_t)cb * (eng->nitems + 1)) *
                sizeof(double) +
-           (size_t)eng->nitems * sizeof(uint2) + ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);
+           ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);  // (items stay in registers)
 }
 
 // Z rows for a grid whose |c| <= cmax.  Z_j(c) = prod over the always-zero
