@@ -363,7 +363,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     uint32_t nitems, const uint2 *__restrict__ items, uint32_t ncoef, const uint32_t *__restrict__ qstart,
     uint32_t nqi, const uint32_t *__restrict__ qitem, double *__restrict__ Q, uint32_t ldQ,
     unsigned long long *__restrict__ stamps, uint32_t xcd, const uint2 *__restrict__ qslot, uint32_t nslot,
-    uint32_t lglmax, const uint4 *__restrict__ qlane)
+    uint32_t lglmax, const uint4 *__restrict__ qlane, const uint32_t *__restrict__ islot, uint32_t npl)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     MDP_RSTAMP(stamps, 6);
@@ -398,9 +398,10 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // by one double2 so rows read by one wave fall on different banks
     constexpr uint32_t PRS = CB * NV + 2;
     double *Prl = Zl + (((size_t)nrows * CB + 1) & ~(size_t)1);  // [nrows][PRS], 16-byte aligned
-    // Pc per item and c, one more slot per c value after the items: zero,
-    // the padding phase 3's unconditional gathers read past an entry's end
-    const uint32_t npl = nitems + 1;
+    // Pc per item and c in npl slots (host table islot: item -> slot);
+    // slots 0-15 hold zeros, the padding phase 3's unconditional gathers
+    // read past an entry's end (one per residue mod 16, so each gather group
+    // can take one no other lane of it reads)
     double *Pl = Prl + (size_t)nrows * PRS;            // [CB/CP][npl][CP]
     uint32_t *Qs = (uint32_t *)(Pl + (size_t)npl * CB);  // [ncoef + 1] (nvar > 8)
     uint32_t *Qi = Qs + ncoef + 1;                     // [nqi]
@@ -515,7 +516,8 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     RowLd L0;
     rowload(min(threadIdx.x, nrw - 1), L0);
     constexpr uint32_t kSt = 4;
-    uint2 ti[kSt];  // the items of this thread's first kSt phase-2 passes
+    uint2 ti[kSt];     // the items of this thread's first kSt phase-2 passes
+    uint32_t si[kSt];  // and their Pc slots
     uint32_t ts[kSt], tq[kSt];
     auto stload = [&](uint32_t i0, uint2 *pi, uint32_t *ps, uint32_t *pq) {
 #pragma unroll
@@ -523,7 +525,10 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
             const uint32_t i = i0 + u * kQrowsBlock;
             // clamped, not guarded: a guarded load sits in a branch, and the
             // row's first use then waited for every staging load too
-            if (pi) pi[u] = items[min(i, nitems - 1)];  // launched only with items
+            if (pi) {  // launched only with items
+                pi[u] = items[min(i, nitems - 1)];
+                si[u] = islot[min(i, nitems - 1)];
+            }
             if constexpr (NV != 8) {  // nvar <= 8: phase 3 reads qlane instead
                 ps[u] = qstart[min(i, ncoef)];
                 pq[u] = nqi ? qitem[min(i, nqi - 1)] : 0u;
@@ -571,7 +576,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // multiply among them: phase 2 is bound by VALU issue.)
     // the first kSt passes' items are still in this thread's staging
     // registers (pass u's item is the one it loaded as ti[u])
-    auto pcitem = [&](uint32_t it, const uint2 t) {
+    auto pcitem = [&](uint32_t sl, const uint2 t) {
         const uint32_t r = (t.x >> 24) | ((t.y >> 24) << 8), nB = ~t.x;
         double nb[NV];
 #pragma unroll
@@ -599,13 +604,13 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
             pc[i] = zr[i] * f[0];
         }
 #pragma unroll
-        for (int i = 0; i < CB; ++i) Pl[pix(npl, it, i)] = pc[i];
+        for (int i = 0; i < CB; ++i) Pl[pix(npl, sl, i)] = pc[i];
     };
 #pragma unroll
     for (uint32_t u = 0; u < kSt; ++u)
-        if (threadIdx.x + u * kQrowsBlock < nitems) pcitem(threadIdx.x + u * kQrowsBlock, ti[u]);
-    for (uint32_t it = threadIdx.x + kSt * kQrowsBlock; it < nitems; it += kQrowsBlock) pcitem(it, items[it]);
-    if (threadIdx.x < CB) Pl[pix(npl, nitems, threadIdx.x)] = 0.0;
+        if (threadIdx.x + u * kQrowsBlock < nitems) pcitem(si[u], ti[u]);
+    for (uint32_t it = threadIdx.x + kSt * kQrowsBlock; it < nitems; it += kQrowsBlock) pcitem(islot[it], items[it]);
+    if (threadIdx.x < 16 * CB) Pl[pix(npl, threadIdx.x / CB, threadIdx.x % CB)] = 0.0;
     __syncthreads();
     MDP_STAMP(stamps, 2);
     // 3. Q rows in the canonical order.  Each entry owns an aligned
@@ -618,10 +623,11 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
     // entry's whole item list (35 on config 3).
     if constexpr (NV == 8) {
         // nvar <= 8: one group per lane (an entry has at most C(8,4) = 70
-        // items, 9 groups), its item indices in registers since the kernel
-        // began (qlane: the group padded with the zero slot nitems, x + 0.0 =
-        // x for these non-negative, NaN or infinite values), so the gathers
-        // follow the barrier directly.  The butterfly runs on DPP: after
+        // items, 9 groups), its items' Pc slots in registers since the kernel
+        // began (qlane: the group padded with a zero slot, x + 0.0 = x for
+        // these non-negative, NaN or infinite values), so the gathers follow
+        // the barrier directly; the slots are coloured on the host so that
+        // each gather group's 16-byte slots fall on distinct banks.  The butterfly runs on DPP: after
         // level l every lane of an aligned 2^(l+1) block holds the same bits
         // (the sums commute exactly), so any lane of the partner block will
         // do -- quad_perm for levels 0-1, row_half_mirror and row_mirror for
@@ -693,7 +699,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
 #pragma unroll
                 for (uint32_t u = 0; u < kQGroup; ++u) {
                     const uint32_t t_ = Qi[j0 + u < i1 ? j0 + u : j0];
-                    itm[u] = j0 + u < i1 ? t_ : nitems;
+                    itm[u] = j0 + u < i1 ? t_ + 16 : 0u;  // slots (nvar > 8: item + 16)
                 }
 #pragma unroll
                 for (int i = 0; i < CB; ++i) {
@@ -1635,7 +1641,8 @@ struct DevCtx {
     size_t cap_zc = 0;
     uint2 *items = nullptr;  // per item {B | row << 24, j | (row >> 8) << 24}
     uint2 *qslot = nullptr;  // k_qrows phase-3 lane table
-    uint32_t *qlane = nullptr;  // k_qrows phase-3 item indices per lane (nvar <= 8)
+    uint32_t *qlane = nullptr;  // k_qrows phase-3 Pc slots per lane (nvar <= 8)
+    uint32_t *islot = nullptr;  // k_qrows: each item's Pc slot
     uint32_t *itemB = nullptr, *qstart = nullptr, *qitem = nullptr;
     size_t cap_zs = 0, cap_zsq = 0, cap_qrow = 0, cap_zg = 0;
     uint32_t zs_len = 0;    // doubles in zs = zs_kmax * nj
@@ -1780,7 +1787,9 @@ struct mdp_engine {
     std::vector<uint32_t> cj_bits, cj_item0, itemB, qstart, qitem, udesc_d, var_cols;
     std::vector<uint32_t> itemRow;  // row (j slot) of each item
     std::vector<uint2> qslot;       // k_qrows phase-3 lanes (build_direct_plan)
-    std::vector<uint32_t> qlane;    // their groups' item indices, kQGroup a lane (nvar <= 8)
+    std::vector<uint32_t> qlane;    // their groups' Pc slots, kQGroup a lane (nvar <= 8)
+    std::vector<uint32_t> islot;    // k_qrows: each item's Pc slot (slots 0-15: zeros)
+    uint32_t npl_slots = 0;         // k_qrows: Pc slots per c value
     // k_fwd_mma (wide years on the matrix cores): per year t its K entries
     // (k | |A_k| << 8 | m << 16 | valid << 31, padded to 4) from kbase[t],
     // and the Q-row slot of each (K entry, new state l) from gbase[t]
@@ -2084,9 +2093,10 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
             for (uint32_t le = 0; le < (1u << en.lgL); ++le)
                 eng->qslot.push_back(make_uint2(en.q, le | (en.lgL << 8) | (en.lgG << 12)));
         while (eng->qslot.size() % 64) eng->qslot.push_back(make_uint2(0xffffffffu, 0u));
-        // nvar <= 8 (one group per lane): each lane's kQGroup item indices,
-        // the zero slot nitems past its entry; at least 64 lanes
-        eng->qlane.assign(std::max<size_t>(eng->qslot.size(), 64) * kQGroup, eng->nitems);
+        // nvar <= 8 (one group per lane): each lane's kQGroup items, nitems
+        // past its entry; at least 64 lanes
+        const uint32_t ni = eng->nitems;
+        eng->qlane.assign(std::max<size_t>(eng->qslot.size(), 64) * kQGroup, ni);
         if (eng->nvar <= 8)
             for (size_t sl = 0; sl < eng->qslot.size(); ++sl) {
                 const uint32_t q = eng->qslot[sl].x, le = eng->qslot[sl].y & 0xffu;
@@ -2094,6 +2104,86 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
                 const uint32_t j0 = eng->qstart[q] + le * kQGroup, i1 = eng->qstart[q + 1];
                 for (uint32_t u = 0; u < kQGroup && j0 + u < i1; ++u) eng->qlane[sl * kQGroup + u] = eng->qitem[j0 + u];
             }
+        // Pc slots (16 bytes per slot and c pair in LDS).  Phase 3 gathers
+        // item u of every lane in one ds_read_b128, serviced in four 16-lane
+        // groups, conflict-free when a group's slots differ mod 16; phase 2
+        // stores eight consecutive items per 8-lane group of a
+        // ds_write_b128, conflict-free when they differ mod 8.  The items are
+        // coloured (colour = slot mod 16) greedily under both rules, the
+        // least-used allowed colour first; slots 0-15 hold zeros, and each
+        // group's padding takes the zero slot of a colour none of its items
+        // has.  nvar > 8 (CSR path): slot = item + 16.
+        eng->islot.resize(ni);
+        for (uint32_t it = 0; it < ni; ++it) eng->islot[it] = it + 16;
+        eng->npl_slots = ni + 16;
+        if (eng->nvar <= 8) {
+            auto lgroup = [](uint32_t l) -> uint32_t {  // ds_read_b128 lane groups
+                const uint32_t h = l & 31u;
+                const uint32_t g = (h < 4 || (h >= 12 && h < 16) || (h >= 20 && h < 28)) ? 0u : 1u;
+                return g + (l >= 32 ? 2u : 0u);
+            };
+            const size_t nl = eng->qslot.size();
+            std::vector<std::vector<uint32_t>> grp;  // per (wave, u, lane group): its items
+            for (size_t w0 = 0; w0 < nl; w0 += 64)
+                for (uint32_t u = 0; u < kQGroup; ++u) {
+                    std::vector<uint32_t> g4[4];
+                    for (uint32_t l = 0; l < 64 && w0 + l < nl; ++l) {
+                        const uint32_t it = eng->qlane[(w0 + l) * kQGroup + u];
+                        if (it < ni) g4[lgroup(l)].push_back(it);
+                    }
+                    for (auto &g : g4) {
+                        std::sort(g.begin(), g.end());
+                        g.erase(std::unique(g.begin(), g.end()), g.end());
+                        grp.push_back(std::move(g));
+                    }
+                }
+            std::vector<std::vector<uint32_t>> ig(ni);
+            for (uint32_t gi = 0; gi < grp.size(); ++gi)
+                for (uint32_t it : grp[gi]) ig[it].push_back(gi);
+            std::vector<int> col(ni, -1);
+            uint32_t cnt[16] = {};
+            for (uint32_t it = 0; it < ni; ++it) {
+                uint32_t forb = 0;
+                for (uint32_t gi : ig[it])
+                    for (uint32_t o : grp[gi])
+                        if (col[o] >= 0) forb |= 1u << col[o];
+                for (uint32_t o = it & ~7u; o < (it | 7u) + 1 && o < ni; ++o)  // phase 2's store group
+                    if (o != it && col[o] >= 0) forb |= 0x101u << (col[o] & 7);
+                int best = -1;
+                for (int pass = 0; pass < 2 && best < 0; ++pass)
+                    for (int cc = 0; cc < 16; ++cc)
+                        if ((pass || !((forb >> cc) & 1u)) && (best < 0 || cnt[cc] < cnt[best])) best = cc;
+                col[it] = best;
+                ++cnt[best];
+            }
+            uint32_t next[16];
+            for (uint32_t cc = 0; cc < 16; ++cc) next[cc] = 16 + cc;
+            uint32_t top = 16;
+            for (uint32_t it = 0; it < ni; ++it) {
+                eng->islot[it] = next[col[it]];
+                next[col[it]] += 16;
+                top = std::max(top, eng->islot[it] + 1);
+            }
+            eng->npl_slots = top;
+            // the lanes' slots; each (wave, u, lane group)'s padding on a free colour
+            for (size_t w0 = 0; w0 < std::max<size_t>(nl, 64); w0 += 64)
+                for (uint32_t u = 0; u < kQGroup; ++u) {
+                    uint32_t used[4] = {};
+                    for (uint32_t l = 0; l < 64; ++l) {
+                        const uint32_t it = eng->qlane[(w0 + l) * kQGroup + u];
+                        if (it < ni) used[lgroup(l)] |= 1u << (eng->islot[it] & 15u);
+                    }
+                    for (uint32_t l = 0; l < 64; ++l) {
+                        uint32_t &x = eng->qlane[(w0 + l) * kQGroup + u];
+                        if (x < ni) {
+                            x = eng->islot[x];
+                        } else {
+                            const uint32_t fr = ~used[lgroup(l)] & 0xffffu;
+                            x = fr ? (uint32_t)__builtin_ctz(fr) : 0u;
+                        }
+                    }
+                }
+        }
     }
     eng->udesc_d.clear();
     for (uint32_t pi : eng->use_pair) {
@@ -2246,7 +2336,7 @@ constexpr size_t kFusedLdsMax = 64 * 1024;  // fused forward kernel: every table
 size_t qrows_lds(const mdp_engine *eng, uint32_t cb)
 {
     const size_t nv = eng->nvar <= 8 ? 8 : eng->nvar <= 16 ? 16 : 24;  // k_qrows NV
-    return ((((size_t)cb * eng->nj + 1) & ~(size_t)1) + (size_t)eng->nj * (cb * nv + 2) + (size_t)cb * (eng->nitems + 1)) *
+    return ((((size_t)cb * eng->nj + 1) & ~(size_t)1) + (size_t)eng->nj * (cb * nv + 2) + (size_t)cb * eng->npl_slots) *
                sizeof(double) +
            ((size_t)eng->ncoef_d + 1 + eng->qitem.size()) * sizeof(uint32_t);  // (items stay in registers)
 }
@@ -2630,7 +2720,8 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
         qitem.push_back(0u);
         if ((rc = dev_upload(&d.sv, sv)) || (rc = dev_upload(&d.items, items)) ||
             (rc = dev_upload(&d.qstart, eng->qstart)) || (rc = dev_upload(&d.qitem, qitem)) ||
-            (rc = dev_upload(&d.qslot, eng->qslot)) || (rc = dev_upload(&d.qlane, eng->qlane)))
+            (rc = dev_upload(&d.qslot, eng->qslot)) || (rc = dev_upload(&d.qlane, eng->qlane)) ||
+            (rc = dev_upload(&d.islot, eng->islot)))
             return rc;
         if (eng->wide) {
             if ((rc = dev_upload(&d.np_d, eng->np)) || (rc = dev_upload(&d.udesc_w, eng->udesc_d))) return rc;
@@ -2675,7 +2766,7 @@ void free_device(DevCtx &d)
     void *ptrs[] = {d.S, d.var_cols, d.row_col, d.pairA, d.pairB, d.pairOff, d.udesc, d.prog,
                     d.pairPart0, d.partP, d.partK0, d.e, d.c, d.ZPV, d.R, d.out, d.gpart,
                     d.zs, d.zsq, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
-                    d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot, d.qlane,
+                    d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot, d.qlane, d.islot,
                     d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
@@ -3051,7 +3142,7 @@ int launch_slot(mdp_engine *eng, DevCtx &d, int k, double *out, OutStrides os, h
                d.zs_kmax, d.zsq, d.zc, d.sv, eng->nitems, d.items, eng->ncoef_d, d.qstart,                     \
                (uint32_t)eng->qitem.size(), d.qitem, d.Qrow, (uint32_t)eng->ldQ, d.stamps[1],                 \
                (uint32_t)(eng->qrows_xcd ? 1u : 0u), d.qslot, (uint32_t)eng->qslot.size(), eng->qslot_lglmax,   \
-               (const uint4 *)d.qlane); } while (0)
+               (const uint4 *)d.qlane, d.islot, eng->npl_slots); } while (0)
         // c values per workgroup: <= qrows_maxcb(nvar) (register budget at 1024 threads)
         if (eng->nvar == 8) {
             if (cb == 4) MDP_QROWS_CB(8, true, 4);
