@@ -61,6 +61,40 @@ def run(name, extra, files=False):
 res = {}
 for name in inputs:  # fill the caches
     run(name, {})
+if os.environ.get("E2E_MALLOC"):
+    # E2E_MALLOC=1: the exit cost against where glibc puts the output buffer
+    # (mmap threshold forced low: every buffer mmapped and unmapped by free;
+    # forced high: every buffer on the brk heap)
+    for sz in (50, 200, 512):
+        inputs[f"config1_s{sz}x"] = (inputs["config1"][0], sz)
+    for rep in range(3):
+        for sz in (50, 200, 512):
+            for vn, extra in (("default", {}), ("mmap4k", {"MALLOC_MMAP_THRESHOLD_": "4096"}),
+                              ("heap", {"MALLOC_MMAP_THRESHOLD_": "1073741824"})):
+                res.setdefault(f"config1_s{sz}_{vn}", []).append(run(f"config1_s{sz}x", extra))
+    print(json.dumps(res))
+    sys.exit(0)
+if os.environ.get("E2E_SIZES"):
+    # E2E_SIZES=1: config 1's problem over grid sizes (where does the exit cost start?)
+    for sz in (50, 100, 150, 200, 300, 512):
+        inputs[f"config1_s{sz}x"] = (inputs["config1"][0], sz)
+        run(f"config1_s{sz}x", {})
+    for rep in range(3):
+        for sz in (50, 100, 150, 200, 300, 512):
+            res.setdefault(f"config1_s{sz}", []).append(run(f"config1_s{sz}x", {}))
+    print(json.dumps(res))
+    sys.exit(0)
+if os.environ.get("E2E_VARIANTS"):
+    # E2E_VARIANTS=1: configs 1 at s = 50 and 512 under runtime settings that
+    # could make the exit's cost (copy engines off, one hardware queue)
+    variants = {"base": {}, "sdma0": {"HSA_ENABLE_SDMA": "0"}, "hwq1": {"GPU_MAX_HW_QUEUES": "1"},
+                "sdma0_hwq1": {"HSA_ENABLE_SDMA": "0", "GPU_MAX_HW_QUEUES": "1"}}
+    for rep in range(3):
+        for vn, extra in variants.items():
+            for name in ("config1", "config1_s512"):
+                res.setdefault(f"{name}_{vn}", []).append(run(name, extra))
+    print(json.dumps(res))
+    sys.exit(0)
 for rep in range(3):
     for name in inputs:
         for mode, extra in (("quick", {}), ("full", {"MIDASPOM_FULL_EXIT": "1"})):
