@@ -1790,6 +1790,8 @@ struct mdp_engine {
     std::vector<uint32_t> qlane;    // their groups' Pc slots, kQGroup a lane (nvar <= 8)
     std::vector<uint32_t> islot;    // k_qrows: each item's Pc slot (slots 0-15: zeros)
     uint32_t npl_slots = 0;         // k_qrows: Pc slots per c value
+    uint32_t slot_conflicts = 0;    // k_qrows: extra gather cycles its slot colouring leaves (per c pair)
+    uint32_t slot_store_conflicts = 0;  // and extra store-group conflicts
     // k_fwd_mma (wide years on the matrix cores): per year t its K entries
     // (k | |A_k| << 8 | m << 16 | valid << 31, padded to 4) from kbase[t],
     // and the Q-row slot of each (K entry, new state l) from gbase[t]
@@ -2156,6 +2158,36 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
                 col[it] = best;
                 ++cnt[best];
             }
+            // min-conflicts repair: move an item to the colour its groups use
+            // least while that lowers its own conflicts (each move lowers the
+            // total, which is symmetric in the pairs), a few sweeps.  A gather
+            // conflict costs a cycle per group; a store conflict only about a
+            // quarter of one (a ds_write_b128's transfer, 13 cycles, hides all
+            // but 3 of the 16 array cycles of a 2-way conflict): weights 4 : 1
+            for (int sweep = 0; sweep < 16; ++sweep) {
+                bool moved = false;
+                for (uint32_t it = 0; it < ni; ++it) {
+                    uint32_t cost[16] = {};
+                    for (uint32_t gi : ig[it])
+                        for (uint32_t o : grp[gi])
+                            if (o != it) cost[col[o]] += 4;
+                    for (uint32_t o = it & ~7u; o < (it | 7u) + 1 && o < ni; ++o)
+                        if (o != it) {
+                            ++cost[col[o] & 7];
+                            ++cost[(col[o] & 7) + 8];
+                        }
+                    int best = col[it];
+                    for (int cc = 0; cc < 16; ++cc)
+                        if (cost[cc] < cost[best] || (cost[cc] == cost[best] && cnt[cc] + 1 < cnt[best])) best = cc;
+                    if (best != col[it]) {
+                        --cnt[col[it]];
+                        ++cnt[best];
+                        col[it] = best;
+                        moved = true;
+                    }
+                }
+                if (!moved) break;
+            }
             uint32_t next[16];
             for (uint32_t cc = 0; cc < 16; ++cc) next[cc] = 16 + cc;
             uint32_t top = 16;
@@ -2165,6 +2197,21 @@ int build_direct_plan(mdp_engine *eng, const mdp_problem *p)
                 top = std::max(top, eng->islot[it] + 1);
             }
             eng->npl_slots = top;
+            // what the colouring leaves: per phase-3 group the extra cycles of
+            // its busiest residue, per phase-2 store group those mod 8
+            uint32_t extra = 0, sextra = 0;
+            for (const auto &g : grp) {
+                uint32_t m[16] = {};
+                for (uint32_t it : g) ++m[eng->islot[it] & 15u];
+                extra += *std::max_element(m, m + 16) - (g.empty() ? 0u : 1u);
+            }
+            for (uint32_t g0 = 0; g0 < ni; g0 += 8) {
+                uint32_t m[8] = {};
+                for (uint32_t it = g0; it < std::min(ni, g0 + 8); ++it) ++m[eng->islot[it] & 7u];
+                sextra += *std::max_element(m, m + 8) - 1u;
+            }
+            eng->slot_conflicts = extra;
+            eng->slot_store_conflicts = sextra;
             // the lanes' slots; each (wave, u, lane group)'s padding on a free colour
             for (size_t w0 = 0; w0 < std::max<size_t>(nl, 64); w0 += 64)
                 for (uint32_t u = 0; u < kQGroup; ++u) {
@@ -3520,8 +3567,9 @@ int mdp_engine_create_opts(const mdp_problem *p, const int *devices, int n_devic
                 if (!r1)
                     mdp_set_error(MDP_ENODEV,
                                   "no HIP device available (forward kernels compiled; nj %u nitems %u "
-                                  "items/row %u ldQ %zu qitems %u qmaxlen %u kzmax %u fused LDS %zu)",
+                                  "items/row %u ldQ %zu qitems %u qmaxlen %u kzmax %u qrows slots %u conflicts %u + %u fused LDS %zu)",
                                   plan.nj, plan.nitems, ipr, (size_t)plan.ldQ, plan.nqi, plan.qmaxlen, plan.kzmax,
+                                  eng->npl_slots, eng->slot_conflicts, eng->slot_store_conflicts,
                                   fused_lds(eng, ((plan.off_zs + (size_t)plan.kzmax * eng->nj) + 127) & ~(size_t)127));
                 delete eng;
                 return r1 ? r1 : MDP_ENODEV;

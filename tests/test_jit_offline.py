@@ -79,3 +79,24 @@ def test_wide_years_plan_offline(row0, wide, expect):
         env["MDP_WIDE"] = wide
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(gpu_available(), reason="offline planning check runs on CPU-only hosts")
+def test_qrows_slot_colouring_offline(tmp_path):
+    """k_qrows' Pc slots (spom_engine.hip build_direct_plan): coloured so the
+    phase-3 gathers (16-lane groups, slots distinct mod 16) and the phase-2
+    stores (8 consecutive items, distinct mod 8) meet few bank conflicts, in
+    about as many slots as items.  Config 3: 416 gather groups, 236 store
+    groups; the plan reports the extra cycles the colouring leaves."""
+    import re
+    env = dict(os.environ, MDP_JIT_CHECK="1")
+    code = SCRIPT.format(root=str(ROOT), src="synth:CONFIG3", tmp=str(tmp_path)).replace(
+        '    assert "forward kernels compiled" in msg, msg\n    print("ok")',
+        '    print(msg)')
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    m = re.search(r"nitems (\d+) .*qrows slots (\d+) conflicts (\d+) \+ (\d+)", r.stdout)
+    assert m, r.stdout + r.stderr
+    nitems, slots, gather, store = map(int, m.groups())
+    assert nitems == 1881
+    assert slots <= nitems + 16 + 64          # 16 zero slots, little slack
+    assert gather <= 32 and store <= 96       # of 416 / 236 groups
