@@ -1653,8 +1653,10 @@ struct DevCtx {
     uint32_t qrows_cb = 1;  // c values per k_qrows workgroup for this grid
     bool qrows_attr_set = false;  // k_qrows' LDS limit raised on this device
     double zs_cmax = -1.0;  // c bound the uploaded zs was pruned for (-1: none yet)
-    hipModule_t jit_mod[2] = {nullptr, nullptr};  // problem-specialised forward kernel [fused]
-    hipFunction_t jit_fn[2] = {nullptr, nullptr};
+    // problem-specialised forward kernel [variant]: 0 reading, 1 fused, 2
+    // reading at kJitKblockTall threads (tall grids, set_grid_dev)
+    hipModule_t jit_mod[3] = {nullptr, nullptr, nullptr};
+    hipFunction_t jit_fn[3] = {nullptr, nullptr, nullptr};
     // a long series: one forward kernel per chunk of years, the state vector
     // handed over in vscr[state][c][e] (ldv e values per (state, c))
     std::vector<hipModule_t> cmod;
@@ -1664,6 +1666,7 @@ struct DevCtx {
     size_t cap_vscr = 0;
     uint32_t ldv = 0;
     bool fused = false;  // this grid runs the fused forward kernel (no k_qrows)
+    bool tall = false;   // this grid runs the reading kernel at kJitKblockTall threads
     // wide path: per-chunk item factors, state-vector scratch, tables
     double *Pg = nullptr, *V = nullptr;
     size_t cap_pg = 0, cap_v = 0;
@@ -1771,8 +1774,8 @@ struct mdp_engine {
     bool jit_shape_env = false;  // MDP_EPL / MDP_JIT_KBLOCK set: one shape for both variants
     double jit_flops_pt = 0;  // its FP64 flops per grid point (counted by the generator)
     size_t ldQ = 0;           // per-c Q block (doubles, even) read by the JIT kernel
-    std::vector<char> jit_code[2];  // forward kernel code objects [fused], compiled on demand
-    std::string jit_src[2];         // their sources (a cached object the runtime refuses is rebuilt)
+    std::vector<char> jit_code[3];  // forward kernel code objects [variant, as DevCtx::jit_fn], compiled on demand
+    std::string jit_src[3];         // their sources (a cached object the runtime refuses is rebuilt)
     std::vector<std::string> chunk_src;
     std::vector<MdpJitPlan> chunks;               // > 1: the series runs as chunks of years
     std::vector<std::vector<char>> chunk_code;    // their code objects
@@ -2500,12 +2503,25 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     return MDP_OK;
 }
 
-// Compile (hipRTC, cached) the engine's forward kernel, fused or not.
-int jit_build(mdp_engine *eng, bool fused)
+// Compile (hipRTC, cached) the engine's forward kernel: variant 0 reading,
+// 1 fused, 2 reading at kJitKblockTall threads (a column of a tall grid in
+// half the blocks: its Q row staged half as often).
+constexpr int kJitKblockTall = 512;
+int jit_build(mdp_engine *eng, int variant)
 {
-    if (!eng->jit_code[fused].empty()) return MDP_OK;
+    const bool fused = variant == 1;
+    if (!eng->jit_code[variant].empty()) return MDP_OK;
     MdpJitPlan plan = eng->jit_plan;
     plan.fused = fused;
+    if (variant == 2) {  // the reading kernel's points per lane, more threads
+        plan.epl = eng->jit_epl > 0 ? eng->jit_epl : mdp_jit_default_epl(plan.udesc);
+        plan.kblock = kJitKblockTall;
+        const std::string src = mdp_jit_forward_source(plan);
+        if (mdp_jit_compile(src, eng->jit_code[2], eng->jit_log) != 0)
+            return mdp_set_error(MDP_EHIP, "hipRTC compilation of the forward kernel failed: %s", eng->jit_log.c_str());
+        eng->jit_src[2] = src;
+        return MDP_OK;
+    }
     // the reading variant's shape (e rows per block = kblock x epl, which
     // set_grid_dev's block count uses before it picks the variant)
     const int epl_r = plan.epl > 0 ? plan.epl : mdp_jit_default_epl(plan.udesc);
@@ -2541,10 +2557,10 @@ int jit_build(mdp_engine *eng, bool fused)
             fclose(f);
         }
     }
-    if (mdp_jit_compile(src, eng->jit_code[fused], eng->jit_log) != 0)
+    if (mdp_jit_compile(src, eng->jit_code[variant], eng->jit_log) != 0)
         return mdp_set_error(MDP_EHIP, "hipRTC compilation of the forward kernel failed: %s",
                              eng->jit_log.c_str());
-    eng->jit_src[fused] = src;
+    eng->jit_src[variant] = src;
     return MDP_OK;
 }
 
@@ -2609,8 +2625,8 @@ hipError_t load_module(std::vector<char> &code, const std::string &src, hipModul
     return hipModuleLoadData(m, code.data());
 }
 
-// Load a forward kernel variant into the device (compiling it if needed).
-int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
+// Load a forward kernel variant (jit_build's) into the device, compiling it if needed.
+int jit_load(mdp_engine *eng, DevCtx &d, int variant)
 {
     if (!eng->chunks.empty()) {  // a long series: its chunk kernels (never fused)
         const size_t nch = eng->chunks.size();
@@ -2654,20 +2670,20 @@ int jit_load(mdp_engine *eng, DevCtx &d, bool fused)
         d.cqidx = std::move(qidx);
         return MDP_OK;
     }
-    if (d.jit_fn[fused]) return MDP_OK;
-    int rc = jit_build(eng, fused);
+    if (d.jit_fn[variant]) return MDP_OK;
+    int rc = jit_build(eng, variant);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(d.device));
     hipModule_t m = nullptr;
     hipFunction_t f = nullptr;
-    HIP_TRY(load_module(eng->jit_code[fused], eng->jit_src[fused], &m));
+    HIP_TRY(load_module(eng->jit_code[variant], eng->jit_src[variant], &m));
     const hipError_t e = hipModuleGetFunction(&f, m, "mdp_fwd_jit");
     if (e != hipSuccess) {
         (void)hipModuleUnload(m);
         return mdp_set_error(MDP_EHIP, "hipModuleGetFunction(mdp_fwd_jit) failed: %s", hipGetErrorString(e));
     }
-    d.jit_mod[fused] = m;
-    d.jit_fn[fused] = f;
+    d.jit_mod[variant] = m;
+    d.jit_fn[variant] = f;
     return MDP_OK;
 }
 
@@ -2924,7 +2940,12 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         const uint32_t gy = (nl + eng->jit_kblock * eng->jit_epl - 1) / (eng->jit_kblock * eng->jit_epl);
         d.fused = eng->chunks.empty() && !eng->qglobal && !eng->jit_plan.vlds && fused_lds(eng, d.ct_len) <= kFusedLdsMax &&
                   d.zs_kmax <= eng->jit_plan.kzmax && (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
-        if ((rc = jit_load(eng, d, d.fused))) return rc;
+        // a column of a tall grid (an even number of e blocks, so no lane more
+        // idles) in half the blocks of twice the threads: each block stages
+        // its column's Q row once (config 3: forward 45.7-46.9 -> 44.3 us)
+        d.tall = !d.fused && eng->chunks.empty() && !eng->jit_plan.vlds && !eng->jit_shape_env &&
+                 eng->jit_kblock * 2 == (uint32_t)kJitKblockTall && gy >= 2 && gy % 2 == 0;
+        if ((rc = jit_load(eng, d, d.fused ? 1 : d.tall ? 2 : 0))) return rc;
         if (!eng->chunks.empty()) {  // the state vectors handed between chunks
             d.ldv = gy * eng->jit_kblock * (uint32_t)eng->jit_epl;
             uint32_t nb = 1;  // most states at a chunk boundary
@@ -3015,7 +3036,7 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, OutStrid
         const uint32_t *qidx = nullptr;
         uint32_t se = os.se, sc = os.sc;
         // threads per e block: kb (x 2 with the split state-vector kernel)
-        const uint32_t kb = d.fused ? eng->jit_kblock_fused : eng->jit_kblock;
+        const uint32_t kb = d.fused ? eng->jit_kblock_fused : d.tall ? (uint32_t)kJitKblockTall : eng->jit_kblock;
         const uint32_t pro = d.fused ? eng->jit_pro_fused : 1u;
         const uint32_t epl = d.fused ? (uint32_t)eng->jit_epl_fused : (uint32_t)eng->jit_epl;
         const uint32_t spl = eng->jit_plan.vlds && (eng->jit_plan.vsplit == 2 || eng->jit_plan.vsplit == 4)
@@ -3049,10 +3070,10 @@ int launch_forward(const mdp_engine *eng, const DevCtx &d, double *out, OutStrid
             return MDP_OK;
         }
         const uint32_t dyn = d.fused ? (d.ct_len + 2) * (uint32_t)sizeof(double) : 0u;  // + staging scratch
-        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused], (uint32_t)(nb * kb * fc * spl * pro), 1, 1, kb * fc * spl * pro, 1, 1, dyn,
-                                         s, args,
-                                         nullptr, t_kev.start, t_kev.stop, 0));
+        HIP_TRY(hipExtModuleLaunchKernel(d.jit_fn[d.fused ? 1 : d.tall ? 2 : 0], (uint32_t)(nb * kb * fc * spl * pro), 1, 1,
+                                         kb * fc * spl * pro, 1, 1, dyn, s, args, nullptr, t_kev.start, t_kev.stop, 0));
         note_launch(eng, "mdp_fwd_jit<%s,maxA%u>", d.fused ? "fused" : "reading", eng->maxA);
+        if (d.tall) note_launch(eng, "mdp_fwd_jit<reading,kb%d>", kJitKblockTall);
         return MDP_OK;
     }
     switch (eng->variant / 100) {

@@ -424,9 +424,14 @@ def test_config2_full_grid_nested(golden):
 
 
 def test_config3_full_grid_sampled(golden):
+    """Config 3's 1024^2 grid, sampled against the oracle: the reading kernel
+    at 512 threads (a column of a tall grid in one block), after k_qrows."""
     model = mdp.Model.load(golden / "config3_256x200.txt")
     g, win = mdp.grid(1024)
-    got = gpu_grid(model, g)
+    with mdp.Engine(model) as eng:
+        got = eng.loglik_grid(g, g)
+        launched = eng.launched()
+    assert "mdp_fwd_jit<reading,kb512>" in launched, launched
     assert np.isfinite(got).any()
     rng = np.random.default_rng(7)
     ie, ic = rng.integers(0, 1024, 160), rng.integers(0, 1024, 160)
