@@ -22,6 +22,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include "cli_exit.h"
 #include "midaspom.h"
 
 static double now_s(void)
@@ -179,16 +180,8 @@ int main(int argc, char **argv)
      * timing the process on the same clock attributes the wall outside main
      * (exec, loader, library constructors; exit handlers, runtime teardown) */
     if (timing) fprintf(stderr, "midaspom clock (s): main_entry %.6f main_return %.6f\n", t_start, now_s());
-    /* Leave without the HIP runtime's exit-time teardown (its static
-     * destructors release every queue and allocation one by one: 40-120 ms
-     * measured after main returned, more than the whole grid on config 1);
-     * the posterior file is closed and stdout is flushed here, and the
-     * kernel driver frees the process's device state on exit either way.
-     * MIDASPOM_FULL_EXIT=1 returns from main instead. */
-    if (!(getenv("MIDASPOM_FULL_EXIT") && atoi(getenv("MIDASPOM_FULL_EXIT")) != 0)) {
-        fflush(stdout);
-        fflush(stderr);
-        _exit(0);
-    }
+    /* the posterior file is closed: leave without the HIP runtime's
+     * exit-time teardown unless a tool needs the exit handlers (cli_exit.h) */
+    mdp_cli_leave(0);
     return 0;
 }

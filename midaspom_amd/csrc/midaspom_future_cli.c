@@ -26,6 +26,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include "cli_exit.h"
 #include "midaspom.h"
 
 struct range {
@@ -196,12 +197,8 @@ int main(int argc, char **argv)
     free(lik);
     mdp_free(pend);
     mdp_free(post);
-    /* without the HIP runtime's exit-time teardown (midaspom_cli.c);
-     * MIDASPOM_FULL_EXIT=1 returns from main instead */
-    if (!(getenv("MIDASPOM_FULL_EXIT") && atoi(getenv("MIDASPOM_FULL_EXIT")) != 0)) {
-        fflush(stdout);
-        fflush(stderr);
-        _exit(0);
-    }
+    /* without the HIP runtime's exit-time teardown unless a tool needs the
+     * exit handlers (cli_exit.h) */
+    mdp_cli_leave(0);
     return 0;
 }

@@ -2875,6 +2875,13 @@ std::vector<uint32_t> point_list(const double *e, uint32_t ne, uint32_t epl)
 int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const double *c,
                  uint32_t nc)
 {
+    // c < 0 is refused: the item factors are folded as |n_b - pC_b| (k_qrows
+    // phase 2, k_witems, the fused prologue), which equals the reference's
+    // (1 - piold)(1 - pC) + piold pC (main_MIDASPOM.c:40) only for pC >= 0;
+    // at c < 0 the reference's pC = min(1, c S) is negative, not a probability
+    for (uint32_t i = 0; i < nc; ++i)
+        if (c[i] < 0.0)
+            return mdp_set_error(MDP_EINVAL, "colonisation rate c[%u] = %g < 0 (the engine takes c >= 0)", i, c[i]);
     HIP_TRY(hipSetDevice(d.device));
     int rc;
     if ((rc = dev_reserve(&d.e, &d.cap_e, ne)) || (rc = dev_reserve(&d.c, &d.cap_c, nc))) return rc;

@@ -1070,10 +1070,45 @@ const char *const kJitOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
 constexpr int kJitNOpts = 3;
 constexpr int kJitCacheFormat = 3;  // bump when the cache key or file layout changes
 
+// The compiler's file identity without loading it: the resolved path, size
+// and mtime of libhiprtc and libamd_comgr next to the HIP runtime this
+// library runs on (located by dladdr), plus LD_LIBRARY_PATH, which can make
+// the dlopen in hiprtc_api() find another libhiprtc.  A comgr / hipRTC
+// hotfix without a runtime version bump then changes the key.
+const std::string &toolchain_identity()
+{
+    static std::once_flag once;
+    static std::string id;
+    std::call_once(once, [] {
+        Dl_info di{};
+        std::string dir;
+        if (dladdr((const void *)&hipRuntimeGetVersion, &di) && di.dli_fname) {
+            dir = di.dli_fname;
+            const size_t sl = dir.rfind('/');
+            dir = sl == std::string::npos ? std::string(".") : dir.substr(0, sl);
+        }
+        for (const char *lib : {"libhiprtc.so.7", "libamd_comgr.so.3"}) {
+            const std::string p = dir + "/" + lib;
+            struct stat st{};
+            char real[4096];
+            id += lib;
+            if (!dir.empty() && stat(p.c_str(), &st) == 0) {
+                id += ' ';
+                id += realpath(p.c_str(), real) ? real : p.c_str();
+                id += ' ' + std::to_string((long long)st.st_size) + ' ' + std::to_string((long long)st.st_mtime);
+            }
+            id += ';';
+        }
+        if (const char *lp = getenv("LD_LIBRARY_PATH")) (id += " ldpath ") += lp;
+    });
+    return id;
+}
+
 // Cache key: the generated source, the compile options, the ROCm release
 // (the HIP runtime's version, which hipRTC ships with -- asking hipRTC itself
-// would load it on every run) and the cache format.  A code object built by
-// another toolchain or with other options therefore lands under another name.
+// would load it on every run), the compiler libraries' file identity and the
+// cache format.  A code object built by another toolchain or with other
+// options therefore lands under another name.
 uint64_t jit_key(const std::string &src)
 {
     int rt = 0;
@@ -1082,7 +1117,7 @@ uint64_t jit_key(const std::string &src)
     k += '\0';
     for (const char *o : kJitOpts) (k += o) += ' ';
     k += "hip " + std::to_string(rt) + " headers " + std::to_string(HIP_VERSION) + " format " +
-         std::to_string(kJitCacheFormat);
+         std::to_string(kJitCacheFormat) + " tools " + toolchain_identity();
     return fnv1a(k);
 }
 

@@ -240,6 +240,20 @@ def test_structural_zeros_exact(golden, engine_path):
     assert_loglik_close(got, ref)
 
 
+def test_negative_c_refused(golden):
+    """c < 0 is refused with MDP_EINVAL (include/midaspom.h): the item factors
+    |n - pC| equal the reference's (1 - piold)(1 - pC) + piold pC
+    (main_MIDASPOM.c:40) only for pC = min(1, c S) >= 0."""
+    model = mdp.Model.load(golden / "occupancies.txt")
+    g, _ = mdp.grid(5)
+    with mdp.Engine(model) as eng:
+        with pytest.raises(_lib.MidaspomError, match=r"c\[1\] = -0.25 < 0"):
+            eng.loglik_grid(g, np.array([0.0, -0.25, 0.5]))
+        with pytest.raises(_lib.MidaspomError):
+            eng.set_grid(g, -g[1:])
+        assert np.isfinite(eng.loglik_grid(g, g)[1:, 1:]).all()  # the engine stays usable
+
+
 def test_single_year_and_constant_series(engine_path):
     for obs in (np.array([[1, 0, -1, 1]]), np.array([[0, 1, 1]] * 6), np.array([[1], [1], [0], [1]])):
         model = mdp.Model.from_obs(obs)
