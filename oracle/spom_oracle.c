@@ -248,16 +248,33 @@ static void ws_free(orc_ws *w)
 }
 
 /* naive row-major C = A(MxK) * B(KxN), ascending-k accumulation (the CBLAS
- * call sites :363 and :379 with alpha=1, beta=0). */
+ * call sites :363 and :379 with alpha=1, beta=0).  Every C[i][j] is
+ * 0.0 + A[i][0] B[0][j] + A[i][1] B[1][j] + ... in ascending k, as the
+ * textbook i-j-k loop sums it; the loops run i-k-j (rows of B streamed) and
+ * skip a term whose A[i][k] is exactly 0 when row k of B is finite: it adds
+ * +-0.0 to a sum that started at +0.0, which changes no bit.  Pe is zero
+ * outside j <= a (compPePc, :18-50), so at 2^10 hidden states this is ~20x
+ * fewer terms (round 6: 1024-state years in the GPU parity tests). */
 static void naive_gemm(unsigned M, unsigned N, unsigned K, const double *A, unsigned lda,
                        const double *B, unsigned ldb, double *C, unsigned ldc)
 {
-    for (unsigned i = 0; i < M; i++)
-        for (unsigned j = 0; j < N; j++) {
-            double acc = 0.0;
-            for (unsigned k = 0; k < K; k++) acc += A[(size_t)i * lda + k] * B[(size_t)k * ldb + j];
-            C[(size_t)i * ldc + j] = acc;
+    unsigned char *fin = (unsigned char *)malloc(K ? K : 1);
+    for (unsigned k = 0; k < K; k++) {
+        unsigned char f = 1;
+        for (unsigned j = 0; j < N; j++) f &= isfinite(B[(size_t)k * ldb + j]) ? 1 : 0;
+        if (fin) fin[k] = f;
+    }
+    for (unsigned i = 0; i < M; i++) {
+        double *c = C + (size_t)i * ldc;
+        for (unsigned j = 0; j < N; j++) c[j] = 0.0;
+        for (unsigned k = 0; k < K; k++) {
+            const double a = A[(size_t)i * lda + k];
+            if (a == 0.0 && fin && fin[k]) continue;
+            const double *b = B + (size_t)k * ldb;
+            for (unsigned j = 0; j < N; j++) c[j] += a * b[j];
         }
+    }
+    free(fin);
 }
 
 static double point_loglik(const orc_model *md, orc_ws *w, double e, double c)
@@ -296,16 +313,23 @@ static double point_loglik(const orc_model *md, orc_ws *w, double e, double c)
     }
     naive_gemm(ne, ne, ns, w->Pe, ns, w->Pc, ne, w->P, ne);
 
-    /* forward propagation, Q3 semantics: row 0 of Pold = ones, other rows 0 */
+    /* forward propagation, Q3 semantics: row 0 of Pold = ones, other rows 0.
+     * With every P entry finite the zero rows stay exactly +0.0 (0 * P
+     * summed from +0.0) and add +0.0 to L, so only row 0 is propagated (the
+     * same bits; at 2^10 states in year 0 the full loop is 10^9 terms a year) */
     const unsigned np0 = md->np[0];
     unsigned npprev = np0;
+    int pfin = 1;
+    for (size_t q = 0; q < (size_t)ne * ne && pfin; q++) pfin = isfinite(w->P[q]);
+    const unsigned nrows = pfin ? 1 : np0;
     memset(w->vold, 0, sizeof(double) * (size_t)np0 * np0);
     for (unsigned q = 0; q < np0; q++) w->vold[q] = 1;
     for (unsigned t = 1; t < md->tmax; t++) {
         const unsigned npt = md->np[t];
         const unsigned *sp = md->simp + md->yoff[t - 1];
         const unsigned *sc = md->simp + md->yoff[t];
-        for (unsigned r = 0; r < np0; r++)
+        if (nrows < np0) memset(w->vnew, 0, sizeof(double) * (size_t)np0 * npt);
+        for (unsigned r = 0; r < nrows; r++)
             for (unsigned l = 0; l < npt; l++) {
                 double acc = 0.0;
                 for (unsigned k = 0; k < npprev; k++)
