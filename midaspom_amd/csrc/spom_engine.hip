@@ -1495,6 +1495,231 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     }
 }
 
+// k_fwd_mmt<RT> (round 6): the same per-year GEMM as k_fwd_mma, for years of
+// up to 1 024 states, with three changes.
+//  * One state buffer in LDS, V[ROWS][PTS] (128 KiB: 256 x 64, 512 x 32 or
+//    1 024 x 16), instead of two: a wave keeps its tiles' new states in
+//    registers until every wave has read the year's old ones (a barrier),
+//    then stores them in place.  So 1 024-state years fit, and years of up to
+//    256 states take 64 points a block (RT = 4 point tiles share each C
+//    gather) where k_fwd_mma took 32.
+//  * K lists per (year, column tile): the entry (k, m) only for m <= the
+//    largest nX over the tile's 16 new states (k_fwd_mma ran m up to |A_k|
+//    for every tile and multiplied the rest through zero slots).
+//  * A wave may own up to TMAX = 4 / RT tiles of a year (years of more than
+//    256 states: 17-64 tiles over 16 waves, dealt longest-list first); years
+//    of at most 8 tiles split each tile's K list into S slices as before, the
+//    partial products parked in rows past the year's tiles and summed in
+//    slice order after a second barrier (deterministic).
+// Workgroups are dealt XCD-aware (the point blocks of one column on one XCD,
+// so the column's Q row is gathered from that XCD's L2).  The products sum
+// in another order than k_fwd_wide's (positive terms: ~1e-15 relative).
+constexpr uint32_t kMmtU = 2;           // K steps (of 4 entries) per pipeline chunk
+constexpr uint32_t kMmtMaxTiles = 64;   // column tiles a year (1 024 states)
+constexpr uint32_t mmt_pts(uint32_t rt) { return 16u * rt; }
+constexpr uint32_t mmt_rows(uint32_t rt) { return 1024u / rt; }
+constexpr uint32_t mmt_ps(uint32_t rt) { return 16u * rt + 8u; }  // power-table row stride (doubles)
+template <int RT>  // point tiles of 16 per block: 4 (<= 256 states), 2 (<= 512), 1 (<= 1 024)
+__global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
+    const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint2 *__restrict__ kt,
+    const uint2 *__restrict__ ktile, const uint32_t *__restrict__ desc, const uint32_t *__restrict__ dbase,
+    const uint2 *__restrict__ wplan, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
+    uint32_t maxA, uint32_t zslot, double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
+{
+    constexpr uint32_t PTS = mmt_pts(RT), ROWS = mmt_rows(RT), PS = mmt_ps(RT), TMAX = 4 / RT;
+    extern __shared__ __attribute__((aligned(16))) double mlds[];
+    double *V = mlds;  // [state][point]
+    double *xp = V + (size_t)ROWS * PTS, *yp = xp + (size_t)(maxA + 1) * PS;  // [r][point]
+    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-aware: workgroups are dealt round-robin over the 8 XCDs; XCD x
+    // takes a contiguous range of logical blocks, i.e. whole columns
+    const uint32_t npb = (ne + PTS - 1) / PTS, full = gridDim.x & ~7u, b = blockIdx.x;
+    const uint32_t lb = b < full ? (b & 7u) * (full >> 3) + (b >> 3) : b;
+    const uint32_t p0 = (lb % npb) * PTS, ic = lb / npb;
+    if (threadIdx.x < PTS) {
+        const uint32_t ie = p0 + threadIdx.x;
+        const double e = ie < ne ? evals[ie] : 0.0;
+        const double x = e > 1.0 ? 1.0 : e, y = 1.0 - x;
+        double a = 1.0, c = 1.0;
+        for (uint32_t r = 0; r <= maxA; ++r) {
+            xp[r * PS + threadIdx.x] = a;
+            yp[r * PS + threadIdx.x] = c;
+            a *= x;
+            c *= y;
+        }
+    }
+    const uint32_t np0 = np[0];
+    for (uint32_t i = threadIdx.x; i < ROWS * PTS; i += kMmaThreads) V[i] = i / PTS < np0 ? 1.0 : 0.0;
+    __syncthreads();
+    const double *q = Q + (size_t)ic * ldQ;
+    const uint32_t kk = lane >> 4, col = lane & 15u;
+    struct Item {
+        uint32_t tile, ks, S, cb, ce, nch, sh, lc4, npcp, ncol;
+        bool active;
+        const uint2 *kl;
+        const uint32_t *dt;
+    };
+    // item i of this wave in year t (host table mmt_wplan: no divisions here)
+    auto plan = [&](uint32_t t, uint32_t i) {
+        Item it;
+        it.ncol = (np[t] + 15) / 16;
+        it.npcp = it.ncol * 16;
+        const uint2 wp = wplan[(t * 16 + wv) * TMAX + i];
+        it.cb = wp.x & 0xffffu;
+        it.ce = wp.x >> 16;
+        it.tile = wp.y & 0xffu;
+        it.ks = (wp.y >> 8) & 0xffu;
+        it.S = (wp.y >> 16) & 0xffu;
+        it.active = (wp.y >> 24) != 0u;
+        const uint2 kt2 = ktile[t * kMmtMaxTiles + it.tile];
+        it.kl = kt + __builtin_amdgcn_readfirstlane(kt2.x);
+        it.nch = kt2.y;
+        it.sh = 32u - (uint32_t)__builtin_clz(it.npcp - 1u);  // descriptor rows [k][2^sh >= npcp]
+        it.lc4 = (it.tile * 16 + col) << 2;
+        it.dt = desc + __builtin_amdgcn_readfirstlane(dbase[t]);
+        return it;
+    };
+    // K entry (uint2): x = V row byte offset (18 bits) | y^m row offset << 18;
+    // y = x^(|A|-m) row offset (16 bits) | m << 16 | k << 21 (k = npp: the
+    // descriptor row of absent transitions, which the padding names)
+    auto kent = [&](const Item &it, uint32_t ch, uint32_t u) {
+        const uint32_t c = ch < it.nch ? ch : it.nch - 1;
+        return it.kl[(c * kMmtU + u) * 4 + kk];
+    };
+    auto dsc = [&](const Item &it, uint2 en) {
+        return *(const uint32_t *)((const char *)it.dt + (((en.y >> 21) << (it.sh + 2)) + it.lc4));
+    };
+    auto cval = [&](uint2 en, uint32_t d) {
+        const uint32_t m = (en.y >> 16) & 31u;
+        return *(const double *)((const char *)q + ((m <= ((d >> kOffBits) & 31u) ? (d & kOffMask) + m : zslot) << 3));
+    };
+    uint2 ee[4][kMmtU];
+    uint32_t dd[2][kMmtU];
+    double bb[2][kMmtU];
+    auto prime_a = [&](const Item &it) {
+#pragma unroll
+        for (uint32_t u = 0; u < kMmtU; ++u) {
+            ee[0][u] = kent(it, it.cb, u);
+            ee[1][u] = kent(it, it.cb + 1, u);
+            ee[2][u] = kent(it, it.cb + 2, u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kMmtU; ++u) {
+            dd[0][u] = dsc(it, ee[0][u]);
+            dd[1][u] = dsc(it, ee[1][u]);
+        }
+    };
+    auto prime_b = [&]() {
+#pragma unroll
+        for (uint32_t u = 0; u < kMmtU; ++u) bb[0][u] = cval(ee[0][u], dd[0][u]);
+    };
+    Item cur = plan(tmax > 1 ? 1u : 0u, 0);
+    if (tmax > 1 && cur.active) {
+        prime_a(cur);
+        prime_b();
+    }
+    for (uint32_t t = 1; t < tmax; ++t) {
+        mdp_d4 acc[TMAX][RT];
+        const Item first = cur;
+#pragma unroll
+        for (uint32_t i = 0; i < TMAX; ++i) {
+#pragma unroll
+            for (uint32_t h = 0; h < RT; ++h) acc[i][h] = mdp_d4{0.0, 0.0, 0.0, 0.0};
+            if (i > 0) {
+                cur = plan(t, i);
+                if (!cur.active) break;  // a wave's items are its first ones
+                prime_a(cur);
+                prime_b();
+            }
+            if (!cur.active) break;
+            mdp_d4(&ac)[RT] = acc[i];  // (i is a constant once unrolled)
+            // one chunk at ring position j: the K entries of ch + 3, the
+            // descriptors of ch + 2, the C values of ch + 1, then ch's products
+            auto chunk = [&](uint32_t ch, auto jc) {
+                constexpr uint32_t j = decltype(jc)::value;
+#pragma unroll
+                for (uint32_t u = 0; u < kMmtU; ++u) ee[(j + 3) & 3][u] = kent(cur, ch + 3, u);
+#pragma unroll
+                for (uint32_t u = 0; u < kMmtU; ++u) dd[j & 1][u] = dsc(cur, ee[(j + 2) & 3][u]);
+#pragma unroll
+                for (uint32_t u = 0; u < kMmtU; ++u) bb[(j + 1) & 1][u] = cval(ee[(j + 1) & 3][u], dd[(j + 1) & 1][u]);
+#pragma unroll
+                for (uint32_t u = 0; u < kMmtU; ++u) {
+                    const uint2 en = ee[j][u];
+#pragma unroll
+                    for (uint32_t h = 0; h < RT; ++h) {
+                        const uint32_t pb = (h * 16 + col) * 8u;
+                        const double wt = *(const double *)((const char *)xp + (en.y & 0xffffu) + pb) *
+                                          *(const double *)((const char *)yp + (en.x >> 18) + pb);
+                        const double av = *(const double *)((const char *)V + (en.x & 0x3ffffu) + pb) * wt;
+                        ac[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(bb[j & 1][u], av, ac[h], 0, 0, 0);
+                    }
+                }
+            };
+            uint32_t ch = cur.cb;
+            for (; ch + 4 <= cur.ce; ch += 4) {
+                chunk(ch, std::integral_constant<uint32_t, 0>{});
+                chunk(ch + 1, std::integral_constant<uint32_t, 1>{});
+                chunk(ch + 2, std::integral_constant<uint32_t, 2>{});
+                chunk(ch + 3, std::integral_constant<uint32_t, 3>{});
+            }
+            if (ch < cur.ce) chunk(ch, std::integral_constant<uint32_t, 0>{});
+            if (ch + 1 < cur.ce) chunk(ch + 1, std::integral_constant<uint32_t, 1>{});
+            if (ch + 2 < cur.ce) chunk(ch + 2, std::integral_constant<uint32_t, 2>{});
+        }
+        // next year's first item: K entries and descriptors in flight across
+        // this year's barriers, its first C values after them
+        const Item nxt = plan(t + 1 < tmax ? t + 1 : t, 0);
+        const bool pnext = t + 1 < tmax && nxt.active;
+        if (pnext) prime_a(nxt);
+        __syncthreads();  // every wave has read the year's old states
+        // the lane's accumulators: states tile * 16 + kk + 4 r of point
+        // h * 16 + col; slices ks >= 1 park theirs past row npcp
+        auto part = [&](uint32_t ks, uint32_t tile) {
+            return V + (size_t)(first.npcp + ((ks - 1) * first.ncol + tile) * 16) * PTS + lane;
+        };
+        if (first.S > 1) {
+            if (first.active && first.ks >= 1) {
+                double *pk = part(first.ks, first.tile);
+#pragma unroll
+                for (uint32_t h = 0; h < RT; ++h)
+#pragma unroll
+                    for (uint32_t r = 0; r < 4; ++r) pk[(h * 4 + r) * 64] = acc[0][h][r];
+            }
+            __syncthreads();
+            if (first.active && first.ks == 0)
+                for (uint32_t j = 1; j < first.S; ++j) {
+                    const double *pj = part(j, first.tile);
+#pragma unroll
+                    for (uint32_t h = 0; h < RT; ++h)
+#pragma unroll
+                        for (uint32_t r = 0; r < 4; ++r) acc[0][h][r] = acc[0][h][r] + pj[(h * 4 + r) * 64];
+                }
+            // (the final stores below go to rows < npcp: no partial is overwritten)
+        }
+        // (padded states l >= npc hold 0: their C values are the zero slot)
+#pragma unroll
+        for (uint32_t i = 0; i < TMAX; ++i) {
+            const Item it = i == 0 ? first : plan(t, i);
+            if (!it.active || it.ks != 0) break;
+            double *dst = V + (size_t)(it.tile * 16 + kk) * PTS + col;
+#pragma unroll
+            for (uint32_t h = 0; h < RT; ++h)
+#pragma unroll
+                for (uint32_t r = 0; r < 4; ++r) dst[(size_t)(4 * r) * PTS + h * 16] = acc[i][h][r];
+        }
+        if (pnext) prime_b();
+        __syncthreads();
+        cur = nxt;
+    }
+    if (threadIdx.x < PTS) {
+        const uint32_t ie = p0 + threadIdx.x, npl = np[tmax - 1];
+        double L = 0.0;
+        for (uint32_t l = 0; l < npl; ++l) L += V[l * PTS + threadIdx.x] * prior0;
+        if (ie < ne) out[(size_t)ie * ld_out + (size_t)ic * out_cs] = log(L);
+    }
+}
+
 typedef const __attribute__((address_space(4))) uint32_t cuint;
 
 // Forward recursion with the state vectors in HBM: lane per e value, one c
@@ -1673,6 +1898,8 @@ struct DevCtx {
     uint32_t *np_d = nullptr, *udesc_w = nullptr;
     uint2 *mma_kt = nullptr, *mma_wplan = nullptr;
     uint32_t *mma_kbase = nullptr, *mma_desc = nullptr, *mma_dbase = nullptr;
+    uint2 *mmt_kt = nullptr, *mmt_ktile = nullptr, *mmt_wplan = nullptr;  // k_fwd_mmt tables
+    uint32_t *mmt_desc = nullptr, *mmt_dbase = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     std::vector<uint8_t> ev_mask;  // per profiled run: slots whose kernel was launched
@@ -1804,6 +2031,14 @@ struct mdp_engine {
     std::vector<uint2> mma_wplan;  // per (year, wave) its work item (chunk range, column tile, slice)
     std::vector<uint32_t> mma_kbase, mma_desc, mma_dbase;
     uint32_t mma_ktmax = 16;
+    // k_fwd_mmt (round 6, the default matrix-core forward: years of up to
+    // 1 024 states): RT point tiles a block, per (year, tile) K lists, per
+    // (year, wave) work items (build_mmt_plan)
+    bool mmt = false;
+    uint32_t mmt_rt = 0;
+    std::vector<uint2> mmt_kt, mmt_ktile, mmt_wplan;
+    std::vector<uint32_t> mmt_desc, mmt_dbase;
+    double mmt_flops_pt = 0;  // executed MFMA flops per grid point (padding included)
     uint32_t qslot_lglmax = 0;      // log2 of the widest lane segment
     std::vector<uint8_t> isvar;
     std::vector<double> Sj;  // [nj][n] colonisation sums of every column for each needed j
@@ -2294,6 +2529,110 @@ size_t device_lds_max()
     return 160 * 1024;
 }
 
+// k_fwd_mmt: the state buffer and the power tables of the block's points
+size_t mmt_lds(const mdp_engine *eng)
+{
+    const uint32_t rt = eng->mmt_rt;
+    return ((size_t)mmt_rows(rt) * mmt_pts(rt) + 2 * ((size_t)eng->maxA + 1) * mmt_ps(rt)) * sizeof(double);
+}
+
+const void *mmt_kernel(const mdp_engine *eng)
+{
+    if (eng->mmt_rt == 4) return (const void *)k_fwd_mmt<4>;
+    if (eng->mmt_rt == 2) return (const void *)k_fwd_mmt<2>;
+    return (const void *)k_fwd_mmt<1>;
+}
+
+// k_fwd_mmt's tables (c-independent): years of at most 1 024 states.
+//  * per year the transition descriptors [k][2^sh >= npcp] (Q-row offset |
+//    nX << kOffBits; an absent transition -- and the row k = npp the padding
+//    names -- the zero slot with nX = 0);
+//  * per (year, column tile) its K entries: every source k with m = 0 ..
+//    the largest nX over the tile's new states (the rest of m <= |A_k| would
+//    meet only zero slots), padded to whole pipeline chunks;
+//  * per (year, wave) up to 4 / RT work items: tiles of years of more than
+//    8 tiles dealt longest list first to the least-loaded wave; smaller years
+//    split each tile's list into S slices (at least two chunks each) over
+//    up to 16 waves.
+void build_mmt_plan(mdp_engine *eng)
+{
+    if (eng->npmax > 1024 || eng->maxA > 24 || eng->tmax < 2) return;
+    const uint32_t rt = eng->npmax <= 256 ? 4u : eng->npmax <= 512 ? 2u : 1u;
+    const uint32_t pts = mmt_pts(rt), ps = mmt_ps(rt), tmaxit = 4 / rt, cw = 4 * kMmtU;
+    const uint32_t none = (uint32_t)eng->ncoef_d;
+    if (none > kOffMask) return;
+    eng->mmt_rt = rt;
+    eng->mmt_kt.clear();
+    eng->mmt_desc.clear();
+    eng->mmt_dbase.assign(eng->tmax + 1, 0u);
+    eng->mmt_ktile.assign((size_t)(eng->tmax + 1) * kMmtMaxTiles, make_uint2(0u, 1u));
+    eng->mmt_wplan.assign((size_t)(eng->tmax + 1) * 16 * tmaxit, make_uint2(0u, 0u));
+    double fl = 0.0;
+    size_t ub = 0;
+    for (uint32_t t = 1; t < eng->tmax; ++t) {
+        const uint32_t npp = eng->np[t - 1], npc = eng->np[t], ncol = (npc + 15) / 16, npcp = ncol * 16;
+        const uint32_t *ud = eng->udesc_d.data() + ub;  // ud[l * npp + k]
+        uint32_t ld = 16;
+        while (ld < npcp) ld *= 2;
+        eng->mmt_dbase[t] = (uint32_t)eng->mmt_desc.size();
+        for (uint32_t k = 0; k <= npp; ++k)
+            for (uint32_t l = 0; l < ld; ++l) {
+                uint32_t dv = none;
+                if (k < npp && l < npc) dv = (ud[(size_t)l * npp + k] & kOffMask) | (((ud[(size_t)l * npp + k] >> kOffBits) & 31u) << kOffBits);
+                eng->mmt_desc.push_back(dv);
+            }
+        std::vector<uint32_t> nch(ncol);
+        for (uint32_t tile = 0; tile < ncol; ++tile) {
+            const size_t start = eng->mmt_kt.size();
+            const uint32_t l1 = std::min(16 * tile + 16, npc);
+            for (uint32_t k = 0; k < npp; ++k) {
+                const uint32_t a = ud[k] >> 27;  // |A_k|
+                uint32_t mx = 0;
+                for (uint32_t l = 16 * tile; l < l1; ++l) mx = std::max(mx, (ud[(size_t)l * npp + k] >> kOffBits) & 31u);
+                for (uint32_t m = 0; m <= mx; ++m)  // V row k, y^m row, x^(a-m) row (bytes); m; k
+                    eng->mmt_kt.push_back(make_uint2((k * pts * 8u) | ((m * ps * 8u) << 18),
+                                                     ((a - m) * ps * 8u) | (m << 16) | (k << 21)));
+            }
+            while ((eng->mmt_kt.size() - start) % cw) eng->mmt_kt.push_back(make_uint2(0u, npp << 21));
+            nch[tile] = (uint32_t)((eng->mmt_kt.size() - start) / cw);
+            eng->mmt_ktile[(size_t)t * kMmtMaxTiles + tile] = make_uint2((uint32_t)start, nch[tile]);
+            fl += 2.0 * 16.0 * (double)(eng->mmt_kt.size() - start);
+        }
+        uint2 *wp = eng->mmt_wplan.data() + (size_t)t * 16 * tmaxit;
+        if (ncol <= 16) {
+            uint32_t S = 1;
+            if (ncol <= 8) S = std::max(1u, std::min(16 / ncol, *std::min_element(nch.begin(), nch.end()) / 2));
+            for (uint32_t wv = 0; wv < 16; ++wv) {
+                const uint32_t tile = wv % ncol, ks = wv / ncol;
+                const bool on = wv < ncol * S;
+                const uint32_t cb = on ? nch[tile] * ks / S : 0, ce = on ? nch[tile] * (ks + 1) / S : 0;
+                for (uint32_t i = 0; i < tmaxit; ++i)
+                    wp[wv * tmaxit + i] = make_uint2(i ? 0u : cb | ce << 16,
+                                                     (i ? 0u : tile | ks << 8) | S << 16 | (!i && on ? 1u : 0u) << 24);
+            }
+        } else {
+            std::vector<uint32_t> order(ncol), cnt(16, 0);
+            std::vector<uint64_t> load(16, 0);
+            for (uint32_t i = 0; i < ncol; ++i) order[i] = i;
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return nch[x] > nch[y]; });
+            for (uint32_t wv = 0; wv < 16; ++wv)
+                for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, 1u << 16);
+            for (uint32_t tile : order) {
+                uint32_t best = 16;
+                for (uint32_t wv = 0; wv < 16; ++wv)
+                    if (cnt[wv] < tmaxit && (best == 16 || load[wv] < load[best])) best = wv;
+                wp[best * tmaxit + cnt[best]++] = make_uint2(nch[tile] << 16, tile | 1u << 16 | 1u << 24);
+                load[best] += nch[tile];
+            }
+        }
+        ub += (size_t)npp * npc;
+    }
+    for (uint32_t i = 0; i < cw; ++i) eng->mmt_kt.push_back(make_uint2(0u, 0u));
+    if (eng->mmt_desc.empty()) eng->mmt_desc.push_back(none);
+    eng->mmt_flops_pt = fl + 2.0 * (eng->maxA + 1) + (double)eng->np[eng->tmax - 1];
+    eng->mmt = mmt_lds(eng) <= device_lds_max() && eng->mmt_kt.size() < 0xffffffffu;
+}
+
 int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
 {
     int rc = build_direct_plan(eng, p);
@@ -2309,10 +2648,15 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
     // entries naming the descriptor row npp (every transition absent), and the
     // transition descriptors [k][2^sh >= npcp] (Q-row offset | nX << kOffBits;
     // an absent transition names the zero slot with nX = 0)
+    // MDP_WIDE_MMA: 0 -> k_fwd_wide; 1 -> round 5's k_fwd_mma (<= 256
+    // states); unset / 2 -> k_fwd_mmt (<= 1 024 states)
+    const char *mv = eng->opts.get("MDP_WIDE_MMA");
+    const int mmode = mv ? atoi(mv) : 2;
+    eng->mmt = false;
+    if (mmode == 2) build_mmt_plan(eng);
     eng->mma = false;
     if (eng->npmax <= 256 && eng->maxA <= 24) {
-        const char *mv = eng->opts.get("MDP_WIDE_MMA");
-        if (!mv || atoi(mv) != 0) {
+        if (mmode == 1) {
             const uint32_t npm = eng->npmax <= 64 ? 64u : eng->npmax <= 128 ? 128u : 256u;
             const uint32_t pts = mma_pts(npm), ps = mma_ps(npm);
             const uint32_t none = (uint32_t)eng->ncoef_d;  // the zero slot, nX = 0
@@ -2795,6 +3139,13 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
                 return rc;
             if (eng->mma)
                 HIP_TRY(hipFuncSetAttribute(mma_kernel(eng), hipFuncAttributeMaxDynamicSharedMemorySize, (int)mma_lds(eng)));
+            if (eng->mmt &&
+                ((rc = dev_upload(&d.mmt_kt, eng->mmt_kt)) || (rc = dev_upload(&d.mmt_ktile, eng->mmt_ktile)) ||
+                 (rc = dev_upload(&d.mmt_wplan, eng->mmt_wplan)) || (rc = dev_upload(&d.mmt_desc, eng->mmt_desc)) ||
+                 (rc = dev_upload(&d.mmt_dbase, eng->mmt_dbase))))
+                return rc;
+            if (eng->mmt)
+                HIP_TRY(hipFuncSetAttribute(mmt_kernel(eng), hipFuncAttributeMaxDynamicSharedMemorySize, (int)mmt_lds(eng)));
             HIP_TRY(hipFuncSetAttribute((const void *)k_fwd_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)wide_lds(eng)));
             return MDP_OK;
@@ -2831,6 +3182,7 @@ void free_device(DevCtx &d)
                     d.zs, d.zsq, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
                     d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot, d.qlane, d.islot,
                     d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan,
+                    d.mmt_kt, d.mmt_ktile, d.mmt_wplan, d.mmt_desc, d.mmt_dbase,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -2921,7 +3273,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         d.wide_cb_fwd = (uint32_t)std::min(cap_c, std::max<size_t>(1, kWideVBytes / 8 / (2 * (size_t)eng->npmax * ne_pad)));
         if (const char *cv = eng->opts.get("MDP_WIDE_CB"))
             d.wide_cb_fwd = std::min(d.wide_cb_fwd, (uint32_t)std::max(1, atoi(cv)));
-        if (!eng->mma && (rc = dev_reserve(&d.V, &d.cap_v, 2 * (size_t)eng->npmax * d.wide_cb_fwd * ne_pad))) return rc;
+        if (!eng->mma && !eng->mmt && (rc = dev_reserve(&d.V, &d.cap_v, 2 * (size_t)eng->npmax * d.wide_cb_fwd * ne_pad))) return rc;
     } else if (eng->jit) {
         // forward kernels with several points per lane read them from a list
         // that puts only e rows of one ratio form in a lane (spom_jit.cpp)
@@ -3149,7 +3501,20 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
             hipLaunchKernelGGL(k_wq, gq, dim3(kBlock), 0, s, c0, eng->nitems, d.Pg, eng->ncoef_d, d.qstart, d.qitem,
                                d.Qrow, (uint32_t)eng->ldQ);
         }
-    } else if (eng->mma) {  // the matrix-core forward: every c in one launch (no HBM state scratch)
+    } else if (eng->mmt) {  // the matrix-core forward: every c in one launch, blocks dealt XCD-aware
+        const uint32_t rt = eng->mmt_rt, npb = (d.ne + mmt_pts(rt) - 1) / mmt_pts(rt);
+        const uint64_t nb = (uint64_t)npb * d.nc;
+        if (nb > 0x7fffffffull) return mdp_set_error(MDP_EUNSUPPORTED, "grid of %llu k_fwd_mmt workgroups", (unsigned long long)nb);
+        note_launch(eng, "k_fwd_mmt<%u>", rt);
+#define MDP_MMT(RT) \
+    hipLaunchKernelGGL((k_fwd_mmt<RT>), dim3((uint32_t)nb), dim3(kMmaThreads), mmt_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, \
+                       d.np_d, d.mmt_kt, d.mmt_ktile, d.mmt_desc, d.mmt_dbase, d.mmt_wplan, eng->tmax, eng->prior0, d.e, \
+                       d.ne, eng->maxA, eng->ncoef_d, out, os.se, os.sc)
+        if (rt == 4) MDP_MMT(4);
+        else if (rt == 2) MDP_MMT(2);
+        else MDP_MMT(1);
+#undef MDP_MMT
+    } else if (eng->mma) {  // round 5's matrix-core forward (MDP_WIDE_MMA=1; years of up to 256 states)
         uint32_t se = os.se, sc = os.sc;
         for (uint32_t c0 = 0; c0 < d.nc; c0 += 65535) {
             const uint32_t n = std::min(65535u, d.nc - c0);
@@ -3883,7 +4248,7 @@ int mdp_engine_kernel_ms(mdp_engine *eng, double *ms, int max_k)
 const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
     if (!eng || k < 0 || k >= 3) return "";
-    if (eng->wide) return k < 2 && !eng->nitems ? "" : k == 2 && eng->mma ? "k_fwd_mma" : kKernelNames[2][k];
+    if (eng->wide) return k < 2 && !eng->nitems ? "" : k == 2 && eng->mmt ? "k_fwd_mmt" : k == 2 && eng->mma ? "k_fwd_mma" : kKernelNames[2][k];
     if (eng->jit && eng->qglobal)  // Q rows built in HBM, then the hipRTC forward kernel
         return k < 2 && !eng->nitems ? "" : k == 2 ? "k_forward" : kKernelNames[2][k];
     // direct path: Z rows inside k_qrows (slot 0 idle); fused: one kernel
@@ -3962,7 +4327,7 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     double per_pt = (double)eng->nuses * (2.0 * (D + 1.0) + 2.0) + 3.0 * (D + 1.0) +
                     2.0 * (double)eng->npmax;
     if (eng->jit) per_pt = eng->jit_flops_pt;  // the generated code's own count
-    if (eng->wide) per_pt = eng->wide_flops_pt;
+    if (eng->wide) per_pt = eng->mmt ? eng->mmt_flops_pt : eng->wide_flops_pt;
     if (flop_impl) *flop_impl = per_pt * pts;
     // SURVEY.md §8(d) F_alg (dense-in-j formulation)
     double fwd = 0;

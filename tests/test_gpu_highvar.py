@@ -131,13 +131,13 @@ def test_generic_path(nvar, monkeypatch):
 @pytest.mark.parametrize("mma", [True, False])
 def test_wide_path(nvar, chunked, mma, monkeypatch):
     """MDP_WIDE=1: k_zrows + k_witems<NV> + k_wq + the forward on the matrix
-    cores, k_fwd_mma (or k_fwd_wide, MDP_WIDE_MMA=0), whole and one c value
+    cores, k_fwd_mmt (or k_fwd_wide, MDP_WIDE_MMA=0), whole and one c value
     per item launch."""
     _, model = _problem(nvar)
     ie, ic, ref = _reference(nvar)
     env = {"MDP_WIDE": "1", **({"MDP_WIDE_CB": "1"} if chunked else {}), **({} if mma else {"MDP_WIDE_MMA": "0"})}
     got, launched, info = _run(model, E_SMALL, C_SMALL, env, monkeypatch)
     assert info["variant"] >= 20000
-    fwd = "k_fwd_mma<64>" if mma else "k_fwd_wide"
+    fwd = "k_fwd_mmt<4>" if mma else "k_fwd_wide"
     assert {f"k_witems<{NV[nvar]}>", "k_wq", fwd, "k_zrows"} <= launched, launched
     assert_loglik_close(got[ie, ic], ref)

@@ -58,7 +58,11 @@ CASES = {
     "lds_states": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37, {},
                    "mdp_fwd_jit<reading"),
     "wide": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
-             {"MDP_WIDE": "1"}, "k_fwd_mma"),
+             {"MDP_WIDE": "1"}, "k_fwd_mmt"),
+    "wide_mma5": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
+                  {"MDP_WIDE": "1", "MDP_WIDE_MMA": "1"}, "k_fwd_mma"),
+    "wide_big": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 10, 4, {1: 9})), 70, 37,
+                 {}, "k_fwd_mmt<2>"),
     "wide_plain": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
                    {"MDP_WIDE": "1", "MDP_WIDE_MMA": "0"}, "k_fwd_wide"),
 }

@@ -276,30 +276,40 @@ def _wide_engine_run(model, e, c, path, monkeypatch):
     """Run on the named path and check it ran: "default" (years of 17-64
     states: the specialised kernel with its states in LDS; more: the wide
     kernels), "wide" (MDP_WIDE=1: k_witems + k_wq + the matrix-core forward
-    k_fwd_mma) or "wide-plain" (k_fwd_wide, MDP_WIDE_MMA=0)."""
+    k_fwd_mmt, years of up to 1 024 states), "wide-mma5" (round 5's
+    k_fwd_mma, MDP_WIDE_MMA=1, up to 256 states) or "wide-plain" (k_fwd_wide,
+    MDP_WIDE_MMA=0)."""
     monkeypatch.delenv("MDP_WIDE", raising=False)
     monkeypatch.delenv("MDP_WIDE_MMA", raising=False)
     if path.startswith("wide"):
         monkeypatch.setenv("MDP_WIDE", "1")
     if path == "wide-plain":
         monkeypatch.setenv("MDP_WIDE_MMA", "0")
+    if path == "wide-mma5":
+        monkeypatch.setenv("MDP_WIDE_MMA", "1")
     with mdp.Engine(model) as eng:
         got = eng.loglik_grid(e, c)
         launched, info = eng.launched(), eng.info()
     if path.startswith("wide") or model.npstates.max() > 64:
-        npm = model.npstates.max()
-        mma = path != "wide-plain" and npm <= 256
-        want = f"k_fwd_mma<{64 if npm <= 64 else 128 if npm <= 128 else 256}" if mma else "k_fwd_wide"
-        if mma:
-            want += ">"
-        assert info["variant"] >= 20000 and want in launched, launched
+        assert info["variant"] >= 20000, info
+        assert launched_forward(model, path) in launched, launched
     else:
         assert 10000 <= info["variant"] < 20000, info
         assert any(k.startswith("mdp_fwd_jit<reading") for k in launched), launched
     return got
 
 
-@pytest.mark.parametrize("path", ["default", "wide", "wide-plain"])
+def launched_forward(model, path):
+    """The wide forward kernel instantiation `path` runs for this model."""
+    npm = int(model.npstates.max())
+    if path == "wide-mma5" and npm <= 256:
+        return f"k_fwd_mma<{64 if npm <= 64 else 128 if npm <= 128 else 256}>"
+    if path in ("default", "wide") and npm <= 1024:
+        return f"k_fwd_mmt<{4 if npm <= 256 else 2 if npm <= 512 else 1}>"
+    return "k_fwd_wide"
+
+
+@pytest.mark.parametrize("path", ["default", "wide", "wide-mma5", "wide-plain"])
 @pytest.mark.parametrize("missing", [{0: 5}, {3: 5}, {2: 6}, {4: 6}, {0: 8}, {3: 8}, {1: 5, 2: 6}, {0: 6, 4: 7},
                                      {1: 8, 2: 7}, {2: 7, 3: 8}])
 def test_wide_years_vs_oracle(missing, path, monkeypatch):
@@ -307,8 +317,8 @@ def test_wide_years_vs_oracle(missing, path, monkeypatch):
     later years, in consecutive years: the reference expands 2^k states for
     any k (main_MIDASPOM.c:225-251) and propagates them (:371-384); up to 64
     states the specialised kernel keeps them in LDS, beyond that (and forced)
-    the wide kernels run -- k_fwd_mma<64|128|256> on the matrix cores (256
-    states: 32 points a block)."""
+    the wide kernels run -- k_fwd_mmt<4> on the matrix cores (64 points a
+    block), round 5's k_fwd_mma<64|128|256> and k_fwd_wide when asked."""
     rng = np.random.default_rng(sum(100 * y + k for y, k in missing.items()))
     obs = _wide_obs(rng, 12, 5, missing)
     model = mdp.Model.from_obs(obs)
@@ -335,11 +345,65 @@ def test_random_wide_problems(seed, monkeypatch):
     e, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.2])))
     c, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.5])))
     ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c, threads=16)
-    for path, cb in (("default", None), ("wide", None), ("wide-plain", None), ("wide", "1")):
+    for path, cb in (("default", None), ("wide", None), ("wide-mma5", None), ("wide-plain", None), ("wide", "1")):
         if cb:
             monkeypatch.setenv("MDP_WIDE_CB", cb)
         got = _wide_engine_run(model, e, c, path, monkeypatch)
         assert_loglik_close(got, ref)
+
+
+def _big_obs(rng, missing, full=()):
+    """10 patches x 6 years (2^10 hidden states): `missing` = {year: k}
+    unvisited patches among patches 1-9 (2^k states), and every patch
+    unvisited in the years of `full` (1 024 states)."""
+    obs = _wide_obs(rng, 10, 6, missing)
+    for yr in full:
+        obs[yr, :] = -1
+    return obs
+
+
+@pytest.mark.parametrize("path", ["default", "wide-plain"])
+@pytest.mark.parametrize("missing,full", [({1: 9}, ()), ({0: 9}, ()), ({2: 9, 3: 9}, ()), ({4: 8}, (2,)),
+                                          ({}, (0,)), ({1: 9}, (2, 3)), ({3: 7}, (5,))],
+                         ids=["512@1", "512@0", "512@2+3", "1024@2", "1024@0", "512@1+1024@2+3", "1024@5"])
+def test_big_years_vs_oracle(missing, full, path, monkeypatch):
+    """Years of 512 and 1 024 states (9 and 10 unvisited patches; the
+    reference expands any number, main_MIDASPOM.c:222-255, and propagates
+    them by dgemm, :371-384): k_fwd_mmt<2> / <1> on the matrix cores by
+    default (a wave takes 2 or 4 column tiles a year), k_fwd_wide when asked;
+    one year, consecutive years, year 0 (Q3: ones over its states) and the
+    last year, against the oracle on a whole 6 x 5 grid."""
+    rng = np.random.default_rng(17 + sum(100 * y + k for y, k in missing.items()) + 7 * sum(full))
+    obs = _big_obs(rng, missing, full)
+    model = mdp.Model.from_obs(obs)
+    assert model.npstates.max() == (1024 if full else 2 ** max(missing.values()))
+    e, _ = mdp.grid(6, 0.0, 1.1)
+    c, _ = mdp.grid(5)
+    got = _wide_engine_run(model, e, c, path, monkeypatch)
+    ref = oracle.OracleModel.from_obs(obs).loglik_grid(e, c, threads=16)
+    assert np.isfinite(ref).sum() >= 9
+    assert_loglik_close(got, ref)
+
+
+@pytest.mark.parametrize("path", ["default", "wide-plain"])
+def test_big_survey_series_sampled(tmp_path, path, monkeypatch):
+    """The 10-variable-patch survey series of scripts/wide_timing.py (60 %
+    unvisited: years of up to 1 024 states, two of 512; 643 328 uses per
+    point): k_fwd_mmt<1> (16 points a block) and k_fwd_wide on a 37 x 23
+    grid (the last point block partial), sampled against the oracle."""
+    cfg = dict(synth.CONFIG2, nvar=10, pmiss=0.6, seed=5, T=30)
+    f = synth.write(tmp_path / "big60.txt", **cfg)
+    model = mdp.Model.load(f)
+    assert model.npstates.max() == 1024
+    e, _ = mdp.grid(37)
+    c, _ = mdp.grid(23)
+    got = _wide_engine_run(model, e, c, path, monkeypatch)
+    rng = np.random.default_rng(8)
+    ie, ic = rng.integers(0, 37, 16), rng.integers(0, 23, 16)
+    ie[:4], ic[:4] = [0, 36, 0, 36], [0, 0, 22, 22]
+    ref = oracle.OracleModel.load(f).loglik_points(e[ie], c[ic], threads=16)
+    assert np.isfinite(ref).sum() >= 8
+    assert_loglik_close(got[ie, ic], ref)
 
 
 @pytest.mark.parametrize("path", ["default", "wide"])
@@ -366,7 +430,7 @@ def test_wide_survey_series_sampled(tmp_path, path, monkeypatch):
 @pytest.mark.parametrize("path", ["default", "wide-plain"])
 def test_wide_survey_series_128_states(tmp_path, path, monkeypatch):
     """The 60 %-unvisited survey series of scripts/wide_timing.py (up to 128
-    states a year, 66 416 uses per point): k_fwd_mma<128> by default, and
+    states a year, 66 416 uses per point): k_fwd_mmt<4> by default, and
     k_fwd_wide, on a 130 x 70 grid (three 64-point blocks, the last partial),
     sampled against the oracle."""
     cfg = dict(synth.CONFIG2, pmiss=0.6, seed=5, T=50)
@@ -386,7 +450,7 @@ def test_wide_survey_series_128_states(tmp_path, path, monkeypatch):
 
 def test_wide_survey_series_256_states(tmp_path, monkeypatch):
     """A 75 %-unvisited survey series (three years of 256 states, 257 024
-    uses per point): k_fwd_mma<256> (32 points a block)
+    uses per point): k_fwd_mmt<4> (64 points a block)
     on a 70 x 40 grid (three 32-point blocks, the last partial), sampled
     against the oracle."""
     cfg = dict(synth.CONFIG2, pmiss=0.75, seed=5, T=30)
@@ -415,7 +479,7 @@ def test_wide_path_matches_direct_path(golden, monkeypatch, fname, s):
     with mdp.Engine(model) as eng:
         assert eng.info()["variant"] >= 20000
         b = eng.loglik_grid(g, g)
-        assert set(eng.kernel_ms()) <= {"k_zrows", "k_witems+k_wq", "k_fwd_wide", "k_fwd_mma"}
+        assert set(eng.kernel_ms()) <= {"k_zrows", "k_witems+k_wq", "k_fwd_wide", "k_fwd_mma", "k_fwd_mmt"}
     assert_loglik_close(b, a, atol=1e-11)
 
 
