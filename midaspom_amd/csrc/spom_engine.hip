@@ -1517,16 +1517,19 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
 constexpr uint32_t kMmtU = 2;           // K steps (of 4 entries) per pipeline chunk
 constexpr uint32_t kMmtMaxTiles = 64;   // column tiles a year (1 024 states)
 constexpr uint32_t mmt_pts(uint32_t rt) { return 16u * rt; }
-constexpr uint32_t mmt_rows(uint32_t rt) { return 1024u / rt; }
-constexpr uint32_t mmt_ps(uint32_t rt) { return 16u * rt + 8u; }  // power-table row stride (doubles)
-template <int RT>  // point tiles of 16 per block: 4 (<= 256 states), 2 (<= 512), 1 (<= 1 024)
+// power-table row stride (doubles): rows r and r + 1 on different LDS bank halves
+constexpr uint32_t mmt_ps(uint32_t rt) { return rt % 2 ? 16u * rt : 16u * rt + 16u; }
+// the instantiations: point tiles of 16 per block and state rows -- <2, 256>
+// (years of up to 256 states), <2, 512>, <1, 1 024>
+template <int RT, int ROWS>
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
     const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint2 *__restrict__ kt,
-    const uint2 *__restrict__ ktile, const uint32_t *__restrict__ desc, const uint32_t *__restrict__ dbase,
-    const uint2 *__restrict__ wplan, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
-    uint32_t maxA, uint32_t zslot, double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
+    const uint32_t *__restrict__ cidx, const uint2 *__restrict__ ktile, const uint2 *__restrict__ wplan, uint32_t tmax,
+    double prior0, const double *__restrict__ evals, uint32_t ne, uint32_t maxA, double *__restrict__ out,
+    uint32_t ld_out, uint32_t out_cs)
 {
-    constexpr uint32_t PTS = mmt_pts(RT), ROWS = mmt_rows(RT), PS = mmt_ps(RT), TMAX = 4 / RT;
+    constexpr uint32_t PTS = mmt_pts(RT), PS = mmt_ps(RT), TMAX = ROWS / 256;
+    static_assert(TMAX * 16 * 16 == ROWS && TMAX * RT <= 4, "tiles per wave");
     extern __shared__ __attribute__((aligned(16))) double mlds[];
     double *V = mlds;  // [state][point]
     double *xp = V + (size_t)ROWS * PTS, *yp = xp + (size_t)(maxA + 1) * PS;  // [r][point]
@@ -1554,45 +1557,48 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
     const double *q = Q + (size_t)ic * ldQ;
     const uint32_t kk = lane >> 4, col = lane & 15u;
     struct Item {
-        uint32_t tile, ks, S, cb, ce, nch, sh, lc4, npcp, ncol;
-        bool active;
+        uint32_t tile, ks, S, pbase, cb, ce, nch, npcp;
+        bool active, split;
         const uint2 *kl;
-        const uint32_t *dt;
+        const uint32_t *cl;
     };
     // item i of this wave in year t (host table mmt_wplan: no divisions here)
     auto plan = [&](uint32_t t, uint32_t i) {
         Item it;
-        it.ncol = (np[t] + 15) / 16;
-        it.npcp = it.ncol * 16;
+        it.npcp = (np[t] + 15) / 16 * 16;
         const uint2 wp = wplan[(t * 16 + wv) * TMAX + i];
         it.cb = wp.x & 0xffffu;
         it.ce = wp.x >> 16;
         it.tile = wp.y & 0xffu;
-        it.ks = (wp.y >> 8) & 0xffu;
-        it.S = (wp.y >> 16) & 0xffu;
+        it.ks = (wp.y >> 8) & 15u;      // slice of the tile's K list
+        it.S = (wp.y >> 12) & 31u;      // the tile's slices
+        it.pbase = (wp.y >> 17) & 31u;  // its partial blocks (slices 1 .. S - 1) from here
+        it.split = (wp.y >> 22) & 1u;   // some tile of the year is sliced (uniform)
         it.active = (wp.y >> 24) != 0u;
         const uint2 kt2 = ktile[t * kMmtMaxTiles + it.tile];
-        it.kl = kt + __builtin_amdgcn_readfirstlane(kt2.x);
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(kt2.x);
+        it.kl = kt + k0;
+        it.cl = cidx + (size_t)k0 * 16;
         it.nch = kt2.y;
-        it.sh = 32u - (uint32_t)__builtin_clz(it.npcp - 1u);  // descriptor rows [k][2^sh >= npcp]
-        it.lc4 = (it.tile * 16 + col) << 2;
-        it.dt = desc + __builtin_amdgcn_readfirstlane(dbase[t]);
         return it;
     };
-    // K entry (uint2): x = V row byte offset (18 bits) | y^m row offset << 18;
-    // y = x^(|A|-m) row offset (16 bits) | m << 16 | k << 21 (k = npp: the
-    // descriptor row of absent transitions, which the padding names)
+    // K entry (uint2, one per 16 lanes): x = V row byte offset (18 bits) |
+    // y^m row offset << 18, y = x^(|A|-m) row offset (16 bits) | m << 16 | k
+    // << 21; and per lane the byte offset in the Q row of C[(k, m)][l] --
+    // Q_kl[m], or the zero slot where m > nX or l is a padded state (host
+    // table, so no descriptor lookup is on the gather's path)
     auto kent = [&](const Item &it, uint32_t ch, uint32_t u) {
         const uint32_t c = ch < it.nch ? ch : it.nch - 1;
         return it.kl[(c * kMmtU + u) * 4 + kk];
     };
-    auto dsc = [&](const Item &it, uint2 en) {
-        return *(const uint32_t *)((const char *)it.dt + (((en.y >> 21) << (it.sh + 2)) + it.lc4));
+    auto coff = [&](const Item &it, uint32_t ch, uint32_t u) {
+        const uint32_t c = ch < it.nch ? ch : it.nch - 1;
+        return it.cl[(c * kMmtU + u) * 64 + lane];
     };
-    auto cval = [&](uint2 en, uint32_t d) {
-        const uint32_t m = (en.y >> 16) & 31u;
-        return *(const double *)((const char *)q + ((m <= ((d >> kOffBits) & 31u) ? (d & kOffMask) + m : zslot) << 3));
-    };
+    auto cval = [&](uint32_t o) { return *(const double *)((const char *)q + o); };
+    // rings by chunk position j = ch - cb: K entries of ch .. ch + 3 (mod
+    // 4), C offsets of ch + 1 and ch + 2 (mod 2; ch's were consumed by its
+    // gathers), C values of ch and ch + 1 (mod 2)
     uint2 ee[4][kMmtU];
     uint32_t dd[2][kMmtU];
     double bb[2][kMmtU];
@@ -1602,16 +1608,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
             ee[0][u] = kent(it, it.cb, u);
             ee[1][u] = kent(it, it.cb + 1, u);
             ee[2][u] = kent(it, it.cb + 2, u);
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kMmtU; ++u) {
-            dd[0][u] = dsc(it, ee[0][u]);
-            dd[1][u] = dsc(it, ee[1][u]);
+            dd[0][u] = coff(it, it.cb, u);
+            dd[1][u] = coff(it, it.cb + 1, u);
         }
     };
     auto prime_b = [&]() {
 #pragma unroll
-        for (uint32_t u = 0; u < kMmtU; ++u) bb[0][u] = cval(ee[0][u], dd[0][u]);
+        for (uint32_t u = 0; u < kMmtU; ++u) bb[0][u] = cval(dd[0][u]);
     };
     Item cur = plan(tmax > 1 ? 1u : 0u, 0);
     if (tmax > 1 && cur.active) {
@@ -1633,16 +1636,17 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
             }
             if (!cur.active) break;
             mdp_d4(&ac)[RT] = acc[i];  // (i is a constant once unrolled)
-            // one chunk at ring position j: the K entries of ch + 3, the
-            // descriptors of ch + 2, the C values of ch + 1, then ch's products
+            // one chunk at ring position j: the K entries of ch + 3, the C
+            // values of ch + 1 (their offsets loaded a chunk ago), the C
+            // offsets of ch + 2, then ch's products
             auto chunk = [&](uint32_t ch, auto jc) {
                 constexpr uint32_t j = decltype(jc)::value;
 #pragma unroll
                 for (uint32_t u = 0; u < kMmtU; ++u) ee[(j + 3) & 3][u] = kent(cur, ch + 3, u);
 #pragma unroll
-                for (uint32_t u = 0; u < kMmtU; ++u) dd[j & 1][u] = dsc(cur, ee[(j + 2) & 3][u]);
+                for (uint32_t u = 0; u < kMmtU; ++u) bb[(j + 1) & 1][u] = cval(dd[(j + 1) & 1][u]);
 #pragma unroll
-                for (uint32_t u = 0; u < kMmtU; ++u) bb[(j + 1) & 1][u] = cval(ee[(j + 1) & 3][u], dd[(j + 1) & 1][u]);
+                for (uint32_t u = 0; u < kMmtU; ++u) dd[j & 1][u] = coff(cur, ch + 2, u);
 #pragma unroll
                 for (uint32_t u = 0; u < kMmtU; ++u) {
                     const uint2 en = ee[j][u];
@@ -1674,13 +1678,14 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
         if (pnext) prime_a(nxt);
         __syncthreads();  // every wave has read the year's old states
         // the lane's accumulators: states tile * 16 + kk + 4 r of point
-        // h * 16 + col; slices ks >= 1 park theirs past row npcp
-        auto part = [&](uint32_t ks, uint32_t tile) {
-            return V + (size_t)(first.npcp + ((ks - 1) * first.ncol + tile) * 16) * PTS + lane;
+        // h * 16 + col; slices ks >= 1 park theirs past row npcp (partial
+        // block pbase + ks - 1 of the year: at most 16 - tiles of them)
+        auto part = [&](uint32_t ks) {
+            return V + (size_t)(first.npcp + (first.pbase + ks - 1) * 16) * PTS + lane;
         };
-        if (first.S > 1) {
+        if (first.split) {
             if (first.active && first.ks >= 1) {
-                double *pk = part(first.ks, first.tile);
+                double *pk = part(first.ks);
 #pragma unroll
                 for (uint32_t h = 0; h < RT; ++h)
 #pragma unroll
@@ -1689,7 +1694,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
             __syncthreads();
             if (first.active && first.ks == 0)
                 for (uint32_t j = 1; j < first.S; ++j) {
-                    const double *pj = part(j, first.tile);
+                    const double *pj = part(j);
 #pragma unroll
                     for (uint32_t h = 0; h < RT; ++h)
 #pragma unroll
@@ -1899,7 +1904,7 @@ struct DevCtx {
     uint2 *mma_kt = nullptr, *mma_wplan = nullptr;
     uint32_t *mma_kbase = nullptr, *mma_desc = nullptr, *mma_dbase = nullptr;
     uint2 *mmt_kt = nullptr, *mmt_ktile = nullptr, *mmt_wplan = nullptr;  // k_fwd_mmt tables
-    uint32_t *mmt_desc = nullptr, *mmt_dbase = nullptr;
+    uint32_t *mmt_cidx = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     std::vector<uint8_t> ev_mask;  // per profiled run: slots whose kernel was launched
@@ -2035,9 +2040,9 @@ struct mdp_engine {
     // 1 024 states): RT point tiles a block, per (year, tile) K lists, per
     // (year, wave) work items (build_mmt_plan)
     bool mmt = false;
-    uint32_t mmt_rt = 0;
+    uint32_t mmt_rt = 0, mmt_rows = 0;
     std::vector<uint2> mmt_kt, mmt_ktile, mmt_wplan;
-    std::vector<uint32_t> mmt_desc, mmt_dbase;
+    std::vector<uint32_t> mmt_cidx;
     double mmt_flops_pt = 0;  // executed MFMA flops per grid point (padding included)
     uint32_t qslot_lglmax = 0;      // log2 of the widest lane segment
     std::vector<uint8_t> isvar;
@@ -2533,54 +2538,46 @@ size_t device_lds_max()
 size_t mmt_lds(const mdp_engine *eng)
 {
     const uint32_t rt = eng->mmt_rt;
-    return ((size_t)mmt_rows(rt) * mmt_pts(rt) + 2 * ((size_t)eng->maxA + 1) * mmt_ps(rt)) * sizeof(double);
+    return ((size_t)eng->mmt_rows * mmt_pts(rt) + 2 * ((size_t)eng->maxA + 1) * mmt_ps(rt)) * sizeof(double);
 }
 
 const void *mmt_kernel(const mdp_engine *eng)
 {
-    if (eng->mmt_rt == 4) return (const void *)k_fwd_mmt<4>;
-    if (eng->mmt_rt == 2) return (const void *)k_fwd_mmt<2>;
-    return (const void *)k_fwd_mmt<1>;
+    if (eng->mmt_rows == 256) return (const void *)k_fwd_mmt<2, 256>;
+    if (eng->mmt_rows == 512) return (const void *)k_fwd_mmt<2, 512>;
+    return (const void *)k_fwd_mmt<1, 1024>;
 }
 
 // k_fwd_mmt's tables (c-independent): years of at most 1 024 states.
-//  * per year the transition descriptors [k][2^sh >= npcp] (Q-row offset |
-//    nX << kOffBits; an absent transition -- and the row k = npp the padding
-//    names -- the zero slot with nX = 0);
 //  * per (year, column tile) its K entries: every source k with m = 0 ..
 //    the largest nX over the tile's new states (the rest of m <= |A_k| would
-//    meet only zero slots), padded to whole pipeline chunks;
-//  * per (year, wave) up to 4 / RT work items: tiles of years of more than
-//    8 tiles dealt longest list first to the least-loaded wave; smaller years
-//    split each tile's list into S slices (at least two chunks each) over
-//    up to 16 waves.
+//    meet only zero slots), padded to whole pipeline chunks; and per K entry
+//    and new state l of the tile, the byte offset in the Q row of Q_kl[m]
+//    (the zero slot where m > nX_kl, for padded states and padded entries)
+//    -- 64 bytes per entry, so the kernel's gathers need no lookup;
+//  * per (year, wave) up to ROWS / 256 work items: tiles of years of more
+//    than 16 tiles dealt longest list first to the least-loaded wave;
+//    smaller years give every tile a wave and the spare waves to the tiles
+//    with the longest lists, each tile's list split into as many slices
+//    (at least two chunks each).
 void build_mmt_plan(mdp_engine *eng)
 {
     if (eng->npmax > 1024 || eng->maxA > 24 || eng->tmax < 2) return;
-    const uint32_t rt = eng->npmax <= 256 ? 4u : eng->npmax <= 512 ? 2u : 1u;
-    const uint32_t pts = mmt_pts(rt), ps = mmt_ps(rt), tmaxit = 4 / rt, cw = 4 * kMmtU;
+    const uint32_t rows = eng->npmax <= 256 ? 256u : eng->npmax <= 512 ? 512u : 1024u, rt = rows == 1024 ? 1u : 2u;
+    const uint32_t pts = mmt_pts(rt), ps = mmt_ps(rt), tmaxit = rows / 256, cw = 4 * kMmtU;
     const uint32_t none = (uint32_t)eng->ncoef_d;
     if (none > kOffMask) return;
     eng->mmt_rt = rt;
+    eng->mmt_rows = rows;
     eng->mmt_kt.clear();
-    eng->mmt_desc.clear();
-    eng->mmt_dbase.assign(eng->tmax + 1, 0u);
+    eng->mmt_cidx.clear();
     eng->mmt_ktile.assign((size_t)(eng->tmax + 1) * kMmtMaxTiles, make_uint2(0u, 1u));
     eng->mmt_wplan.assign((size_t)(eng->tmax + 1) * 16 * tmaxit, make_uint2(0u, 0u));
     double fl = 0.0;
     size_t ub = 0;
     for (uint32_t t = 1; t < eng->tmax; ++t) {
-        const uint32_t npp = eng->np[t - 1], npc = eng->np[t], ncol = (npc + 15) / 16, npcp = ncol * 16;
+        const uint32_t npp = eng->np[t - 1], npc = eng->np[t], ncol = (npc + 15) / 16;
         const uint32_t *ud = eng->udesc_d.data() + ub;  // ud[l * npp + k]
-        uint32_t ld = 16;
-        while (ld < npcp) ld *= 2;
-        eng->mmt_dbase[t] = (uint32_t)eng->mmt_desc.size();
-        for (uint32_t k = 0; k <= npp; ++k)
-            for (uint32_t l = 0; l < ld; ++l) {
-                uint32_t dv = none;
-                if (k < npp && l < npc) dv = (ud[(size_t)l * npp + k] & kOffMask) | (((ud[(size_t)l * npp + k] >> kOffBits) & 31u) << kOffBits);
-                eng->mmt_desc.push_back(dv);
-            }
         std::vector<uint32_t> nch(ncol);
         for (uint32_t tile = 0; tile < ncol; ++tile) {
             const size_t start = eng->mmt_kt.size();
@@ -2589,26 +2586,50 @@ void build_mmt_plan(mdp_engine *eng)
                 const uint32_t a = ud[k] >> 27;  // |A_k|
                 uint32_t mx = 0;
                 for (uint32_t l = 16 * tile; l < l1; ++l) mx = std::max(mx, (ud[(size_t)l * npp + k] >> kOffBits) & 31u);
-                for (uint32_t m = 0; m <= mx; ++m)  // V row k, y^m row, x^(a-m) row (bytes); m; k
+                for (uint32_t m = 0; m <= mx; ++m) {  // V row k, y^m row, x^(a-m) row (bytes); m; k
                     eng->mmt_kt.push_back(make_uint2((k * pts * 8u) | ((m * ps * 8u) << 18),
                                                      ((a - m) * ps * 8u) | (m << 16) | (k << 21)));
+                    for (uint32_t l = 16 * tile; l < 16 * tile + 16; ++l) {
+                        uint32_t o = none;
+                        if (l < npc) {
+                            const uint32_t dsc = ud[(size_t)l * npp + k];
+                            if (m <= ((dsc >> kOffBits) & 31u)) o = (dsc & kOffMask) + m;
+                        }
+                        eng->mmt_cidx.push_back(o * 8u);
+                    }
+                }
             }
-            while ((eng->mmt_kt.size() - start) % cw) eng->mmt_kt.push_back(make_uint2(0u, npp << 21));
+            while ((eng->mmt_kt.size() - start) % cw) {
+                eng->mmt_kt.push_back(make_uint2(0u, npp << 21));
+                for (uint32_t l = 0; l < 16; ++l) eng->mmt_cidx.push_back(none * 8u);
+            }
             nch[tile] = (uint32_t)((eng->mmt_kt.size() - start) / cw);
             eng->mmt_ktile[(size_t)t * kMmtMaxTiles + tile] = make_uint2((uint32_t)start, nch[tile]);
             fl += 2.0 * 16.0 * (double)(eng->mmt_kt.size() - start);
         }
         uint2 *wp = eng->mmt_wplan.data() + (size_t)t * 16 * tmaxit;
         if (ncol <= 16) {
-            uint32_t S = 1;
-            if (ncol <= 8) S = std::max(1u, std::min(16 / ncol, *std::min_element(nch.begin(), nch.end()) / 2));
-            for (uint32_t wv = 0; wv < 16; ++wv) {
-                const uint32_t tile = wv % ncol, ks = wv / ncol;
-                const bool on = wv < ncol * S;
-                const uint32_t cb = on ? nch[tile] * ks / S : 0, ce = on ? nch[tile] * (ks + 1) / S : 0;
-                for (uint32_t i = 0; i < tmaxit; ++i)
-                    wp[wv * tmaxit + i] = make_uint2(i ? 0u : cb | ce << 16,
-                                                     (i ? 0u : tile | ks << 8) | S << 16 | (!i && on ? 1u : 0u) << 24);
+            // waves per tile: one each, the rest to the tile whose slices
+            // are longest (each slice at least two chunks)
+            std::vector<uint32_t> w(ncol, 1);
+            for (uint32_t spare = 16 - ncol; spare; --spare) {
+                uint32_t best = ncol;
+                for (uint32_t i = 0; i < ncol; ++i)
+                    if (nch[i] / (w[i] + 1) >= 2 && (best == ncol || nch[i] * w[best] > nch[best] * w[i])) best = i;
+                if (best == ncol) break;
+                ++w[best];
+            }
+            const uint32_t split = *std::max_element(w.begin(), w.end()) > 1 ? 1u : 0u;
+            for (uint32_t wv = 0; wv < 16; ++wv)
+                for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, split << 22);
+            uint32_t wv = 0, pbase = 0;
+            for (uint32_t tile = 0; tile < ncol; ++tile) {
+                for (uint32_t ks = 0; ks < w[tile]; ++ks, ++wv) {
+                    const uint32_t cb = nch[tile] * ks / w[tile], ce = nch[tile] * (ks + 1) / w[tile];
+                    wp[wv * tmaxit] = make_uint2(cb | ce << 16, tile | ks << 8 | w[tile] << 12 | pbase << 17 |
+                                                                   split << 22 | 1u << 24);
+                }
+                pbase += w[tile] - 1;
             }
         } else {
             std::vector<uint32_t> order(ncol), cnt(16, 0);
@@ -2616,21 +2637,24 @@ void build_mmt_plan(mdp_engine *eng)
             for (uint32_t i = 0; i < ncol; ++i) order[i] = i;
             std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return nch[x] > nch[y]; });
             for (uint32_t wv = 0; wv < 16; ++wv)
-                for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, 1u << 16);
+                for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, 0u);
             for (uint32_t tile : order) {
                 uint32_t best = 16;
                 for (uint32_t wv = 0; wv < 16; ++wv)
                     if (cnt[wv] < tmaxit && (best == 16 || load[wv] < load[best])) best = wv;
-                wp[best * tmaxit + cnt[best]++] = make_uint2(nch[tile] << 16, tile | 1u << 16 | 1u << 24);
+                wp[best * tmaxit + cnt[best]++] = make_uint2(nch[tile] << 16, tile | 1u << 12 | 1u << 24);
                 load[best] += nch[tile];
             }
         }
         ub += (size_t)npp * npc;
     }
-    for (uint32_t i = 0; i < cw; ++i) eng->mmt_kt.push_back(make_uint2(0u, 0u));
-    if (eng->mmt_desc.empty()) eng->mmt_desc.push_back(none);
     eng->mmt_flops_pt = fl + 2.0 * (eng->maxA + 1) + (double)eng->np[eng->tmax - 1];
-    eng->mmt = mmt_lds(eng) <= device_lds_max() && eng->mmt_kt.size() < 0xffffffffu;
+    // (the offsets' table is the plan's largest: 64 bytes per K entry)
+    eng->mmt = mmt_lds(eng) <= device_lds_max() && eng->mmt_kt.size() < (1u << 26) && (size_t)none * 8u < 0xffffffffu;
+    if (!eng->mmt) {
+        eng->mmt_kt.clear();
+        eng->mmt_cidx.clear();
+    }
 }
 
 int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
@@ -3141,8 +3165,7 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
                 HIP_TRY(hipFuncSetAttribute(mma_kernel(eng), hipFuncAttributeMaxDynamicSharedMemorySize, (int)mma_lds(eng)));
             if (eng->mmt &&
                 ((rc = dev_upload(&d.mmt_kt, eng->mmt_kt)) || (rc = dev_upload(&d.mmt_ktile, eng->mmt_ktile)) ||
-                 (rc = dev_upload(&d.mmt_wplan, eng->mmt_wplan)) || (rc = dev_upload(&d.mmt_desc, eng->mmt_desc)) ||
-                 (rc = dev_upload(&d.mmt_dbase, eng->mmt_dbase))))
+                 (rc = dev_upload(&d.mmt_wplan, eng->mmt_wplan)) || (rc = dev_upload(&d.mmt_cidx, eng->mmt_cidx))))
                 return rc;
             if (eng->mmt)
                 HIP_TRY(hipFuncSetAttribute(mmt_kernel(eng), hipFuncAttributeMaxDynamicSharedMemorySize, (int)mmt_lds(eng)));
@@ -3182,7 +3205,7 @@ void free_device(DevCtx &d)
                     d.zs, d.zsq, d.sv, d.Qrow, d.Zg, d.coltab, d.items, d.itemB, d.qstart, d.qitem,
                     d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot, d.qlane, d.islot,
                     d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan,
-                    d.mmt_kt, d.mmt_ktile, d.mmt_wplan, d.mmt_desc, d.mmt_dbase,
+                    d.mmt_kt, d.mmt_ktile, d.mmt_wplan, d.mmt_cidx,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -3502,17 +3525,17 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
                                d.Qrow, (uint32_t)eng->ldQ);
         }
     } else if (eng->mmt) {  // the matrix-core forward: every c in one launch, blocks dealt XCD-aware
-        const uint32_t rt = eng->mmt_rt, npb = (d.ne + mmt_pts(rt) - 1) / mmt_pts(rt);
+        const uint32_t rt = eng->mmt_rt, rows = eng->mmt_rows, npb = (d.ne + mmt_pts(rt) - 1) / mmt_pts(rt);
         const uint64_t nb = (uint64_t)npb * d.nc;
         if (nb > 0x7fffffffull) return mdp_set_error(MDP_EUNSUPPORTED, "grid of %llu k_fwd_mmt workgroups", (unsigned long long)nb);
-        note_launch(eng, "k_fwd_mmt<%u>", rt);
-#define MDP_MMT(RT) \
-    hipLaunchKernelGGL((k_fwd_mmt<RT>), dim3((uint32_t)nb), dim3(kMmaThreads), mmt_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, \
-                       d.np_d, d.mmt_kt, d.mmt_ktile, d.mmt_desc, d.mmt_dbase, d.mmt_wplan, eng->tmax, eng->prior0, d.e, \
-                       d.ne, eng->maxA, eng->ncoef_d, out, os.se, os.sc)
-        if (rt == 4) MDP_MMT(4);
-        else if (rt == 2) MDP_MMT(2);
-        else MDP_MMT(1);
+        note_launch(eng, "k_fwd_mmt<%u,%u>", rt, rows);
+#define MDP_MMT(RT, ROWS) \
+    hipLaunchKernelGGL((k_fwd_mmt<RT, ROWS>), dim3((uint32_t)nb), dim3(kMmaThreads), mmt_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, \
+                       d.np_d, d.mmt_kt, d.mmt_cidx, d.mmt_ktile, d.mmt_wplan, eng->tmax, eng->prior0, d.e, d.ne, \
+                       eng->maxA, out, os.se, os.sc)
+        if (rows == 256) MDP_MMT(2, 256);
+        else if (rows == 512) MDP_MMT(2, 512);
+        else MDP_MMT(1, 1024);
 #undef MDP_MMT
     } else if (eng->mma) {  // round 5's matrix-core forward (MDP_WIDE_MMA=1; years of up to 256 states)
         uint32_t se = os.se, sc = os.sc;
