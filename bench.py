@@ -228,6 +228,12 @@ def cpu_baseline(input_path, g_e, g_c, lik_gpu, ltot_gpu, tmax, tmpdir, budget_s
     return res, parity
 
 
+def _coll_name(args):
+    """The collective library a multi-rank line used: RCCL for the nccl
+    backend (ROCm), else the rehearsal backend's own name."""
+    return "RCCL" if args.backend == "nccl" else args.backend
+
+
 def _coll_tensor(t, args):
     """The tensor a collective runs on: itself under RCCL, a host copy under
     a rehearsal backend (gloo moves host tensors only)."""
@@ -310,7 +316,8 @@ def bench_future(args, world, rank, dev):
         "data": "examples/input (shipped), posterior from the GPU engine at s=101",
         "config": {"workload": "config5: MIDASPOM_future, 10^6 replicates x 50 years, examples/input",
                    "patches": int(n), "replicates": nsim, "years": tfut,
-                   "parallelism": f"replicate ranges x{world}" + (", RCCL reduce" if world > 1 else "")},
+                   "parallelism": f"replicate ranges x{world}" + (f", {_coll_name(args)} reduce" if world > 1 else ""),
+                   "backend": args.backend if world > 1 else None},
         "kernel_ms": {"k_future": kms},
         "roofline": {"kernel": "k_future", "bound": "valu-issue",
                      "compute_unit": "VALU issue cycles (Philox integer work), instructions priced by class",
@@ -413,7 +420,8 @@ def bench_dieoff(args, world, rank, dev):
         "data": "examples/input first survey row (shipped)",
         "config": {"workload": f"config4: MIDASPOM_dieoff (e,c,K_D) {s}^3 grid, ts=20, tdis=10, n=8",
                    "grid": [s, s, s], "patches": int(n), "states": ns,
-                   "parallelism": f"e-row slabs x{world}" + (", RCCL gather" if world > 1 else "")},
+                   "parallelism": f"e-row slabs x{world}" + (f", {_coll_name(args)} gather" if world > 1 else ""),
+                   "backend": args.backend if world > 1 else None},
         "job": {"ms": job_ms, "what": "one pass + one gather to rank 0" if world > 1 else "one pass"},
         "kernel_ms": kms,
         "roofline": {"kernel": "k_scn_lik", "bound": "fp64-valu", "compute_unit": "FP64 VALU",
@@ -421,6 +429,8 @@ def bench_dieoff(args, world, rank, dev):
                      "frac": achieved / FP64_PEAK_TFLOPS, **_pmc_traffic(4), "flop_per_point_year": flop_year},
         "cpu_baseline": None,
     }
+    if world == 1 and not args.no_projection:
+        result["projection"] = projection_block(args, dev, stream, [4])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle
         rng = np.random.default_rng(0)
@@ -488,15 +498,15 @@ def strong_scaling(model, s, tmax, rank, world, dev, args):
     eng.set_grid(g[r0:r1], g)
     eng.set_layout("ce")
     out = torch.zeros((s, cap), dtype=torch.float64, device=dev)
-    gathered = [torch.empty_like(out) for _ in range(world)] if rank == 0 else None
+    # the gather's targets on rank 0 (host tensors under a rehearsal backend)
+    gathered = [_coll_tensor(torch.empty_like(out), args) for _ in range(world)] if rank == 0 else None
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
         eng.run(out.data_ptr(), cap, stream)
 
     def gather():
-        src = _coll_tensor(out, args)
-        dist.gather(src, [_coll_tensor(x, args) for x in gathered] if gathered else None, dst=0)
+        dist.gather(_coll_tensor(out, args), gathered, dst=0)
 
     for _ in range(max(1, args.warmup)):
         step()
@@ -516,13 +526,139 @@ def strong_scaling(model, s, tmax, rank, world, dev, args):
     t = _coll_tensor(torch.tensor([dt], dtype=torch.float64, device=dev), args)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    same = None
+    if rank == 0:
+        # the gathered grid (the last pass's slabs, [c][e] each) against the
+        # whole grid computed by this one rank: the same bits, as the
+        # reference's MPI build gives the same file for any rank count
+        full = np.empty((s, s), dtype=np.float64)
+        for r in range(world):
+            a, b = mdist.row_slab(r, world, s)
+            full[:, a:b] = gathered[r][:, : b - a].cpu().numpy()
+        eng.set_grid(g, g)
+        one = torch.empty((s, s), dtype=torch.float64, device=dev)
+        eng.run(one.data_ptr(), s, stream)
+        torch.cuda.synchronize(dev)
+        same = bool(np.array_equal(full, one.cpu().numpy(), equal_nan=True))
     eng.close()
     units = s * s * (tmax - 1)
     return {"scaling": "strong", "grid": [s, s], "rows_per_rank": {"rank0": cap, "others": s // world},
+            "gathered_equals_one_rank": same, "backend": args.backend,
             "job_ms": job_ms, "value": units / (job_ms * 1e-3),
             "what": "fixed s x s grid in N e-row slabs: one pass per rank + one gather to rank 0",
             "steps_ms_per_step": dt / args.steps * 1e3, "steps_value": units * args.steps / dt,
             "steps_what": f"{args.steps} passes + one gather (the gather amortised)"}
+
+
+def _ms_per_pass(run, dev, reps):
+    """Mean wall (ms) of `reps` back-to-back passes after two warm ones,
+    bracketed by synchronize (the bench step's own timing)."""
+    run()
+    run()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+PROJ_NS = (2, 4, 8)
+
+
+def _project(t1_ms, slab_ms, nbytes):
+    """Projection record of one split: per N the slowest rank's pass against
+    the one-GPU pass, and the bytes rank 0 receives in the job's one gather
+    (((N - 1) / N of the grid, padded slabs), which only a multi-GPU run
+    times."""
+    out = {}
+    for n, ms in slab_ms.items():
+        worst = max(ms)
+        out[str(n)] = {"slab_ms": ms, "max_slab_ms": worst, "projected_speedup": t1_ms / worst,
+                       "gather_bytes_to_rank0": int(nbytes * (n - 1) / n)}
+    return out
+
+
+def project_likelihood(model, s, dev, stream, reps, splits=("e", "c")):
+    """Strong-scaling projection measured on ONE GPU: the fixed
+    s x s grid split over N = 2, 4, 8 ranks, each rank's exact slab timed
+    alone on this GPU as one pass of the path (the engine picks its kernels
+    for the slab's shape, as a rank would); projected_speedup = one-GPU pass /
+    slowest slab.  Splits: "e" -- e-row slabs (main_MIDASPOM_MPI.c:361-368,
+    remainder to rank 0); "c" -- c-column slabs (each rank then forms only
+    its own columns' per-c tables; in the [c][e] layout a c-slab is one
+    contiguous block for the gather, and the posterior file does not depend
+    on the split).  The slab kernel times name the term that bounds it."""
+    from midaspom_amd import dist as mdist
+    g, _ = mdp.grid(s, 0.0, 1.0)
+    eng = mdp.Engine(model, devices=[dev.index])
+    eng.set_layout("ce")
+    out = torch.empty((s, s), dtype=torch.float64, device=dev)
+
+    def timed(e, c, kernels=False):
+        eng.set_grid(e, c)
+        ms = _ms_per_pass(lambda: eng.run(out.data_ptr(), len(e), stream), dev, reps)
+        return ms, (eng.time_kernels(out.data_ptr(), len(e), stream, reps=reps) if kernels else None)
+
+    t1, k1 = timed(g, g, True)
+    res = {"one_gpu_ms": t1, "one_gpu_kernel_ms": k1, "reps": reps}
+    for split in splits:
+        slab_ms, kslab = {}, {}
+        for n in PROJ_NS:
+            slab_ms[n] = []
+            for r in range(n):
+                a, b = mdist.row_slab(r, n, s)
+                ms, km = timed(*((g[a:b], g) if split == "e" else (g, g[a:b])), kernels=(r == 0))
+                slab_ms[n].append(ms)
+                if km is not None:
+                    kslab[n] = km  # rank 0's slab (the largest: the remainder is its)
+        proj = _project(t1, slab_ms, s * s * 8)
+        for n in PROJ_NS:
+            proj[str(n)]["rank0_kernel_ms"] = kslab[n]
+        res[f"split_{split}"] = proj
+    eng.close()
+    return res
+
+
+def project_dieoff(s, dev, stream, reps):
+    """The same projection for config 4 (die-off (e, c, K_D) = s^3): e-row
+    slabs, each rank's slab timed alone on this GPU."""
+    from midaspom_amd import dist as mdist
+    inp = ROOT / "tests" / "golden" / "occupancies.txt"
+    g, _ = mdp.grid(s, 0.0, 1.0)
+    K = mdp.kgrid(s, 0.1, 100.0)
+    sc = mdp.Scenario(mdp.first_row(inp), "dieoff", m=400.0, d=100.0, device=dev.index)
+    out = torch.empty((s, s, s), dtype=torch.float64, device=dev)
+
+    def timed(e):
+        sc.set_grid(e, g, K, ts=20, tdis=10)
+        return _ms_per_pass(lambda: sc.run(out.data_ptr(), stream), dev, reps)
+
+    t1 = timed(g)
+    slab_ms = {n: [timed(g[a:b]) for a, b in (mdist.row_slab(r, n, s) for r in range(n))] for n in PROJ_NS}
+    sc.close()
+    return {"one_gpu_ms": t1, "reps": reps, "split_e": _project(t1, slab_ms, s ** 3 * 8)}
+
+
+def projection_block(args, dev, stream, cfgs):
+    """The projections of `cfgs` (each guarded: a failing leg reports its
+    error instead of costing the bench line)."""
+    res = {}
+    for c in cfgs:
+        try:
+            if c == 4:
+                res["config4"] = project_dieoff(args.grid4, dev, stream, reps=2)
+            else:
+                gen = CONFIGS[c]
+                m = mdp.Model.load(synth.write(Path(tempfile.mkdtemp(prefix="mdp_proj_")) / "in.txt", **gen["gen"]),
+                                   m=400.0, p=0.5, d=100.0)
+                res[f"config{c}"] = project_likelihood(m, gen["s"], dev, stream, reps=20 if c == 2 else 10)
+        except Exception as exc:  # noqa: BLE001 -- reported, not fatal
+            res[f"config{c}"] = {"error": repr(exc)}
+    res["what"] = ("strong scaling of the fixed grid projected from ONE GPU: each rank's exact slab timed alone "
+                   "(one pass); projected_speedup = one-GPU pass / slowest slab; the job's one gather is not in "
+                   "it (gather_bytes_to_rank0; the N-GPU lines time it)")
+    return res
 
 
 def resolve_world(args, env=None):
@@ -596,6 +732,8 @@ def main():
                     help="device layout of log L: ce = [c][e] (coalesced stores, default), ec = [e][c] rows")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank plumbing only, no GPU (tests)")
+    ap.add_argument("--no-projection", action="store_true",
+                    help="N = 1: skip the one-GPU strong-scaling projection of configs 2, 3, 4 and 6")
     args = ap.parse_args()
 
     world, rank, local, spawn = resolve_world(args)
@@ -756,7 +894,9 @@ def main():
         "data": "synthetic (SURVEY.md Appendix C generator, md5-checked input)",
         "config": {"workload": cfg["name"], "patches": model.n, "years": tmax, "grid": [world * s, s],
                    "per_rank_grid": [s, s], "nvar": model.nvar, "nstates": model.nstates,
-                   "nextid": model.nextid, "parallelism": f"e-row slabs x{world}" + (", RCCL gather" if world > 1 else ""),
+                   "nextid": model.nextid,
+                   "parallelism": f"e-row slabs x{world}" + (f", {_coll_name(args)} gather" if world > 1 else ""),
+                   "backend": args.backend if world > 1 else None,
                    # [c][e] is the product's layout: the CLIs (mdp_loglik_grid_layout), the torchrun
                    # drop-in (dist.gather_cols) and the normaliser / writer views all use it
                    "layout": "[c][e] (MDP_LAYOUT_CE, the drop-ins' layout)" if args.layout == "ce"
@@ -802,6 +942,8 @@ def main():
             "fwd_ps_per_point_use": fwd_ms * 1e9 / (s * s * max(1, info["nuses"])),
         },
     }
+    if world == 1 and not args.no_projection:
+        result["projection"] = projection_block(args, dev, stream, [2, 3, 4, 6] if args.config == 2 else [args.config])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         lik = torch.empty((s, s), dtype=torch.float64, device=dev)
         eng.run(lik.data_ptr(), s, stream)

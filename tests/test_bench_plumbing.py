@@ -78,3 +78,41 @@ def test_torchrun_launch_unchanged():
                        capture_output=True, text=True, timeout=240, env=_clean_env(), cwd=str(ROOT))
     assert r.returncode == 0, r.stderr
     _check_slabs(_json_line(r.stdout), 2)
+
+
+def test_projection_record():
+    """The one-GPU strong-scaling projection (bench.project_likelihood /
+    project_dieoff): per N the slowest rank's slab against the one-GPU pass,
+    and the bytes rank 0 receives in the job's one gather."""
+    b = _bench()
+    p = b._project(10.0, {2: [5.5, 5.0], 4: [3.0, 2.5, 2.5, 2.5], 8: [2.0] + [1.25] * 7}, 1024 * 1024 * 8)
+    assert set(p) == {"2", "4", "8"}
+    assert p["2"]["max_slab_ms"] == 5.5 and p["2"]["projected_speedup"] == pytest.approx(10 / 5.5)
+    assert p["8"]["projected_speedup"] == pytest.approx(5.0)
+    assert p["4"]["gather_bytes_to_rank0"] == 1024 * 1024 * 8 * 3 // 4
+    assert b.PROJ_NS == (2, 4, 8)
+
+
+def test_coll_name():
+    b = _bench()
+    assert b._coll_name(argparse.Namespace(backend="nccl")) == "RCCL"
+    assert b._coll_name(argparse.Namespace(backend="gloo")) == "gloo"
+
+
+@pytest.mark.gpu
+def test_projection_legs_on_gpu():
+    """The projection legs the default N = 1 line carries, on config 2 (both
+    splits) and a small die-off grid: every rank's slab timed, speedups > 0."""
+    import torch
+    b = _bench()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    res = b.projection_block(argparse.Namespace(grid4=32), dev, stream, [2, 4])
+    for key, splits in (("config2", ("split_e", "split_c")), ("config4", ("split_e",))):
+        r = res[key]
+        assert "error" not in r, r
+        assert r["one_gpu_ms"] > 0
+        for sp in splits:
+            for n in b.PROJ_NS:
+                rec = r[sp][str(n)]
+                assert len(rec["slab_ms"]) == n and rec["projected_speedup"] > 0
