@@ -1495,44 +1495,51 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
     }
 }
 
-// k_fwd_mmt<RT> (round 6): the same per-year GEMM as k_fwd_mma, for years of
-// up to 1 024 states, with three changes.
-//  * One state buffer in LDS, V[ROWS][PTS] (128 KiB: 256 x 64, 512 x 32 or
-//    1 024 x 16), instead of two: a wave keeps its tiles' new states in
-//    registers until every wave has read the year's old ones (a barrier),
-//    then stores them in place.  So 1 024-state years fit, and years of up to
-//    256 states take 64 points a block (RT = 4 point tiles share each C
-//    gather) where k_fwd_mma took 32.
+// k_fwd_mmt<RT, ROWS, DB> (round 6): the per-year GEMM of k_fwd_mma, for
+// years of up to 1 024 states, with three changes.
 //  * K lists per (year, column tile): the entry (k, m) only for m <= the
 //    largest nX over the tile's 16 new states (k_fwd_mma ran m up to |A_k|
-//    for every tile and multiplied the rest through zero slots).
-//  * A wave may own up to TMAX = 4 / RT tiles of a year (years of more than
-//    256 states: 17-64 tiles over 16 waves, dealt longest-list first); years
-//    of at most 8 tiles split each tile's K list into S slices as before, the
-//    partial products parked in rows past the year's tiles and summed in
-//    slice order after a second barrier (deterministic).
+//    for every tile and multiplied the rest through zero slots), and the
+//    gathers' Q-row offsets per (entry, new state) from a host table, so no
+//    descriptor lookup sits between a K entry and its gather.
+//  * Years of more than 256 states (ROWS 512 / 1 024, 32 / 16 points a
+//    block): ONE state buffer in LDS (DB = false, 128 KiB): a wave keeps its
+//    tiles' new states in registers until every wave has read the year's old
+//    ones (a barrier), then stores them in place.  A wave owns up to ROWS /
+//    256 tiles a year (17-64 tiles over 16 waves, longest lists first).
+//    Years of up to 128 / 256 states keep k_fwd_mma's two buffers (DB = true,
+//    64 / 32 points a block, one barrier a year).
+//  * Years of at most 16 tiles give every tile a wave and the spare waves to
+//    the tiles with the longest lists (a tile's list split into slices of at
+//    least two chunks); slice 1 parks its partial products in the tile's own
+//    destination rows (two buffers) or past the year's tiles (one buffer),
+//    later slices past the year's tiles, and slice 0 adds them in slice
+//    order after a barrier (deterministic).
 // Workgroups are dealt XCD-aware (the point blocks of one column on one XCD,
 // so the column's Q row is gathered from that XCD's L2).  The products sum
 // in another order than k_fwd_wide's (positive terms: ~1e-15 relative).
-constexpr uint32_t kMmtU = 2;           // K steps (of 4 entries) per pipeline chunk
+// K steps (of 4 entries) per pipeline chunk: 2, or 1 with 4 point tiles
+// (their 4 W operands a step leave no registers for a second step in flight)
+constexpr uint32_t mmt_u(uint32_t rt) { return rt == 4 ? 1u : 2u; }
 constexpr uint32_t kMmtMaxTiles = 64;   // column tiles a year (1 024 states)
 constexpr uint32_t mmt_pts(uint32_t rt) { return 16u * rt; }
 // power-table row stride (doubles): rows r and r + 1 on different LDS bank halves
 constexpr uint32_t mmt_ps(uint32_t rt) { return rt % 2 ? 16u * rt : 16u * rt + 16u; }
-// the instantiations: point tiles of 16 per block and state rows -- <2, 256>
-// (years of up to 256 states), <2, 512>, <1, 1 024>
-template <int RT, int ROWS>
+// the instantiations (RT point tiles of 16, ROWS state rows, two buffers or
+// one): <4, 128, true> years of up to 128 states, <2, 256, true> 256,
+// <2, 512, false> 512, <1, 1 024, false> 1 024
+template <int RT, int ROWS, bool DB>
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
     const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint2 *__restrict__ kt,
     const uint32_t *__restrict__ cidx, const uint2 *__restrict__ ktile, const uint2 *__restrict__ wplan, uint32_t tmax,
     double prior0, const double *__restrict__ evals, uint32_t ne, uint32_t maxA, double *__restrict__ out,
     uint32_t ld_out, uint32_t out_cs)
 {
-    constexpr uint32_t PTS = mmt_pts(RT), PS = mmt_ps(RT), TMAX = ROWS / 256;
-    static_assert(TMAX * 16 * 16 == ROWS && TMAX * RT <= 4, "tiles per wave");
+    constexpr uint32_t PTS = mmt_pts(RT), PS = mmt_ps(RT), TMAX = ROWS > 256 ? ROWS / 256 : 1, U = mmt_u(RT);
+    static_assert(TMAX * RT <= 4 && (ROWS <= 256 || TMAX * 256 == ROWS), "tiles per wave");
     extern __shared__ __attribute__((aligned(16))) double mlds[];
-    double *V = mlds;  // [state][point]
-    double *xp = V + (size_t)ROWS * PTS, *yp = xp + (size_t)(maxA + 1) * PS;  // [r][point]
+    double *Va = mlds, *Vb = DB ? mlds + (size_t)ROWS * PTS : mlds;  // [state][point]: read / written
+    double *xp = mlds + (DB ? 2 : 1) * (size_t)ROWS * PTS, *yp = xp + (size_t)(maxA + 1) * PS;  // [r][point]
     const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // XCD-aware: workgroups are dealt round-robin over the 8 XCDs; XCD x
     // takes a contiguous range of logical blocks, i.e. whole columns
@@ -1552,7 +1559,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
         }
     }
     const uint32_t np0 = np[0];
-    for (uint32_t i = threadIdx.x; i < ROWS * PTS; i += kMmaThreads) V[i] = i / PTS < np0 ? 1.0 : 0.0;
+    for (uint32_t i = threadIdx.x; i < ROWS * PTS; i += kMmaThreads) Va[i] = i / PTS < np0 ? 1.0 : 0.0;
     __syncthreads();
     const double *q = Q + (size_t)ic * ldQ;
     const uint32_t kk = lane >> 4, col = lane & 15u;
@@ -1589,22 +1596,22 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
     // table, so no descriptor lookup is on the gather's path)
     auto kent = [&](const Item &it, uint32_t ch, uint32_t u) {
         const uint32_t c = ch < it.nch ? ch : it.nch - 1;
-        return it.kl[(c * kMmtU + u) * 4 + kk];
+        return it.kl[(c * U + u) * 4 + kk];
     };
     auto coff = [&](const Item &it, uint32_t ch, uint32_t u) {
         const uint32_t c = ch < it.nch ? ch : it.nch - 1;
-        return it.cl[(c * kMmtU + u) * 64 + lane];
+        return it.cl[(c * U + u) * 64 + lane];
     };
     auto cval = [&](uint32_t o) { return *(const double *)((const char *)q + o); };
     // rings by chunk position j = ch - cb: K entries of ch .. ch + 3 (mod
     // 4), C offsets of ch + 1 and ch + 2 (mod 2; ch's were consumed by its
     // gathers), C values of ch and ch + 1 (mod 2)
-    uint2 ee[4][kMmtU];
-    uint32_t dd[2][kMmtU];
-    double bb[2][kMmtU];
+    uint2 ee[4][U];
+    uint32_t dd[2][U];
+    double bb[2][U];
     auto prime_a = [&](const Item &it) {
 #pragma unroll
-        for (uint32_t u = 0; u < kMmtU; ++u) {
+        for (uint32_t u = 0; u < U; ++u) {
             ee[0][u] = kent(it, it.cb, u);
             ee[1][u] = kent(it, it.cb + 1, u);
             ee[2][u] = kent(it, it.cb + 2, u);
@@ -1614,7 +1621,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
     };
     auto prime_b = [&]() {
 #pragma unroll
-        for (uint32_t u = 0; u < kMmtU; ++u) bb[0][u] = cval(dd[0][u]);
+        for (uint32_t u = 0; u < U; ++u) bb[0][u] = cval(dd[0][u]);
     };
     Item cur = plan(tmax > 1 ? 1u : 0u, 0);
     if (tmax > 1 && cur.active) {
@@ -1642,20 +1649,20 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
             auto chunk = [&](uint32_t ch, auto jc) {
                 constexpr uint32_t j = decltype(jc)::value;
 #pragma unroll
-                for (uint32_t u = 0; u < kMmtU; ++u) ee[(j + 3) & 3][u] = kent(cur, ch + 3, u);
+                for (uint32_t u = 0; u < U; ++u) ee[(j + 3) & 3][u] = kent(cur, ch + 3, u);
 #pragma unroll
-                for (uint32_t u = 0; u < kMmtU; ++u) bb[(j + 1) & 1][u] = cval(dd[(j + 1) & 1][u]);
+                for (uint32_t u = 0; u < U; ++u) bb[(j + 1) & 1][u] = cval(dd[(j + 1) & 1][u]);
 #pragma unroll
-                for (uint32_t u = 0; u < kMmtU; ++u) dd[j & 1][u] = coff(cur, ch + 2, u);
+                for (uint32_t u = 0; u < U; ++u) dd[j & 1][u] = coff(cur, ch + 2, u);
 #pragma unroll
-                for (uint32_t u = 0; u < kMmtU; ++u) {
+                for (uint32_t u = 0; u < U; ++u) {
                     const uint2 en = ee[j][u];
 #pragma unroll
                     for (uint32_t h = 0; h < RT; ++h) {
                         const uint32_t pb = (h * 16 + col) * 8u;
                         const double wt = *(const double *)((const char *)xp + (en.y & 0xffffu) + pb) *
                                           *(const double *)((const char *)yp + (en.x >> 18) + pb);
-                        const double av = *(const double *)((const char *)V + (en.x & 0x3ffffu) + pb) * wt;
+                        const double av = *(const double *)((const char *)Va + (en.x & 0x3ffffu) + pb) * wt;
                         ac[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(bb[j & 1][u], av, ac[h], 0, 0, 0);
                     }
                 }
@@ -1676,38 +1683,59 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
         const Item nxt = plan(t + 1 < tmax ? t + 1 : t, 0);
         const bool pnext = t + 1 < tmax && nxt.active;
         if (pnext) prime_a(nxt);
-        __syncthreads();  // every wave has read the year's old states
+        if constexpr (!DB) __syncthreads();  // one buffer: every wave has read the year's old states
         // the lane's accumulators: states tile * 16 + kk + 4 r of point
-        // h * 16 + col; slices ks >= 1 park theirs past row npcp (partial
-        // block pbase + ks - 1 of the year: at most 16 - tiles of them)
-        auto part = [&](uint32_t ks) {
-            return V + (size_t)(first.npcp + (first.pbase + ks - 1) * 16) * PTS + lane;
+        // h * 16 + col.  A sliced tile's slices ks >= 1 park theirs: slice 1
+        // of two buffers in the tile's destination rows, the rest past row
+        // npcp in partial block pbase + ks - (DB ? 2 : 1) of the year (the
+        // host keeps them within ROWS rows)
+        auto dst_of = [&](uint32_t tile) { return Vb + (size_t)(tile * 16 + kk) * PTS + col; };
+        auto park = [&](uint32_t ks) {
+            return Vb + (size_t)(first.npcp + (first.pbase + ks - (DB ? 2u : 1u)) * 16) * PTS + lane;
         };
         if (first.split) {
             if (first.active && first.ks >= 1) {
-                double *pk = part(first.ks);
+                if (DB && first.ks == 1) {
+                    double *dst = dst_of(first.tile);
 #pragma unroll
-                for (uint32_t h = 0; h < RT; ++h)
+                    for (uint32_t h = 0; h < RT; ++h)
 #pragma unroll
-                    for (uint32_t r = 0; r < 4; ++r) pk[(h * 4 + r) * 64] = acc[0][h][r];
+                        for (uint32_t r = 0; r < 4; ++r) dst[(size_t)(4 * r) * PTS + h * 16] = acc[0][h][r];
+                } else {
+                    double *pk = park(first.ks);
+#pragma unroll
+                    for (uint32_t h = 0; h < RT; ++h)
+#pragma unroll
+                        for (uint32_t r = 0; r < 4; ++r) pk[(h * 4 + r) * 64] = acc[0][h][r];
+                }
             }
             __syncthreads();
             if (first.active && first.ks == 0)
                 for (uint32_t j = 1; j < first.S; ++j) {
-                    const double *pj = part(j);
+                    if (DB && j == 1) {
+                        const double *dst = dst_of(first.tile);
 #pragma unroll
-                    for (uint32_t h = 0; h < RT; ++h)
+                        for (uint32_t h = 0; h < RT; ++h)
 #pragma unroll
-                        for (uint32_t r = 0; r < 4; ++r) acc[0][h][r] = acc[0][h][r] + pj[(h * 4 + r) * 64];
+                            for (uint32_t r = 0; r < 4; ++r)
+                                acc[0][h][r] = acc[0][h][r] + dst[(size_t)(4 * r) * PTS + h * 16];
+                    } else {
+                        const double *pj = park(j);
+#pragma unroll
+                        for (uint32_t h = 0; h < RT; ++h)
+#pragma unroll
+                            for (uint32_t r = 0; r < 4; ++r) acc[0][h][r] = acc[0][h][r] + pj[(h * 4 + r) * 64];
+                    }
                 }
-            // (the final stores below go to rows < npcp: no partial is overwritten)
+            // (the final stores below go to rows < npcp, never to a parked
+            // block, and a tile's slice-1 rows are read only by its slice 0)
         }
         // (padded states l >= npc hold 0: their C values are the zero slot)
 #pragma unroll
         for (uint32_t i = 0; i < TMAX; ++i) {
             const Item it = i == 0 ? first : plan(t, i);
             if (!it.active || it.ks != 0) break;
-            double *dst = V + (size_t)(it.tile * 16 + kk) * PTS + col;
+            double *dst = dst_of(it.tile);
 #pragma unroll
             for (uint32_t h = 0; h < RT; ++h)
 #pragma unroll
@@ -1715,12 +1743,17 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
         }
         if (pnext) prime_b();
         __syncthreads();
+        if constexpr (DB) {
+            double *tv = Va;
+            Va = Vb;
+            Vb = tv;
+        }
         cur = nxt;
     }
     if (threadIdx.x < PTS) {
         const uint32_t ie = p0 + threadIdx.x, npl = np[tmax - 1];
         double L = 0.0;
-        for (uint32_t l = 0; l < npl; ++l) L += V[l * PTS + threadIdx.x] * prior0;
+        for (uint32_t l = 0; l < npl; ++l) L += Va[l * PTS + threadIdx.x] * prior0;
         if (ie < ne) out[(size_t)ie * ld_out + (size_t)ic * out_cs] = log(L);
     }
 }
@@ -2535,17 +2568,32 @@ size_t device_lds_max()
 }
 
 // k_fwd_mmt: the state buffer and the power tables of the block's points
+// k_fwd_mmt's shapes by the largest year: RT point tiles, state rows, two buffers
+struct MmtShape {
+    uint32_t rt, rows;
+    bool db;
+};
+inline MmtShape mmt_shape(uint32_t npmax)
+{
+    if (npmax <= 128) return {4u, 128u, true};
+    if (npmax <= 256) return {2u, 256u, true};
+    if (npmax <= 512) return {2u, 512u, false};
+    return {1u, 1024u, false};
+}
+
 size_t mmt_lds(const mdp_engine *eng)
 {
-    const uint32_t rt = eng->mmt_rt;
-    return ((size_t)eng->mmt_rows * mmt_pts(rt) + 2 * ((size_t)eng->maxA + 1) * mmt_ps(rt)) * sizeof(double);
+    const MmtShape sh = mmt_shape(eng->npmax);
+    return ((sh.db ? 2 : 1) * (size_t)sh.rows * mmt_pts(sh.rt) + 2 * ((size_t)eng->maxA + 1) * mmt_ps(sh.rt)) *
+           sizeof(double);
 }
 
 const void *mmt_kernel(const mdp_engine *eng)
 {
-    if (eng->mmt_rows == 256) return (const void *)k_fwd_mmt<2, 256>;
-    if (eng->mmt_rows == 512) return (const void *)k_fwd_mmt<2, 512>;
-    return (const void *)k_fwd_mmt<1, 1024>;
+    if (eng->mmt_rows == 128) return (const void *)k_fwd_mmt<4, 128, true>;
+    if (eng->mmt_rows == 256) return (const void *)k_fwd_mmt<2, 256, true>;
+    if (eng->mmt_rows == 512) return (const void *)k_fwd_mmt<2, 512, false>;
+    return (const void *)k_fwd_mmt<1, 1024, false>;
 }
 
 // k_fwd_mmt's tables (c-independent): years of at most 1 024 states.
@@ -2563,8 +2611,9 @@ const void *mmt_kernel(const mdp_engine *eng)
 void build_mmt_plan(mdp_engine *eng)
 {
     if (eng->npmax > 1024 || eng->maxA > 24 || eng->tmax < 2) return;
-    const uint32_t rows = eng->npmax <= 256 ? 256u : eng->npmax <= 512 ? 512u : 1024u, rt = rows == 1024 ? 1u : 2u;
-    const uint32_t pts = mmt_pts(rt), ps = mmt_ps(rt), tmaxit = rows / 256, cw = 4 * kMmtU;
+    const MmtShape shp = mmt_shape(eng->npmax);
+    const uint32_t rows = shp.rows, rt = shp.rt, pts = mmt_pts(rt), ps = mmt_ps(rt);
+    const uint32_t tmaxit = rows > 256 ? rows / 256 : 1, cw = 4 * mmt_u(rt), inplace = shp.db ? 2u : 1u;
     const uint32_t none = (uint32_t)eng->ncoef_d;
     if (none > kOffMask) return;
     eng->mmt_rt = rt;
@@ -2610,14 +2659,20 @@ void build_mmt_plan(mdp_engine *eng)
         uint2 *wp = eng->mmt_wplan.data() + (size_t)t * 16 * tmaxit;
         if (ncol <= 16) {
             // waves per tile: one each, the rest to the tile whose slices
-            // are longest (each slice at least two chunks)
+            // are longest (each slice at least two chunks; the parked
+            // partials -- every slice past the first `inplace` of a tile --
+            // within the buffer's rows past the year's tiles)
             std::vector<uint32_t> w(ncol, 1);
+            uint32_t parked = 0;
+            const uint32_t room = (rows - ncol * 16) / 16;
             for (uint32_t spare = 16 - ncol; spare; --spare) {
                 uint32_t best = ncol;
                 for (uint32_t i = 0; i < ncol; ++i)
-                    if (nch[i] / (w[i] + 1) >= 2 && (best == ncol || nch[i] * w[best] > nch[best] * w[i])) best = i;
+                    if (nch[i] / (w[i] + 1) >= 2 && (w[i] + 1 <= inplace || parked < room) &&
+                        (best == ncol || nch[i] * w[best] > nch[best] * w[i]))
+                        best = i;
                 if (best == ncol) break;
-                ++w[best];
+                if (++w[best] > inplace) ++parked;
             }
             const uint32_t split = *std::max_element(w.begin(), w.end()) > 1 ? 1u : 0u;
             for (uint32_t wv = 0; wv < 16; ++wv)
@@ -2629,7 +2684,7 @@ void build_mmt_plan(mdp_engine *eng)
                     wp[wv * tmaxit] = make_uint2(cb | ce << 16, tile | ks << 8 | w[tile] << 12 | pbase << 17 |
                                                                    split << 22 | 1u << 24);
                 }
-                pbase += w[tile] - 1;
+                pbase += w[tile] > inplace ? w[tile] - inplace : 0;
             }
         } else {
             std::vector<uint32_t> order(ncol), cnt(16, 0);
@@ -3526,16 +3581,18 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
         }
     } else if (eng->mmt) {  // the matrix-core forward: every c in one launch, blocks dealt XCD-aware
         const uint32_t rt = eng->mmt_rt, rows = eng->mmt_rows, npb = (d.ne + mmt_pts(rt) - 1) / mmt_pts(rt);
+        const bool db = mmt_shape(eng->npmax).db;
         const uint64_t nb = (uint64_t)npb * d.nc;
         if (nb > 0x7fffffffull) return mdp_set_error(MDP_EUNSUPPORTED, "grid of %llu k_fwd_mmt workgroups", (unsigned long long)nb);
-        note_launch(eng, "k_fwd_mmt<%u,%u>", rt, rows);
-#define MDP_MMT(RT, ROWS) \
-    hipLaunchKernelGGL((k_fwd_mmt<RT, ROWS>), dim3((uint32_t)nb), dim3(kMmaThreads), mmt_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, \
+        note_launch(eng, "k_fwd_mmt<%u,%u,%s>", rt, rows, db ? "2buf" : "1buf");
+#define MDP_MMT(RT, ROWS, DB) \
+    hipLaunchKernelGGL((k_fwd_mmt<RT, ROWS, DB>), dim3((uint32_t)nb), dim3(kMmaThreads), mmt_lds(eng), s, d.Qrow, (uint32_t)eng->ldQ, \
                        d.np_d, d.mmt_kt, d.mmt_cidx, d.mmt_ktile, d.mmt_wplan, eng->tmax, eng->prior0, d.e, d.ne, \
                        eng->maxA, out, os.se, os.sc)
-        if (rows == 256) MDP_MMT(2, 256);
-        else if (rows == 512) MDP_MMT(2, 512);
-        else MDP_MMT(1, 1024);
+        if (rows == 128) MDP_MMT(4, 128, true);
+        else if (rows == 256) MDP_MMT(2, 256, true);
+        else if (rows == 512) MDP_MMT(2, 512, false);
+        else MDP_MMT(1, 1024, false);
 #undef MDP_MMT
     } else if (eng->mma) {  // round 5's matrix-core forward (MDP_WIDE_MMA=1; years of up to 256 states)
         uint32_t se = os.se, sc = os.sc;

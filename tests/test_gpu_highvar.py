@@ -138,6 +138,6 @@ def test_wide_path(nvar, chunked, mma, monkeypatch):
     env = {"MDP_WIDE": "1", **({"MDP_WIDE_CB": "1"} if chunked else {}), **({} if mma else {"MDP_WIDE_MMA": "0"})}
     got, launched, info = _run(model, E_SMALL, C_SMALL, env, monkeypatch)
     assert info["variant"] >= 20000
-    fwd = "k_fwd_mmt<2,256>" if mma else "k_fwd_wide"
+    fwd = "k_fwd_mmt<4,128,2buf>" if mma else "k_fwd_wide"
     assert {f"k_witems<{NV[nvar]}>", "k_wq", fwd, "k_zrows"} <= launched, launched
     assert_loglik_close(got[ie, ic], ref)

@@ -62,7 +62,7 @@ CASES = {
     "wide_mma5": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
                   {"MDP_WIDE": "1", "MDP_WIDE_MMA": "1"}, "k_fwd_mma"),
     "wide_big": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 10, 4, {1: 9})), 70, 37,
-                 {}, "k_fwd_mmt<2,512>"),
+                 {}, "k_fwd_mmt<2,512,1buf>"),
     "wide_plain": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
                    {"MDP_WIDE": "1", "MDP_WIDE_MMA": "0"}, "k_fwd_wide"),
 }
