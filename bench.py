@@ -483,27 +483,30 @@ def time_job(step, gather, dev, world, reps=3):
 
 def strong_scaling(model, s, tmax, rank, world, dev, args):
     """The reference's MPI job on a FIXED grid (main_MIDASPOM_MPI.c:361-368,
-    482-506): the s x s grid split into `world` e-row slabs (remainder to
-    rank 0), each rank one pass over its slab in the product's [c][e]
-    layout, then ONE gather of the padded slabs to rank 0 (RCCL over xGMI).
-    Timed as that job (median of 10, barrier + synchronize either side, max
-    over ranks) and as K passes + one gather; value = s^2 (tmax - 1) units
-    over the time.  Work per rank shrinks as N grows, so this is the
-    strong-scaling figure ("scaling": "strong")."""
+    482-506) as the drop-in runs it (midaspom_amd/dist.py): the s x s grid
+    split into `world` c-column slabs (remainder to rank 0; each rank forms
+    only its own columns' per-c tables, for the whole grid's |c| bound), each
+    rank one pass over its slab in the product's [c][e] layout, then ONE
+    gather of the padded slabs to rank 0 (RCCL over xGMI).  Timed as that job
+    (median of 10, barrier + synchronize either side, max over ranks) and as
+    K passes + one gather; value = s^2 (tmax - 1) units over the time.  Work
+    per rank shrinks as N grows, so this is the strong-scaling figure
+    ("scaling": "strong")."""
     from midaspom_amd import dist as mdist
     g, _ = mdp.grid(s, 0.0, 1.0)
-    r0, r1 = mdist.row_slab(rank, world, s)
+    c0, c1 = mdist.row_slab(rank, world, s)
     cap = s // world + s % world
     eng = mdp.Engine(model, devices=[dev.index])
-    eng.set_grid(g[r0:r1], g)
+    eng.set_cbound(float(np.abs(g).max()))
+    eng.set_grid(g, g[c0:c1])
     eng.set_layout("ce")
-    out = torch.zeros((s, cap), dtype=torch.float64, device=dev)
+    out = torch.zeros((cap, s), dtype=torch.float64, device=dev)
     # the gather's targets on rank 0 (host tensors under a rehearsal backend)
     gathered = [_coll_tensor(torch.empty_like(out), args) for _ in range(world)] if rank == 0 else None
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
-        eng.run(out.data_ptr(), cap, stream)
+        eng.run(out.data_ptr(), s, stream)
 
     def gather():
         dist.gather(_coll_tensor(out, args), gathered, dst=0)
@@ -531,10 +534,10 @@ def strong_scaling(model, s, tmax, rank, world, dev, args):
         # the gathered grid (the last pass's slabs, [c][e] each) against the
         # whole grid computed by this one rank: the same bits, as the
         # reference's MPI build gives the same file for any rank count
-        full = np.empty((s, s), dtype=np.float64)
+        full = np.empty((s, s), dtype=np.float64)  # [c][e]
         for r in range(world):
             a, b = mdist.row_slab(r, world, s)
-            full[:, a:b] = gathered[r][:, : b - a].cpu().numpy()
+            full[a:b] = gathered[r][: b - a].cpu().numpy()
         eng.set_grid(g, g)
         one = torch.empty((s, s), dtype=torch.float64, device=dev)
         eng.run(one.data_ptr(), s, stream)
@@ -542,10 +545,11 @@ def strong_scaling(model, s, tmax, rank, world, dev, args):
         same = bool(np.array_equal(full, one.cpu().numpy(), equal_nan=True))
     eng.close()
     units = s * s * (tmax - 1)
-    return {"scaling": "strong", "grid": [s, s], "rows_per_rank": {"rank0": cap, "others": s // world},
+    return {"scaling": "strong", "grid": [s, s], "split": "c-column slabs (dist.py)",
+            "cols_per_rank": {"rank0": cap, "others": s // world},
             "gathered_equals_one_rank": same, "backend": args.backend,
             "job_ms": job_ms, "value": units / (job_ms * 1e-3),
-            "what": "fixed s x s grid in N e-row slabs: one pass per rank + one gather to rank 0",
+            "what": "fixed s x s grid in N c-column slabs: one pass per rank + one gather to rank 0",
             "steps_ms_per_step": dt / args.steps * 1e3, "steps_value": units * args.steps / dt,
             "steps_what": f"{args.steps} passes + one gather (the gather amortised)"}
 
@@ -593,6 +597,7 @@ def project_likelihood(model, s, dev, stream, reps, splits=("e", "c")):
     g, _ = mdp.grid(s, 0.0, 1.0)
     eng = mdp.Engine(model, devices=[dev.index])
     eng.set_layout("ce")
+    eng.set_cbound(float(np.abs(g).max()))  # as a column-slab rank builds its tables (dist.py)
     out = torch.empty((s, s), dtype=torch.float64, device=dev)
 
     def timed(e, c, kernels=False):
@@ -705,7 +710,7 @@ def dry_run(args, world, rank):
         dist.init_process_group("gloo")
     s = CONFIGS[args.config]["s"]
     mine = {"rank": rank, "weak_rows": [rank * s, (rank + 1) * s],
-            "strong_rows": {str(c): list(mdist.row_slab(rank, world, CONFIGS[c]["s"])) for c in (2, 3)}}
+            "strong_cols": {str(c): list(mdist.row_slab(rank, world, CONFIGS[c]["s"])) for c in (2, 3)}}
     allr = [None] * world
     if world > 1:
         dist.all_gather_object(allr, mine)

@@ -36,7 +36,7 @@ extern "C" {
 #define MDP_ENODEV (-5)       /* no usable GPU                             */
 #define MDP_EUNSUPPORTED (-6) /* problem outside the engine's limits       */
 
-#define MDP_ABI_VERSION 8
+#define MDP_ABI_VERSION 9
 
 /* ------------------------------------------------------------------ */
 /* Host model: parse + state enumeration (the reference's L2 layer)    */
@@ -162,6 +162,14 @@ int mdp_loglik_grid_layout(mdp_engine *engine, const double *e, uint32_t ne, con
                            int layout, double *out);
 int mdp_engine_set_grid(mdp_engine *engine, const double *e, uint32_t ne, const double *c,
                         uint32_t nc);
+/* The bound the per-c tables of the following grids are built for (ABI 9):
+ * max(|c| over the grid, cbound).  The Z rows split their always-zero
+ * columns into explicit factors and a log series by |c| S, so
+ * two grids with different max |c| evaluate some columns in different (equally
+ * exact, ~1e-15) forms.  Ranks that compute column slabs of ONE grid pass
+ * that grid's max |c| here, so each computes the bits a single-rank run
+ * would (midaspom_amd/dist.py).  0 (the default) uses the grid's own. */
+int mdp_engine_set_cbound(mdp_engine *engine, double cbound);
 int mdp_engine_run(mdp_engine *engine, double *d_out, uint32_t ld_out, void *stream);
 
 /* Kernel timing: when enabled, every kernel of a run is launched with its own

@@ -183,6 +183,12 @@ class Engine:
         check(lib().mdp_engine_set_grid(self._h, _dptr(e), e.size, _dptr(c), c.size))
         self.ne, self.nc = e.size, c.size
 
+    def set_cbound(self, cbound: float) -> None:
+        """Build the per-c tables of the following grids for |c| <= max(the
+        grid's, cbound) (ABI 9): ranks computing column slabs of one grid pass
+        its max |c|, so every slab has the bits of a one-rank run."""
+        check(lib().mdp_engine_set_cbound(self._h, float(cbound)))
+
     def set_layout(self, layout: str) -> None:
         """Layout ``run`` writes: "ec" (default) out[ie*ld + ic], the
         reference's lik[i][j]; "ce" out[ic*ld + ie] (ld >= ne), whose stores

@@ -111,6 +111,7 @@ SIGNATURES = [
     ("mdp_engine_set_grid", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_u32, c_dbl_p, c_u32]),
     ("mdp_engine_run", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u32, ctypes.c_void_p]),
     ("mdp_engine_set_layout", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("mdp_engine_set_cbound", ctypes.c_int, [ctypes.c_void_p, ctypes.c_double]),
     ("mdp_engine_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("mdp_engine_kernel_ms", ctypes.c_int, [ctypes.c_void_p, c_dbl_p, ctypes.c_int]),
     ("mdp_engine_time_kernels", ctypes.c_int,

@@ -116,8 +116,13 @@ def main(argv=None) -> int:
             dist.init_process_group(backend)
         compute = mdist.gpu_slab_compute(model, dev)
         out(f"Starting parallel likelihood computation process {rank + 1}/{world}\n", all_ranks=True)
+        # this rank's c columns for every e (dist.py: the per-c tables split
+        # with the grid; built for the whole grid's |c| bound, so the same
+        # bits as one rank); the progress lines keep the reference's e-row
+        # slabs (main_MIDASPOM_MPI.c:361-368, :463)
+        c0, c1 = mdist.row_slab(rank, world, a.s)
+        local_lik = compute(g, g[c0:c1], cbound=float(abs(g).max()))
         r0, r1 = mdist.row_slab(rank, world, a.s)
-        local_lik = compute(g[r0:r1], g)
         for ie in range(r0, r1):  # main_MIDASPOM_MPI.c:463
             out(f"{(ie + 1 - r0) * 100.0 / (r1 - r0):.2f}% done\n")
         out(f"end likelihood computation process {rank + 1}/{world}\n", all_ranks=True)
@@ -125,8 +130,8 @@ def main(argv=None) -> int:
             out(f"Sending data (proc {rank})... ", all_ranks=True)
         else:
             out(f"Gathering data from {world - 1} proc... ")
-        lik = mdist.gather_cols(local_lik, rank, world, a.s, a.s,
-                                device=None if backend == "nccl" else "cpu")
+        lik = mdist.gather_colslabs(local_lik, rank, world, a.s, a.s,
+                                    device=None if backend == "nccl" else "cpu")
         out("done\n", all_ranks=True)
         compute.engine.close()
         dist.destroy_process_group()

@@ -1930,6 +1930,7 @@ struct DevCtx {
     uint32_t ldv = 0;
     bool fused = false;  // this grid runs the fused forward kernel (no k_qrows)
     bool tall = false;   // this grid runs the reading kernel at kJitKblockTall threads
+    uint32_t ncu = 0;    // the device's compute units (0: not asked yet)
     // wide path: per-chunk item factors, state-vector scratch, tables
     double *Pg = nullptr, *V = nullptr;
     size_t cap_pg = 0, cap_v = 0;
@@ -2046,6 +2047,7 @@ struct mdp_engine {
     std::vector<std::vector<char>> chunk_code;    // their code objects
     bool qglobal = false;     // Q rows built by k_zrows + k_witems + k_wq (k_qrows' tables exceed the LDS)
     int layout = MDP_LAYOUT_EC;  // mdp_engine_run's output layout (mdp_engine_set_layout)
+    double cbound = 0.0;         // the per-c tables' |c| bound at least this (mdp_engine_set_cbound)
     int fused_mode = -1;            // MDP_FUSED: -1 auto, 0, 1
     MdpJitPlan jit_plan;
     // direct path (jit): k_qrows computes Pc[j][b] for the needed (j, b)
@@ -3322,7 +3324,7 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     }
     const bool qglobal = eng->wide || eng->qglobal;  // Q rows from k_zrows + k_witems + k_wq
     if (eng->wide || eng->jit) {
-        double cmax = 0.0;
+        double cmax = eng->cbound;
         for (uint32_t i = 0; i < nc; ++i) cmax = std::isnan(c[i]) ? c[i] : std::max(cmax, std::fabs(c[i]));
         if ((rc = dev_reserve(&d.Qrow, &d.cap_qrow, (size_t)nc * eng->ldQ))) return rc;
         if (!(d.zs_cmax == cmax) && (rc = upload_qrows_tables(eng, d, cmax))) return rc;
@@ -3379,9 +3381,17 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
                   d.zs_kmax <= eng->jit_plan.kzmax && (eng->fused_mode == 1 || (eng->fused_mode == -1 && gy <= 1));
         // a column of a tall grid (an even number of e blocks, so no lane more
         // idles) in half the blocks of twice the threads: each block stages
-        // its column's Q row once (config 3: forward 45.7-46.9 -> 44.3 us)
+        // its column's Q row once (config 3: forward 45.7-46.9 -> 44.3 us) --
+        // while that still leaves a block for every CU (a column slab of
+        // config 3, 1 024 x 128: 128 tall blocks would idle half the chip)
+        if (!d.ncu) {
+            int v = 0;
+            d.ncu = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d.device) == hipSuccess && v > 0
+                        ? (uint32_t)v : 256u;
+        }
         d.tall = !d.fused && eng->chunks.empty() && !eng->jit_plan.vlds && !eng->jit_shape_env &&
-                 eng->jit_kblock * 2 == (uint32_t)kJitKblockTall && gy >= 2 && gy % 2 == 0;
+                 eng->jit_kblock * 2 == (uint32_t)kJitKblockTall && gy >= 2 && gy % 2 == 0 &&
+                 (uint64_t)nc * (gy / 2) >= d.ncu;
         if ((rc = jit_load(eng, d, d.fused ? 1 : d.tall ? 2 : 0))) return rc;
         if (!eng->chunks.empty()) {  // the state vectors handed between chunks
             d.ldv = gy * eng->jit_kblock * (uint32_t)eng->jit_epl;
@@ -4121,6 +4131,14 @@ int mdp_engine_set_grid(mdp_engine *eng, const double *e, uint32_t ne, const dou
     if (eng->devs.size() != 1)
         return mdp_set_error(MDP_EINVAL, "mdp_engine_set_grid needs a single-device engine");
     return set_grid_dev(eng, eng->devs[0], e, ne, c, nc);
+}
+
+int mdp_engine_set_cbound(mdp_engine *eng, double cbound)
+{
+    if (!eng) return mdp_set_error(MDP_EINVAL, "null argument");
+    if (!(cbound >= 0.0) || std::isinf(cbound)) return mdp_set_error(MDP_EINVAL, "cbound %g (want a finite value >= 0)", cbound);
+    eng->cbound = cbound;
+    return MDP_OK;
 }
 
 int mdp_engine_set_layout(mdp_engine *eng, int layout)

@@ -1,10 +1,18 @@
-"""One process per GPU: e-row slabs + a single gather (the MIDASPOM_MPI.out
-decomposition, sources/main_MIDASPOM_MPI.c:361-368 and :482-506).
+"""One process per GPU: grid slabs + a single gather (the MIDASPOM_MPI.out
+job shape, sources/main_MIDASPOM_MPI.c:361-368 and :482-506).
 
-Rank r computes rows [r0, r1) of the s x s log-likelihood grid on its own
-GPU; the slabs meet on rank 0 in ONE collective (torch.distributed gather:
-RCCL over xGMI with the "nccl" backend, gloo on CPU), padded to equal size
-because collectives move equal-sized buffers.  Rank 0 normalises and writes.
+The reference splits the s x s grid into e-row slabs (remainder to rank 0).
+Every rank then forms all s columns' per-c coefficient tables, a fixed cost
+that does not shrink with the rank count, so the GPU drop-in splits the c
+columns instead (round 6): rank r computes columns [c0, c1) -- the same
+partition function, row_slab, on the c axis -- for every e, in the devices'
+[c][e] layout, where a column slab is one contiguous block; the slabs meet on
+rank 0 in ONE collective (torch.distributed gather: RCCL over xGMI with the
+"nccl" backend, gloo on CPU), padded to equal size because collectives move
+equal-sized buffers.  Every rank builds its tables for the whole grid's max
+|c| (mdp_engine_set_cbound), so the gathered grid has the bits of a one-rank
+run and the posterior file does not depend on the rank count.  Rank 0
+normalises and writes.  The e-row helpers stay for the row-split callers.
 """
 from __future__ import annotations
 
@@ -71,6 +79,31 @@ def gather_cols(local, rank: int, world: int, s: int, nc: int, device=None):
     return full.T
 
 
+def gather_colslabs(local, rank: int, world: int, ne: int, nc: int, device=None):
+    """Gather every rank's column slab (torch tensor [cols, ne], float64: the
+    [c][e] layout) to rank 0 in one collective.  Returns on rank 0 the
+    transposed view of the full [nc, ne] array -- indexed [ie][ic] like
+    gather_rows' result; log_total / write_posterior read it in place -- and
+    None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    avg, rem = divmod(nc, world)
+    cap = avg + rem
+    dev = local.device if device is None else device
+    buf = torch.zeros((cap, ne), dtype=torch.float64, device=dev)
+    buf[: local.shape[0]] = local
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, parts, dst=0)
+    if rank != 0:
+        return None
+    full = np.empty((nc, ne), dtype=np.float64)
+    for r in range(world):
+        c0, c1 = row_slab(r, world, nc)
+        full[c0:c1] = parts[r][: c1 - c0].cpu().numpy()
+    return full.T
+
+
 def distributed_loglik(e, c, rank: int, world: int,
                        compute: Callable[[np.ndarray, np.ndarray], object], device=None):
     """Each rank computes its slab with `compute(e_slab, c)` (a torch tensor
@@ -109,9 +142,12 @@ def gpu_slab_compute(model, device_index: int):
     eng = mdp.Engine(model, devices=[device_index])
     eng.set_layout("ce")
 
-    def compute(e_slab, c):
+    def compute(e_slab, c, cbound=0.0):
+        """log L of e_slab x c as [len(c), len(e_slab)]; cbound: the whole
+        grid's max |c| when c is a column slab of it."""
         out = torch.empty((len(c), len(e_slab)), dtype=torch.float64, device=f"cuda:{device_index}")
-        if len(e_slab):
+        if len(e_slab) and len(c):
+            eng.set_cbound(cbound)
             eng.set_grid(e_slab, c)
             eng.run(out.data_ptr(), len(e_slab), torch.cuda.current_stream(device_index).cuda_stream)
         return out

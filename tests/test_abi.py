@@ -40,7 +40,7 @@ def test_python_binding_covers_header():
 
 
 def test_abi_version():
-    assert _lib.lib().mdp_abi_version() == 8
+    assert _lib.lib().mdp_abi_version() == 9
 
 
 def test_engine_library_is_gfx950():

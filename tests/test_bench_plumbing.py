@@ -54,7 +54,7 @@ def _json_line(out):
 def _check_slabs(res, n):
     assert res["n_gpus"] == n and [r["rank"] for r in res["ranks"]] == list(range(n))
     for cfg, s in (("2", 512), ("3", 1024)):
-        rows = [r["strong_rows"][cfg] for r in res["ranks"]]
+        rows = [r["strong_cols"][cfg] for r in res["ranks"]]
         assert rows[0][0] == 0 and rows[-1][1] == s
         assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))  # contiguous, in rank order
         assert rows[0][1] - rows[0][0] == s // n + s % n      # the remainder on rank 0

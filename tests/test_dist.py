@@ -1,5 +1,6 @@
-"""Multi-process path on CPU: world_size-2 gloo ranks shard the e rows as
-main_MIDASPOM_MPI.c:361-368 does and gather them to rank 0 in one
+"""Multi-process path on CPU: world_size-2/3 gloo ranks shard the grid --
+the e rows as main_MIDASPOM_MPI.c:361-368 does, and the c columns as the
+drop-in does (dist.py, round 6) -- and gather the slabs to rank 0 in one
 collective; the slab compute here is the CPU oracle (the GPU engine is
 exercised by the -m gpu tests)."""
 from __future__ import annotations
@@ -102,6 +103,46 @@ def test_gloo_gather_cols_matches_single_process(golden, tmp_path, world):
     om = oracle.OracleModel.load(inp)
     g, _ = oracle.grid(s)
     assert np.array_equal(got, om.loglik_grid(g, g, threads=1))
+
+
+def _colslab_worker(rank, world, port, inp, ne, nc, outdir):
+    """The drop-in's split (dist.py, round 6): each rank the c columns
+    [c0, c1) for every e, as [cols][e] -- what gpu_slab_compute leaves in
+    HBM -- gathered in one collective (gather_colslabs)."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, str(ROOT))
+    import oracle
+    from midaspom_amd import dist as md
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    om = oracle.OracleModel.load(inp, 400.0, 0.5, 100.0)
+    ge, _ = oracle.grid(ne)
+    gc, _ = oracle.grid(nc)
+    c0, c1 = md.row_slab(rank, world, nc)
+    slab = om.loglik_grid(ge, gc[c0:c1], threads=1)           # [e][cols]
+    local = torch.from_numpy(np.ascontiguousarray(slab.T))    # [cols][e]
+    full = md.gather_colslabs(local, rank, world, ne, nc)
+    if rank == 0:
+        assert full.shape == (ne, nc) and full.T.flags.c_contiguous
+        np.save(os.path.join(outdir, "full.npy"), np.ascontiguousarray(full))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_gather_colslabs_matches_single_process(golden, tmp_path, world):
+    """Column slabs (remainder columns on rank 0) gathered in one collective
+    give the single-process grid, as its [ie][ic] view, bit for bit."""
+    import oracle
+    ne, nc = 7, 11
+    inp = str(golden / "config2_64x50.txt")
+    mp.spawn(_colslab_worker, args=(world, _free_port(), inp, ne, nc, str(tmp_path)), nprocs=world, join=True)
+    got = np.load(tmp_path / "full.npy")
+    om = oracle.OracleModel.load(inp)
+    ge, _ = oracle.grid(ne)
+    gc, _ = oracle.grid(nc)
+    assert np.array_equal(got, om.loglik_grid(ge, gc, threads=1))
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
