@@ -205,3 +205,29 @@ print("ok")
     os.chmod(cache, 0o700)
     assert "ok" in run(code, env)
     assert len(list(cache.glob("fwd_*.co"))) == 2
+
+
+def test_integration_option_table():
+    """INTEGRATION.md §4 names only options the default library accepts (the
+    Python mirror, itself checked against the C list above), the scenario
+    options, the environment-read cache / timing variables, the diag-only
+    names (said to be diag-only) and the round-4 names it says were deleted
+    (which the library refuses)."""
+    import re
+    from midaspom_amd import _lib
+    text = (ROOT / "INTEGRATION.md").read_text()
+    sec = text[text.index("## 4. Engine options"):text.index("## 5.")]
+    names = set(re.findall(r"MDP_[A-Z0-9_]+", sec))
+    accepted = set(_lib.ENGINE_OPTION_NAMES) - set(_lib.DIAG_OPTION_NAMES)
+    env_read = {"MDP_JIT_CACHE", "MDP_JIT_NOCACHE", "MDP_SETUP_TIMING"}
+    diag = set(_lib.DIAG_OPTION_NAMES)
+    deleted = {"MDP_FUSED_SBUILD", "MDP_FUSED_BAL", "MDP_FUSED_PH2FLAT", "MDP_FUSED_CMERGE", "MDP_FUSED_DIRECT",
+               "MDP_JIT_EARLYW"}
+    unknown = names - accepted - set(_lib.SCENARIO_OPTION_NAMES) - env_read - diag - deleted - {"MDP_EINVAL"}
+    assert not unknown, f"INTEGRATION.md §4 names options the library does not accept: {sorted(unknown)}"
+    for sentence in re.split(r"(?<=[.;])\s", sec):
+        if any(n in sentence for n in deleted):
+            assert "deleted" in sentence and "refuses" in sentence, sentence
+        if any(n in sentence for n in diag):
+            assert "diag" in sentence, sentence
+    assert "MDP_WIDE_MMA" in names and "k_fwd_mmt" in sec
