@@ -1502,13 +1502,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mma(
 //    for every tile and multiplied the rest through zero slots), and the
 //    gathers' Q-row offsets per (entry, new state) from a host table, so no
 //    descriptor lookup sits between a K entry and its gather.
-//  * Years of more than 256 states (ROWS 512 / 1 024, 32 / 16 points a
-//    block): ONE state buffer in LDS (DB = false, 128 KiB): a wave keeps its
-//    tiles' new states in registers until every wave has read the year's old
-//    ones (a barrier), then stores them in place.  A wave owns up to ROWS /
-//    256 tiles a year (17-64 tiles over 16 waves, longest lists first).
-//    Years of up to 128 / 256 states keep k_fwd_mma's two buffers (DB = true,
-//    64 / 32 points a block, one barrier a year).
+//  * Years of more than 128 states (ROWS 256 / 512 / 1 024, 32 / 32 / 16
+//    points a block): ONE state buffer in LDS (DB = false, 64 / 128 / 128
+//    KiB): a wave keeps its tiles' new states in registers until every wave
+//    has read the year's old ones (a barrier), then stores them in place.  A
+//    wave owns up to ROWS / 256 tiles a year (17-64 tiles over 16 waves,
+//    longest lists first).  Years of up to 128 states keep k_fwd_mma's two
+//    buffers (DB = true, 64 points a block, one barrier a year).
 //  * Years of at most 16 tiles give every tile a wave and the spare waves to
 //    the tiles with the longest lists (a tile's list split into slices of at
 //    least two chunks); slice 1 parks its partial products in the tile's own
@@ -1526,8 +1526,8 @@ constexpr uint32_t mmt_pts(uint32_t rt) { return 16u * rt; }
 // power-table row stride (doubles): rows r and r + 1 on different LDS bank halves
 constexpr uint32_t mmt_ps(uint32_t rt) { return rt % 2 ? 16u * rt : 16u * rt + 16u; }
 // the instantiations (RT point tiles of 16, ROWS state rows, two buffers or
-// one): <4, 128, true> years of up to 128 states, <2, 256, true> 256,
-// <2, 512, false> 512, <1, 1 024, false> 1 024
+// one): <4, 128, true> years of up to 128 states, <2, 256, false> 256,
+// <2, 512, false> 512, <1, 1 024, false> 1 024 (mmt_shape)
 template <int RT, int ROWS, bool DB>
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
     const double *__restrict__ Q, uint32_t ldQ, const uint32_t *__restrict__ np, const uint2 *__restrict__ kt,
@@ -2575,17 +2575,21 @@ struct MmtShape {
     uint32_t rt, rows;
     bool db;
 };
-inline MmtShape mmt_shape(uint32_t npmax)
+// (measured, profiles/r06/wide: years of up to 128 states run 25 % faster on
+// <4, 128, 2buf> than on <2, 256, 1buf>; a 256-state problem 6 % faster on
+// one buffer than on <2, 256, 2buf>)
+inline MmtShape mmt_shape(const mdp_engine *eng)
 {
+    const uint32_t npmax = eng->npmax;
     if (npmax <= 128) return {4u, 128u, true};
-    if (npmax <= 256) return {2u, 256u, true};
+    if (npmax <= 256) return {2u, 256u, false};
     if (npmax <= 512) return {2u, 512u, false};
     return {1u, 1024u, false};
 }
 
 size_t mmt_lds(const mdp_engine *eng)
 {
-    const MmtShape sh = mmt_shape(eng->npmax);
+    const MmtShape sh = mmt_shape(eng);
     return ((sh.db ? 2 : 1) * (size_t)sh.rows * mmt_pts(sh.rt) + 2 * ((size_t)eng->maxA + 1) * mmt_ps(sh.rt)) *
            sizeof(double);
 }
@@ -2593,7 +2597,7 @@ size_t mmt_lds(const mdp_engine *eng)
 const void *mmt_kernel(const mdp_engine *eng)
 {
     if (eng->mmt_rows == 128) return (const void *)k_fwd_mmt<4, 128, true>;
-    if (eng->mmt_rows == 256) return (const void *)k_fwd_mmt<2, 256, true>;
+    if (eng->mmt_rows == 256) return (const void *)k_fwd_mmt<2, 256, false>;
     if (eng->mmt_rows == 512) return (const void *)k_fwd_mmt<2, 512, false>;
     return (const void *)k_fwd_mmt<1, 1024, false>;
 }
@@ -2613,7 +2617,7 @@ const void *mmt_kernel(const mdp_engine *eng)
 void build_mmt_plan(mdp_engine *eng)
 {
     if (eng->npmax > 1024 || eng->maxA > 24 || eng->tmax < 2) return;
-    const MmtShape shp = mmt_shape(eng->npmax);
+    const MmtShape shp = mmt_shape(eng);
     const uint32_t rows = shp.rows, rt = shp.rt, pts = mmt_pts(rt), ps = mmt_ps(rt);
     const uint32_t tmaxit = rows > 256 ? rows / 256 : 1, cw = 4 * mmt_u(rt), inplace = shp.db ? 2u : 1u;
     const uint32_t none = (uint32_t)eng->ncoef_d;
@@ -3591,7 +3595,7 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
         }
     } else if (eng->mmt) {  // the matrix-core forward: every c in one launch, blocks dealt XCD-aware
         const uint32_t rt = eng->mmt_rt, rows = eng->mmt_rows, npb = (d.ne + mmt_pts(rt) - 1) / mmt_pts(rt);
-        const bool db = mmt_shape(eng->npmax).db;
+        const bool db = mmt_shape(eng).db;
         const uint64_t nb = (uint64_t)npb * d.nc;
         if (nb > 0x7fffffffull) return mdp_set_error(MDP_EUNSUPPORTED, "grid of %llu k_fwd_mmt workgroups", (unsigned long long)nb);
         note_launch(eng, "k_fwd_mmt<%u,%u,%s>", rt, rows, db ? "2buf" : "1buf");
@@ -3600,7 +3604,7 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
                        d.np_d, d.mmt_kt, d.mmt_cidx, d.mmt_ktile, d.mmt_wplan, eng->tmax, eng->prior0, d.e, d.ne, \
                        eng->maxA, out, os.se, os.sc)
         if (rows == 128) MDP_MMT(4, 128, true);
-        else if (rows == 256) MDP_MMT(2, 256, true);
+        else if (rows == 256) MDP_MMT(2, 256, false);
         else if (rows == 512) MDP_MMT(2, 512, false);
         else MDP_MMT(1, 1024, false);
 #undef MDP_MMT

@@ -305,7 +305,7 @@ def launched_forward(model, path):
     if path == "wide-mma5" and npm <= 256:
         return f"k_fwd_mma<{64 if npm <= 64 else 128 if npm <= 128 else 256}>"
     if path in ("default", "wide") and npm <= 1024:
-        return f"k_fwd_mmt<{'4,128,2buf' if npm <= 128 else '2,256,2buf' if npm <= 256 else '2,512,1buf' if npm <= 512 else '1,1024,1buf'}>"
+        return f"k_fwd_mmt<{'4,128,2buf' if npm <= 128 else '2,256,1buf' if npm <= 256 else '2,512,1buf' if npm <= 512 else '1,1024,1buf'}>"
     return "k_fwd_wide"
 
 
