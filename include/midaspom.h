@@ -135,10 +135,10 @@ void mdp_engine_destroy(mdp_engine *engine);
 /* out[ie*nc + ic] = log L(e[ie], c[ic]) (-inf where L == 0), host memory.
  * Rows are split over the engine's devices in contiguous slabs (remainder to
  * device 0, as main_MIDASPOM_MPI.c:361-368).  Replaces main_MIDASPOM.c:341-395
- * (and the MPI gather :482-506).  Every c must be >= 0 (MDP_EINVAL otherwise,
- * here and in mdp_engine_set_grid): the reference's pC = min(1, c S)
- * (:350-358) is a probability only there, and the kernels' item factors
- * |n - pC| assume it. */
+ * (and the MPI gather :482-506).  Every c must be finite and >= 0
+ * (MDP_EINVAL otherwise, here and in mdp_engine_set_grid): the reference's
+ * pC = min(1, c S) (:350-358) is a probability only there, and the kernels'
+ * item factors |n - pC| and minNum clamps assume it. */
 int mdp_loglik_grid(mdp_engine *engine, const double *e, uint32_t ne, const double *c,
                     uint32_t nc, double *out);
 

@@ -440,7 +440,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
         for (uint32_t i = 0; i < NB; ++i) {
             const uint32_t b = q * NB + i;
             const double x = sv[(size_t)r * nvar + (EXACT ? b : min(b, nvar - 1))];
-            L.sb[i] = (EXACT || b < nvar) ? x : -1.0;
+            L.sb[i] = (EXACT || b < nvar) ? x : HUGE_VAL;  // padded slot: pressure 1.0
         }
     };
     auto rowwork = [&](uint32_t w, const RowLd &L) {
@@ -500,8 +500,7 @@ __global__ __launch_bounds__(kQrowsBlock) void k_qrows(
             double pr[NB];
 #pragma unroll
             for (uint32_t j = 0; j < NB; ++j) {
-                const double tt = cv[i] * L.sb[j];
-                pr[j] = L.sb[j] < 0.0 || tt > 1.0 ? 1.0 : tt;
+                pr[j] = fmin(cv[i] * L.sb[j], 1.0);  // (+inf marks: 1.0, at c = 0 too -- minNum drops NaN)
             }
             double2 *pd = (double2 *)(Prl + (size_t)r * PRS + i * NV + q * NB);
 #pragma unroll
@@ -1192,10 +1191,8 @@ __global__ __launch_bounds__(kBlock) void k_witems(const double *__restrict__ cv
     double f[NV];
 #pragma unroll
     for (int b = 0; b < NV; ++b) {
-        const double sb = (uint32_t)b < nvar ? sv[(size_t)r * nvar + b] : -1.0;
-        double pcv = c * sb;
-        pcv = pcv > 1.0 ? 1.0 : pcv;
-        const double p = sb < 0.0 ? 1.0 : pcv;
+        const double sb = (uint32_t)b < nvar ? sv[(size_t)r * nvar + b] : HUGE_VAL;
+        const double p = fmin(c * sb, 1.0);  // (k_qrows' form: +inf marks give 1.0)
         const uint32_t nbit = (uint32_t)b < nvar ? (nB >> (nvar - 1 - (uint32_t)b)) & 1u : 0u;
         f[b] = (double)nbit - p;  // |n - p|: k_qrows' fold
     }
@@ -2906,10 +2903,10 @@ int upload_qrows_tables(const mdp_engine *eng, DevCtx &d, double cmax)
     const size_t kimg = pl.zpad ? std::max<size_t>(kmax, std::max<uint32_t>(8u, pl.kzmax)) : kmax;
     const size_t ct = ((size_t)pl.off_zs + kimg * nj + 127) & ~(size_t)127;
     std::vector<double> img(ct, 0.0);
-    for (uint32_t js = 0; js < nj; ++js)  // (the columns of j marked -1: pressure 1.0)
+    for (uint32_t js = 0; js < nj; ++js)  // (the columns of j marked +inf: pressure fmin(c inf, 1) = 1.0)
         for (uint32_t b = 0; b < eng->nvar; ++b)
             img[(size_t)js * eng->nvar + b] = ((eng->cj_bits[js] >> (eng->nvar - 1 - b)) & 1u)
-                                                   ? -1.0
+                                                   ? HUGE_VAL
                                                    : eng->Sj[(size_t)js * n + eng->var_cols[b]];
     uint2 *it = (uint2 *)(img.data() + pl.off_it);
     for (uint32_t i = 0; i < eng->nitems; ++i) {
@@ -3201,7 +3198,7 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
         for (uint32_t js = 0; js < eng->nj; ++js)
             for (uint32_t b = 0; b < eng->nvar; ++b)
                 sv[(size_t)js * eng->nvar + b] = ((eng->cj_bits[js] >> (eng->nvar - 1 - b)) & 1u)
-                                                      ? -1.0  // column of j: k_qrows sets pC = 1.0
+                                                      ? HUGE_VAL  // column of j: pC = fmin(c inf, 1) = 1.0
                                                       : eng->Sj[(size_t)js * eng->n + eng->var_cols[b]];
         std::vector<uint2> items(eng->nitems + 1, make_uint2(0u, 0u));
         for (uint32_t i = 0; i < eng->nitems; ++i) {
@@ -3315,9 +3312,11 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
     // phase 2, k_witems, the fused prologue), which equals the reference's
     // (1 - piold)(1 - pC) + piold pC (main_MIDASPOM.c:40) only for pC >= 0;
     // at c < 0 the reference's pC = min(1, c S) is negative, not a probability
+    // (and a NaN or infinite c: the pressures min(1, c S) are then clamped
+    // by minNum, which drops NaN, where the reference would carry it)
     for (uint32_t i = 0; i < nc; ++i)
-        if (c[i] < 0.0)
-            return mdp_set_error(MDP_EINVAL, "colonisation rate c[%u] = %g < 0 (the engine takes c >= 0)", i, c[i]);
+        if (!(c[i] >= 0.0) || std::isinf(c[i]))
+            return mdp_set_error(MDP_EINVAL, "colonisation rate c[%u] = %g (the engine takes finite c >= 0)", i, c[i]);
     HIP_TRY(hipSetDevice(d.device));
     int rc;
     if ((rc = dev_reserve(&d.e, &d.cap_e, ne)) || (rc = dev_reserve(&d.c, &d.cap_c, nc))) return rc;

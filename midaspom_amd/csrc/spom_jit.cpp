@@ -608,8 +608,12 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "        const uint2 t = Itl[it];\n"
              "        const u32 r = (t.x >> 24) | ((t.y >> 24) << 8), B = t.x & 0xffffffu, j = t.y & 0xffffffu;\n"
              // f_b = j_b ? 1 : B_b ? p_b : 1 - p_b with p_b = min(1, c S): one
-             // select for the clamp and j (the image marks j's columns -1; j <= B,
-             // so B_b is set there), then |n_b - p_b| with n_b = 1.0 where B_b
+             // v_min_f64 for the clamp and j (round 6: the image marks j's
+             // columns +inf, so c S is +inf -- or NaN at c = 0, which minNum
+             // drops -- and p_b = 1.0; j <= B, so B_b is set there; the
+             // compare-and-select form cost 4 more instructions a factor,
+             // config 2 8.49 -> 8.32 us, profiles/r06/cfg2), then |n_b - p_b|
+             // with n_b = 1.0 where B_b
              // is clear -- the same bits as fma(s, p, n), (s, n) = (1, 0) or
              // (-1, 1) (1 - p rounded once, |0 - p| = p), with the abs moved to
              // the product (k_qrows uses the same fold)
@@ -619,8 +623,7 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              "#pragma unroll\n"
              "        for (int b = 0; b < NVAR; ++b) {\n"
              "            const u32 bit = NVAR - 1 - b;\n"
-             "            const double sv = Svl[r * NVAR + b], pcv = c * sv;\n"
-             "            const double p = (pcv > 1.0) | (sv < 0.0) ? 1.0 : pcv;\n"
+             "            const double p = fmin(c * Svl[r * NVAR + b], 1.0);\n"
              "            f[b] = (double)((nB >> bit) & 1u) - p;\n"
              "        }\n"
              "#pragma unroll\n"

@@ -247,10 +247,13 @@ def test_negative_c_refused(golden):
     model = mdp.Model.load(golden / "occupancies.txt")
     g, _ = mdp.grid(5)
     with mdp.Engine(model) as eng:
-        with pytest.raises(_lib.MidaspomError, match=r"c\[1\] = -0.25 < 0"):
+        with pytest.raises(_lib.MidaspomError, match=r"c\[1\] = -0.25 \(the engine takes finite c >= 0\)"):
             eng.loglik_grid(g, np.array([0.0, -0.25, 0.5]))
         with pytest.raises(_lib.MidaspomError):
             eng.set_grid(g, -g[1:])
+        for bad in (np.nan, np.inf):
+            with pytest.raises(_lib.MidaspomError):
+                eng.loglik_grid(g, np.array([0.5, bad]))
         assert np.isfinite(eng.loglik_grid(g, g)[1:-1, 1:]).all()  # the engine stays usable (e = 0, 1: -inf)
 
 
