@@ -1,8 +1,16 @@
 /* Floor of a HIP command-line program: load the runtime, count the devices
- * (HIP start-up), optionally touch device 0 (context), then exit normally or
- * by _exit (no runtime teardown).  Usage: hipinit_probe [ctx] [fast] */
+ * (HIP start-up), optionally touch device 0 (context), optionally sleep
+ * (sleep=<ms>: is the exit's cost a background task started with the
+ * runtime, which a longer-lived process hides?), then exit normally or by
+ * _exit (no runtime teardown).  Prints main's entry / return on
+ * CLOCK_MONOTONIC so the parent can time the exit.
+ * thread: create and join one host thread before the exit (the drop-in CLI's
+ * writer uses threads on grids of 256^2 cells and more, where its exit is fast).
+ * Usage: hipinit_probe [ctx] [fast] [sleep=<ms>] [thread] */
 #include <hip/hip_runtime_api.h>
+#include <pthread.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <time.h>
 #include <unistd.h>
@@ -14,12 +22,16 @@ static double now_s(void)
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
+static void *noop(void *p) { return p; }
+
 int main(int argc, char **argv)
 {
-    int ctx = 0, fast = 0;
+    int ctx = 0, fast = 0, sleep_ms = 0, thread = 0;
     for (int i = 1; i < argc; i++) {
         if (!strcmp(argv[i], "ctx")) ctx = 1;
         if (!strcmp(argv[i], "fast")) fast = 1;
+        if (!strncmp(argv[i], "sleep=", 6)) sleep_ms = atoi(argv[i] + 6);
+        if (!strcmp(argv[i], "thread")) thread = 1;
     }
     const double t0 = now_s();
     int n = 0;
@@ -34,7 +46,14 @@ int main(int argc, char **argv)
         hipFree(p);
     }
     const double t2 = now_s();
+    if (sleep_ms > 0) usleep((useconds_t)sleep_ms * 1000u);
+    if (thread) {
+        pthread_t th;
+        if (pthread_create(&th, NULL, noop, NULL) == 0) pthread_join(th, NULL);
+    }
     fprintf(stderr, "hipinit_probe: devices %d count %.3f ctx %.3f\n", n, t1 - t0, t2 - t1);
+    fprintf(stderr, "hipinit_probe clock: main_entry %.6f main_return %.6f\n", t0, now_s());
+    fflush(stderr);
     if (fast) _exit(0);
     return 0;
 }
