@@ -11,18 +11,68 @@
  *   - a tool that writes its results at exit is attached: rocprofv3 /
  *     rocprofiler-sdk (ROCP_TOOL_LIBRARIES, set by rocprofv3) or gcov
  *     (GCOV_PREFIX / GCOV_PREFIX_STRIP).
+ *
+ * Before the _exit the host's cores are woken (round 6): on the GPU pool's
+ * boxes a process that holds a HIP context takes 40-70 ms to be reaped after
+ * _exit -- the same for a bare device-count program, with or without a
+ * context touch, after 0-400 ms of sleep -- unless several host cores were
+ * busy just before it exits: 16 threads spinning 2 ms and joined cut it to
+ * 1 ms, 2 threads or one idle thread do not (scripts/exit_probe.py,
+ * profiles/r06/analysis/exit_probe_*.jsonl).  The CLI's own writer and
+ * normaliser run threads on grids of 256^2 cells and more, which is why its
+ * exit was fast there and slow below (round 5's open question).  The cause
+ * is in the kernel's exit path, not in this code; the warm-up costs ~2 ms of
+ * wall.  MIDASPOM_EXIT_WARM=<threads>[,<microseconds>] changes it (0: off).
  */
 #ifndef MIDASPOM_CLI_EXIT_H
 #define MIDASPOM_CLI_EXIT_H
 
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
 #include <unistd.h>
 
 static inline int mdp_cli_env_set(const char *name)
 {
     const char *v = getenv(name);
     return v && *v;
+}
+
+static inline double mdp_cli_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void *mdp_cli_spin(void *p)
+{
+    const double until = mdp_cli_now() + *(const double *)p;
+    volatile unsigned long n = 0;
+    while (mdp_cli_now() < until) ++n;
+    return NULL;
+}
+
+/* wake `threads` host cores for `us` microseconds each (joined) */
+static inline void mdp_cli_warm_cores(void)
+{
+    int threads = 16, us = 2000;
+    const char *w = getenv("MIDASPOM_EXIT_WARM");
+    if (w && *w) {
+        threads = atoi(w);
+        const char *c = w;
+        while (*c && *c != ',') ++c;
+        if (*c == ',') us = atoi(c + 1);
+    }
+    if (threads <= 0 || us <= 0) return;
+    if (threads > 64) threads = 64;
+    const double secs = 1e-6 * (double)us;
+    pthread_t th[64];
+    int ok[64] = {0};
+    for (int i = 0; i < threads; i++) ok[i] = pthread_create(&th[i], NULL, mdp_cli_spin, (void *)&secs) == 0;
+    for (int i = 0; i < threads; i++)
+        if (ok[i]) pthread_join(th[i], NULL);
 }
 
 /* leave now with `code` (fast path), or return so main can return it */
@@ -34,6 +84,7 @@ static inline void mdp_cli_leave(int code)
         return;
     fflush(stdout);
     fflush(stderr);
+    mdp_cli_warm_cores();
     _exit(code);
 }
 

@@ -1,9 +1,10 @@
-"""Is the drop-in CLI's exit remainder on small grids a background task of
-the HIP runtime / driver that a longer-lived process hides?  Times, from the
-parent on CLOCK_MONOTONIC, the wall after main returns for
+"""Where the drop-in CLI's exit remainder on small grids goes (cli_exit.h).
+Times, from the parent on CLOCK_MONOTONIC, the wall after main returns for
 scripts/ubench/hipinit_probe (device count + a 1 MiB context touch, then
-_exit) with 0-400 ms of sleep before the exit, and the CLI on config 1
-(s = 50) and s = 512 -- 5 runs each, interleaved.  One JSON line per case."""
+_exit; variants: sleep before the exit, one thread, pools of busy threads)
+and for the CLI on config 1 at s = 50 and 512 with and without its
+pre-exit core warm-up (MIDASPOM_EXIT_WARM) -- 5 runs each, interleaved.  One
+JSON line per case (rounds 5-6: profiles/r06/analysis/exit_probe_*.jsonl)."""
 import json
 import os
 import subprocess
@@ -30,9 +31,9 @@ def stamps(err, key):
     return None
 
 
-def run(cmd, key):
+def run(cmd, key, extra=None):
     t0 = time.monotonic()
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True)
+    r = subprocess.run(cmd, env=dict(env, **(extra or {})), capture_output=True, text=True)
     t1 = time.monotonic()
     assert r.returncode == 0, r.stderr[-500:]
     st = stamps(r.stderr, key)
@@ -40,18 +41,19 @@ def run(cmd, key):
             "main": round(st["main_return"] - st["main_entry"], 4), "after_main": round(t1 - st["main_return"], 4)}
 
 
-cases = {f"probe_sleep{ms}": ([str(PROBE), "ctx", "fast", f"sleep={ms}"], "hipinit_probe clock:") for ms in (0, 200)}
-cases["probe_thread"] = ([str(PROBE), "ctx", "fast", "thread"], "hipinit_probe clock:")
-cases["probe_thread_full_exit"] = ([str(PROBE), "ctx", "thread"], "hipinit_probe clock:")
-cases["probe_full_exit"] = ([str(PROBE), "ctx"], "hipinit_probe clock:")
-for s in (50, 200, 256, 512):
-    cases[f"cli_s{s}"] = ([str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", str(s), "-i", str(inp), "-o",
-                          str(tmp / "p.txt")], "midaspom clock (s):")
-run(*cases["cli_s50"])  # fill the code-object cache
+cases = {f"probe_sleep{ms}": ([str(PROBE), "ctx", "fast", f"sleep={ms}"], "hipinit_probe clock:", None) for ms in (0,)}
+cases["probe_pool16"] = ([str(PROBE), "ctx", "fast", "pool=16"], "hipinit_probe clock:", None)
+cli = lambda s: [str(_lib.CLI_PATH), "-m", "400", "-d", "100", "-s", str(s), "-i", str(inp), "-o", str(tmp / "p.txt")]
+for s in (50, 512):
+    cases[f"cli_s{s}"] = (cli(s), "midaspom clock (s):", None)  # default: 16 cores warmed 2 ms before _exit
+    cases[f"cli_s{s}_nowarm"] = (cli(s), "midaspom clock (s):", {"MIDASPOM_EXIT_WARM": "0"})
+for w in ("16,500", "8,2000", "4,2000"):
+    cases[f"cli_s50_warm{w}"] = (cli(50), "midaspom clock (s):", {"MIDASPOM_EXIT_WARM": w})
+run(*cases["cli_s50"][:2])  # fill the code-object cache
 res = {k: [] for k in cases}
 for _ in range(5):
-    for k, (cmd, key) in cases.items():
-        res[k].append(run(cmd, key))
+    for k, (cmd, key, extra) in cases.items():
+        res[k].append(run(cmd, key, extra))
 for k, v in res.items():
     med = {f: sorted(x[f] for x in v)[len(v) // 2] for f in v[0]}
     print(json.dumps({"case": k, "median": med, "runs": v}), flush=True)
