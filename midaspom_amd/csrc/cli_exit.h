@@ -17,12 +17,15 @@
  * _exit -- the same for a bare device-count program, with or without a
  * context touch, after 0-400 ms of sleep -- unless several host cores were
  * busy just before it exits: 16 threads spinning 2 ms and joined cut it to
- * 1 ms, 2 threads or one idle thread do not (scripts/exit_probe.py,
+ * 1 ms, 2 threads or one idle thread do not; in the CLI on config 1 (s = 50)
+ * 16 x 0.5 ms, 8 x 2 ms and 4 x 2 ms all take the remainder from 74 ms to
+ * 2-4 ms, counting the spin (scripts/exit_probe.py,
  * profiles/r06/analysis/exit_probe_*.jsonl).  The CLI's own writer and
  * normaliser run threads on grids of 256^2 cells and more, which is why its
- * exit was fast there and slow below (round 5's open question).  The cause
- * is in the kernel's exit path, not in this code; the warm-up costs ~2 ms of
- * wall.  MIDASPOM_EXIT_WARM=<threads>[,<microseconds>] changes it (0: off).
+ * exit was fast there and slow below (round 5's open question: s = 255 pays
+ * 69 ms, s = 256 1 ms).  The cause is in the kernel's exit path, not in this
+ * code.  MIDASPOM_EXIT_WARM=<threads>[,<microseconds>] changes the default
+ * 16 x 500 us (0: off).
  */
 #ifndef MIDASPOM_CLI_EXIT_H
 #define MIDASPOM_CLI_EXIT_H
@@ -57,7 +60,7 @@ static void *mdp_cli_spin(void *p)
 /* wake `threads` host cores for `us` microseconds each (joined) */
 static inline void mdp_cli_warm_cores(void)
 {
-    int threads = 16, us = 2000;
+    int threads = 16, us = 500;
     const char *w = getenv("MIDASPOM_EXIT_WARM");
     if (w && *w) {
         threads = atoi(w);
