@@ -2749,6 +2749,7 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
             eng->mma_dbase.assign(eng->tmax + 1, 0u);
             eng->mma_ktmax = 16;
             size_t ub = 0;
+            bool pad_overflow = false;
             for (uint32_t t = 1; t < eng->tmax; ++t) {
                 const uint32_t npp = eng->np[t - 1], npc = eng->np[t], npcp = (npc + 15) / 16 * 16;
                 uint32_t ld = 16;
@@ -2761,6 +2762,10 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
                         eng->mma_kt.push_back(make_uint2((k * pts * 8u) | (((a - m) * ps * 8u) << 16),
                                                          (m * ps * 8u) | (m << 16) | (k * kMmaDummy)));
                 }
+                // padding names descriptor row npp through the 8-bit k field:
+                // row 256 would wrap to row 0 (the advisor's round-5 finding),
+                // so a 256-state year that needs padding leaves k_fwd_mma
+                if (eng->mma_kt.size() % (4 * kMmaU) && npp > 255) pad_overflow = true;
                 while (eng->mma_kt.size() % (4 * kMmaU)) eng->mma_kt.push_back(make_uint2(0u, npp * kMmaDummy));
                 eng->mma_ktmax = std::max<uint32_t>(eng->mma_ktmax, (uint32_t)eng->mma_kt.size() - eng->mma_kbase[t]);
                 for (uint32_t k = 0; k <= npp; ++k)
@@ -2798,7 +2803,7 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
             for (uint32_t i = 0; i < 4 * kMmaU; ++i) eng->mma_kt.push_back(make_uint2(0u, 0u));
             if (eng->mma_desc.empty()) eng->mma_desc.push_back(none);
             const size_t lmax = device_lds_max();
-            eng->mma = mma_lds(eng) <= lmax && none <= kOffMask;
+            eng->mma = mma_lds(eng) <= lmax && none <= kOffMask && !pad_overflow;
         }
     }
     return MDP_OK;
