@@ -800,7 +800,8 @@ def main():
     # or the reference's [e][c] rows; the slab is s x s either way
     eng.set_layout(args.layout)
     out = torch.empty((s, s), dtype=torch.float64, device=dev)
-    gathered = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # the gather's targets on rank 0 (host tensors under a rehearsal backend)
+    gathered = [_coll_tensor(torch.empty_like(out), args) for _ in range(world)] if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     # A step = one pass of the hot path over this rank's slab (no exchange:
@@ -812,8 +813,7 @@ def main():
 
     def gather():
         if world > 1:
-            src = _coll_tensor(out, args)
-            dist.gather(src, [_coll_tensor(g, args) for g in gathered] if gathered else None, dst=0)
+            dist.gather(_coll_tensor(out, args), gathered, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -831,6 +831,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    weak_same = None
+    if world > 1 and rank == 0:
+        # the gathered (N s) x s grid against the same grid computed by this
+        # one rank alone: the same bits (each point's arithmetic is its own)
+        one_eng = mdp.Engine(model, devices=[dev.index])
+        one_eng.set_grid(g_all, g_c)
+        one_eng.set_layout(args.layout)
+        one = torch.empty((s, world * s) if args.layout == "ce" else (world * s, s), dtype=torch.float64, device=dev)
+        one_eng.run(one.data_ptr(), one.shape[1], stream)
+        torch.cuda.synchronize(dev)
+        one_eng.close()
+        parts = [x.cpu().numpy() for x in gathered]
+        full = np.concatenate(parts, axis=1 if args.layout == "ce" else 0)
+        weak_same = bool(np.array_equal(full, one.cpu().numpy(), equal_nan=True))
     job_ms = time_job(step, gather, dev, world)
     strong = None
     if world > 1 and not args.no_strong:
@@ -911,6 +925,7 @@ def main():
         "job": {"ms": job_ms, "value": world * s * s * (tmax - 1) / (job_ms * 1e-3),
                 "what": "one pass + one gather to rank 0" if world > 1 else "one pass"},
         **({"strong": strong} if strong else {}),
+        **({"gathered_equals_one_rank": weak_same} if world > 1 else {}),
         "kernel_ms": kms,
         "roofline": {
             "kernel": "k_forward",
