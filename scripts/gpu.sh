@@ -56,7 +56,7 @@ rehearse)
 prof)
   for CFG in ${3:-2 3}; do
     case $CFG in 4) A="--steps 3 --warmup 1";; 3|6) A="--steps 20 --warmup 3";; *) A="--steps 50 --warmup 5";; esac
-    PROF $O/prof_cfg$CFG "" 400 -- python3 $R/bench.py --config $CFG $A --no-cpu-baseline > $O/bench_cfg$CFG.json 2> $O/bench_cfg$CFG.err || { echo "prof cfg$CFG failed"; tail $O/bench_cfg$CFG.err; exit 1; }
+    PROF $O/prof_cfg$CFG "" 400 -- python3 $R/bench.py --config $CFG $A --no-cpu-baseline --no-projection > $O/bench_cfg$CFG.json 2> $O/bench_cfg$CFG.err || { echo "prof cfg$CFG failed"; tail $O/bench_cfg$CFG.err; exit 1; }
     echo "prof cfg$CFG ok"
   done ;;
 pmc)
@@ -65,7 +65,7 @@ pmc)
              "SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_SMEM" \
              "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
-    PROF $O/c${CFG}p$i "$set" 150 -- python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 3 --warmup 1 > $O/c${CFG}p$i.json 2> $O/c${CFG}p$i.err || { echo "pmc pass $i failed"; tail $O/c${CFG}p$i.err; exit 1; }
+    PROF $O/c${CFG}p$i "$set" 150 -- python3 $R/bench.py --config $CFG --no-cpu-baseline --no-projection --steps 3 --warmup 1 > $O/c${CFG}p$i.json 2> $O/c${CFG}p$i.err || { echo "pmc pass $i failed"; tail $O/c${CFG}p$i.err; exit 1; }
   done
   python3 scripts/pmc_summary.py $O/c${CFG}p1 $O/c${CFG}p2 > $O/pmc_summary_cfg$CFG.txt || exit 1
   mkdir -p $O/t && cp -r $O/c${CFG}p3 $O/t/c${CFG}p7 && cp -r $O/c${CFG}p4 $O/t/c${CFG}p8
@@ -76,7 +76,7 @@ traffic)
     KN=""; [ $CFG = 4 ] && KN="k_scn<"; [ $CFG = 5 ] && KN="k_future<"
     for p in 7:FETCH_SIZE 8:WRITE_SIZE; do
       i=${p%%:*}; C=${p#*:}
-      PROF $O/c${CFG}p$i "$C" 200 -- python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 2 --warmup 1 > $O/c${CFG}p$i.json 2> $O/c${CFG}p$i.err || { echo "pmc $CFG $C failed"; tail $O/c${CFG}p$i.err; exit 1; }
+      PROF $O/c${CFG}p$i "$C" 200 -- python3 $R/bench.py --config $CFG --no-cpu-baseline --no-projection --steps 2 --warmup 1 > $O/c${CFG}p$i.json 2> $O/c${CFG}p$i.err || { echo "pmc $CFG $C failed"; tail $O/c${CFG}p$i.err; exit 1; }
     done
     python3 scripts/pmc_traffic.py $O $CFG $O/pmc_traffic_cfg$CFG.json $KN || exit 1
   done ;;
