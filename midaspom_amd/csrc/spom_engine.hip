@@ -43,6 +43,7 @@
 #include <set>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "mdp_internal.h"
@@ -1173,7 +1174,8 @@ __global__ __launch_bounds__(kBlock) void k_forward_lds(
 // out [state][point] so every lane's access is coalesced.
 // ---------------------------------------------------------------------------
 
-// Pg[cl][it] = Pc[j][B] of item `it` at c = cvals[c0 + cl]: Z_row(c) times the
+// Pg[cl * ldp + it] = Pc[j][B] of item `it` at c = cvals[c0 + cl] (ldp: nitems,
+// or nitems + 1 for k_fwd_hs, whose rows end in a zero slot): Z_row(c) times the
 // var-column factors f_b = B_b ? pC_b : 1 - pC_b, pC_b = min(1, c S[j][b])
 // (1.0 for the columns of j, marked -1 in sv), combined in k_qrows' pairwise
 // tree over NV slots -- the same bits k_qrows produces.
@@ -1181,7 +1183,8 @@ template <int NV>
 __global__ __launch_bounds__(kBlock) void k_witems(const double *__restrict__ cvals, uint32_t nc, uint32_t c0,
                                                    uint32_t nvar, const double *__restrict__ Zg,
                                                    const double *__restrict__ sv, uint32_t nitems,
-                                                   const uint2 *__restrict__ items, double *__restrict__ Pg)
+                                                   const uint2 *__restrict__ items, double *__restrict__ Pg,
+                                                   uint32_t ldp)
 {
     const uint32_t it = blockIdx.x * kBlock + threadIdx.x, cl = blockIdx.y;
     if (it >= nitems) return;
@@ -1202,7 +1205,7 @@ __global__ __launch_bounds__(kBlock) void k_witems(const double *__restrict__ cv
     for (int sh = 2; sh < NV; sh *= 2)
 #pragma unroll
         for (int b = 0; b + sh < NV; b += 2 * sh) f[b] *= f[b + sh];
-    Pg[(size_t)cl * nitems + it] = Zg[(size_t)r * nc + c0 + cl] * f[0];
+    Pg[(size_t)cl * ldp + it] = Zg[(size_t)r * nc + c0 + cl] * f[0];
 }
 
 // Q[c0 + cl][q] = the q-th entry's items summed in CSR (ascending j) order,
@@ -1755,6 +1758,242 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
     }
 }
 
+// k_fwd_hs<RT, NB> (round 6): the wide forward through the hidden states.
+// The reference's own factorisation (main_MIDASPOM.c:18-50, :363, :371-384):
+// P = Pe Pc over the hidden states j, so year t is
+//     U[p][j] = sum_{k: A_k >= j} v[p][k] x^(|A_k| - |j|) y^|j|     (v Pe)
+//     n[p][l] = sum_{j <= B_l} Pc[j][B_l] U[p][j]                  (U Pc)
+// instead of one (nX+1)-term polynomial per transition (k, l): for a year of
+// 2^f completions of f unvisited patches that is ~3^f (j, l) terms per
+// point, not ~2^f 2^f (|A|+1) -- 10-25x fewer for years of 256-1 024 states.
+// The block's points keep one vector over the whole 2^NB cube of hidden
+// states in LDS, V[j][p] (NB = nvar <= 10; 2^NB x 16 RT doubles = 128 KiB):
+//  * v Pe: Pe is a tensor product over the patches (per patch: occupied ->
+//    extinct w.p. x, survives w.p. y), applied in place as one butterfly pass
+//    per patch of W = the bits occupied in some state of year t - 1: first
+//    the patches unobserved that year (F; every pair of positions is a
+//    state), then the always-occupied ones (O), each writing its "extinct"
+//    half by assignment (those positions held no state: no zeroing needed).
+//    Position lists per pass come from the host (pass tables);
+//  * U Pc: the per-year GEMM on the matrix cores as k_fwd_mmt's, with K = the
+//    hidden states j a column tile of new states can reach (subsets of the
+//    tile's union within W), the W operand U[j][p] read straight from the
+//    cube, and the C operand Pc[j][B_l] gathered from the column's item
+//    factors (k_witems' Pg rows, ld = nitems + 1: a zero slot at nitems for
+//    j not <= B_l) through a host table of offsets;
+//  * the year's new states are stored at their own cube positions B_l (after
+//    a barrier: U is dead by then), ready for the next year's butterflies.
+// Tiles per wave as k_fwd_mmt (longest lists first past 16 tiles; smaller
+// years give a tile up to two waves, slice 1 parked in the tile's own
+// destination rows).  Q3 semantics: ones at year 0's states; L = prior0 x
+// the sum over the last year's states.  Sums reordered against the
+// reference's (positive terms for e in [0, 1]: ~1e-15 relative).
+template <int RT, int NB>
+__global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
+    const double *__restrict__ Pg, uint32_t ldp, uint32_t c0, const uint32_t *__restrict__ np,
+    const uint32_t *__restrict__ kt, const uint32_t *__restrict__ cidx, const uint2 *__restrict__ ktile,
+    const uint2 *__restrict__ wplan, const uint4 *__restrict__ pass, const uint32_t *__restrict__ pbase,
+    const uint32_t *__restrict__ ppos, const uint32_t *__restrict__ dpos, const uint32_t *__restrict__ dbase,
+    const uint32_t *__restrict__ pk, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
+    double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
+{
+    constexpr uint32_t PTS = mmt_pts(RT), NC = 1u << NB, TMAX = NC > 256 ? NC / 256 : 1, U = mmt_u(RT);
+    static_assert(TMAX * RT <= 4 && NC * PTS <= 16384, "cube and tiles");
+    extern __shared__ __attribute__((aligned(16))) double mlds[];
+    double *V = mlds;  // [j][point]
+    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-aware: XCD x takes a contiguous range of logical blocks (whole columns)
+    const uint32_t npb = (ne + PTS - 1) / PTS, full = gridDim.x & ~7u, b = blockIdx.x;
+    const uint32_t lb = b < full ? (b & 7u) * (full >> 3) + (b >> 3) : b;
+    const uint32_t p0 = (lb % npb) * PTS, cl = lb / npb, ic = c0 + cl;
+    // this thread's point in the pass loops (1 024 is a multiple of PTS)
+    const uint32_t pp = threadIdx.x % PTS;
+    double xq, yq;
+    {
+        const uint32_t ie = p0 + pp;
+        const double e = ie < ne ? evals[ie] : 0.0;
+        xq = e > 1.0 ? 1.0 : e;
+        yq = 1.0 - xq;
+    }
+    // the cube starts at zero (a position no year has written holds a finite
+    // value whenever it is read: padded K entries meet it with C = 0), then
+    // ones at year 0's states (Q3)
+    for (uint32_t i = threadIdx.x; i < NC * PTS; i += kMmaThreads) V[i] = 0.0;
+    __syncthreads();
+    {
+        const uint32_t n0 = (np[0] + 15) / 16 * 16, d0 = dbase[0];
+        for (uint32_t i = threadIdx.x; i < n0 * PTS; i += kMmaThreads) {
+            const uint32_t pos = dpos[d0 + i / PTS];
+            if (pos != ~0u) V[pos * PTS + i % PTS] = 1.0;
+        }
+    }
+    __syncthreads();
+    const double *q = Pg + (size_t)cl * ldp;
+    const uint32_t kk = lane >> 4, col = lane & 15u;
+    struct Item {
+        uint32_t tile, ks, S, pbase, cb, ce, nch;
+        bool active, split;
+        const uint32_t *kl, *cl;
+    };
+    auto plan = [&](uint32_t t, uint32_t i) {
+        Item it;
+        const uint2 wp = wplan[(t * 16 + wv) * TMAX + i];
+        it.cb = wp.x & 0xffffu;
+        it.ce = wp.x >> 16;
+        it.tile = wp.y & 0xffu;
+        it.ks = (wp.y >> 8) & 15u;
+        it.S = (wp.y >> 12) & 31u;
+        it.pbase = (wp.y >> 17) & 31u;
+        it.split = (wp.y >> 22) & 1u;
+        it.active = (wp.y >> 24) != 0u;
+        const uint2 kt2 = ktile[t * kMmtMaxTiles + it.tile];
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(kt2.x);
+        it.kl = kt + k0;
+        it.cl = cidx + (size_t)k0 * 16;
+        it.nch = kt2.y;
+        return it;
+    };
+    // K entry (one per 16 lanes): the LDS byte offset of U's row j; per lane
+    // the byte offset of Pc[j][B_l] in the column's Pg row (or its zero slot)
+    auto kent = [&](const Item &it, uint32_t ch, uint32_t u) {
+        const uint32_t c = ch < it.nch ? ch : it.nch - 1;
+        return it.kl[(c * U + u) * 4 + kk];
+    };
+    auto coff = [&](const Item &it, uint32_t ch, uint32_t u) {
+        const uint32_t c = ch < it.nch ? ch : it.nch - 1;
+        return it.cl[(c * U + u) * 64 + lane];
+    };
+    auto cval = [&](uint32_t o) { return *(const double *)((const char *)q + o); };
+    uint32_t ee[4][U];
+    uint32_t dd[2][U];
+    double bb[2][U];
+    auto prime = [&](const Item &it) {
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            ee[0][u] = kent(it, it.cb, u);
+            ee[1][u] = kent(it, it.cb + 1, u);
+            ee[2][u] = kent(it, it.cb + 2, u);
+            dd[0][u] = coff(it, it.cb, u);
+            dd[1][u] = coff(it, it.cb + 1, u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) bb[0][u] = cval(dd[0][u]);
+    };
+    for (uint32_t t = 1; t < tmax; ++t) {
+        // v Pe: one butterfly pass per patch of W (pass table: bit mask,
+        // pairs, position-list base; a position's bit 31 says its partner
+        // already holds a value to add to)
+        const uint32_t pb0 = pbase[t], pb1 = pbase[t + 1];
+        for (uint32_t ps = pb0; ps < pb1; ++ps) {
+            const uint4 pd = pass[ps];  // (uniform)
+            const uint32_t bit = pd.x, npairs = pd.y, base = pd.z;
+            for (uint32_t i = threadIdx.x / PTS; i < npairs; i += kMmaThreads / PTS) {
+                const uint32_t pe = ppos[base + i], a1 = pe & 0x7fffffffu;
+                double *v1 = V + (size_t)a1 * PTS + pp, *v0 = V + (size_t)(a1 ^ bit) * PTS + pp;
+                const double w = *v1, z = (pe >> 31) ? *v0 : 0.0;
+                *v0 = fma(xq, w, z);
+                *v1 = yq * w;
+            }
+            __syncthreads();
+        }
+        // U Pc on the matrix cores
+        mdp_d4 acc[TMAX][RT];
+        Item cur = plan(t, 0);
+        const Item first = cur;
+#pragma unroll
+        for (uint32_t i = 0; i < TMAX; ++i) {
+#pragma unroll
+            for (uint32_t h = 0; h < RT; ++h) acc[i][h] = mdp_d4{0.0, 0.0, 0.0, 0.0};
+            if (i > 0) cur = plan(t, i);
+            if (!cur.active) break;  // a wave's items are its first ones
+            prime(cur);
+            mdp_d4(&ac)[RT] = acc[i];  // (i is a constant once unrolled)
+            auto chunk = [&](uint32_t ch, auto jc) {
+                constexpr uint32_t j = decltype(jc)::value;
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) ee[(j + 3) & 3][u] = kent(cur, ch + 3, u);
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) bb[(j + 1) & 1][u] = cval(dd[(j + 1) & 1][u]);
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) dd[j & 1][u] = coff(cur, ch + 2, u);
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t joff = ee[j][u];
+#pragma unroll
+                    for (uint32_t h = 0; h < RT; ++h) {
+                        const double av = *(const double *)((const char *)V + joff + (h * 16 + col) * 8u);
+                        ac[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(bb[j & 1][u], av, ac[h], 0, 0, 0);
+                    }
+                }
+            };
+            uint32_t ch = cur.cb;
+            for (; ch + 4 <= cur.ce; ch += 4) {
+                chunk(ch, std::integral_constant<uint32_t, 0>{});
+                chunk(ch + 1, std::integral_constant<uint32_t, 1>{});
+                chunk(ch + 2, std::integral_constant<uint32_t, 2>{});
+                chunk(ch + 3, std::integral_constant<uint32_t, 3>{});
+            }
+            if (ch < cur.ce) chunk(ch, std::integral_constant<uint32_t, 0>{});
+            if (ch + 1 < cur.ce) chunk(ch + 1, std::integral_constant<uint32_t, 1>{});
+            if (ch + 2 < cur.ce) chunk(ch + 2, std::integral_constant<uint32_t, 2>{});
+        }
+        __syncthreads();  // every wave has read U
+        // the lane's accumulators: new states tile * 16 + kk + 4 r (tile
+        // order; dpos: their cube positions, ~0 for padding) of point h * 16 + col
+        const uint32_t db = dbase[t];
+        auto store = [&](uint32_t tile, const mdp_d4 (&a)[RT]) {
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) {
+                const uint32_t pos = dpos[db + tile * 16 + kk + 4 * r];
+                if (pos == ~0u) continue;
+                double *dst = V + (size_t)pos * PTS + col;
+#pragma unroll
+                for (uint32_t h = 0; h < RT; ++h) dst[h * 16] = a[h][r];
+            }
+        };
+        // a sliced tile's slices ks >= 1 park their partials in 16-row
+        // blocks of the cube that hold none of the year's states (host table
+        // pk: U is dead, and the next year's butterflies write such a
+        // position before reading it); slice 0 adds them in slice order
+        if (first.split) {
+            auto park = [&](uint32_t ks) { return V + (size_t)pk[t * 16 + first.pbase + ks - 1] * PTS + lane; };
+            if (first.active && first.ks >= 1) {
+                double *pkp = park(first.ks);
+#pragma unroll
+                for (uint32_t h = 0; h < RT; ++h)
+#pragma unroll
+                    for (uint32_t r = 0; r < 4; ++r) pkp[(h * 4 + r) * 64] = acc[0][h][r];
+            }
+            __syncthreads();
+            if (first.active && first.ks == 0)
+                for (uint32_t j = 1; j < first.S; ++j) {
+                    const double *pj = park(j);
+#pragma unroll
+                    for (uint32_t h = 0; h < RT; ++h)
+#pragma unroll
+                        for (uint32_t r = 0; r < 4; ++r) acc[0][h][r] = acc[0][h][r] + pj[(h * 4 + r) * 64];
+                }
+            __syncthreads();  // parked blocks read before any tile's store
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < TMAX; ++i) {
+            const Item it = i == 0 ? first : plan(t, i);
+            if (!it.active || it.ks != 0) break;
+            store(it.tile, acc[i]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < PTS) {
+        const uint32_t ie = p0 + threadIdx.x, dl = dbase[tmax - 1], npl = (np[tmax - 1] + 15) / 16 * 16;
+        double L = 0.0;
+        for (uint32_t l = 0; l < npl; ++l) {
+            const uint32_t pos = dpos[dl + l];
+            if (pos != ~0u) L += V[pos * PTS + threadIdx.x] * prior0;
+        }
+        if (ie < ne) out[(size_t)ie * ld_out + (size_t)ic * out_cs] = log(L);
+    }
+}
+
 typedef const __attribute__((address_space(4))) uint32_t cuint;
 
 // Forward recursion with the state vectors in HBM: lane per e value, one c
@@ -1936,6 +2175,11 @@ struct DevCtx {
     uint32_t *mma_kbase = nullptr, *mma_desc = nullptr, *mma_dbase = nullptr;
     uint2 *mmt_kt = nullptr, *mmt_ktile = nullptr, *mmt_wplan = nullptr;  // k_fwd_mmt tables
     uint32_t *mmt_cidx = nullptr;
+    // k_fwd_hs tables
+    uint32_t *hs_kt = nullptr, *hs_cidx = nullptr, *hs_pbase = nullptr, *hs_ppos = nullptr, *hs_dpos = nullptr,
+             *hs_dbase = nullptr, *hs_pk = nullptr;
+    uint2 *hs_ktile = nullptr, *hs_wplan = nullptr;
+    uint4 *hs_pass = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
     std::vector<uint8_t> ev_mask;  // per profiled run: slots whose kernel was launched
@@ -2076,6 +2320,17 @@ struct mdp_engine {
     std::vector<uint2> mmt_kt, mmt_ktile, mmt_wplan;
     std::vector<uint32_t> mmt_cidx;
     double mmt_flops_pt = 0;  // executed MFMA flops per grid point (padding included)
+    // k_fwd_hs (round 6, through the hidden states: build_hs_plan): 2^hs_nb
+    // cube positions, RT point tiles; per (year, tile) K lists of hidden
+    // states and their item offsets, per year butterfly passes, the new
+    // states' cube positions in tile order and free 16-row park blocks
+    bool hs = false;
+    uint32_t hs_rt = 0, hs_nb = 0;
+    std::vector<uint32_t> hs_kt, hs_cidx, hs_pbase, hs_ppos, hs_dpos, hs_dbase, hs_pk;
+    std::vector<uint2> hs_ktile, hs_wplan;
+    std::vector<uint4> hs_pass;
+    double hs_flops_pt = 0, hs_mfma_pt = 0;  // FP64 flops per grid point (padding included), of them MFMA
+    std::vector<uint32_t> ystate;  // each year's states (short_state bits), year_off order
     uint32_t qslot_lglmax = 0;      // log2 of the widest lane segment
     std::vector<uint8_t> isvar;
     std::vector<double> Sj;  // [nj][n] colonisation sums of every column for each needed j
@@ -2163,6 +2418,9 @@ int build_plan(mdp_engine *eng, const mdp_problem *p)
         eng->np[t] = p->year_off[t + 1] - p->year_off[t];
         eng->npmax = std::max(eng->npmax, eng->np[t]);
     }
+    eng->ystate.clear();
+    for (uint32_t i = 0; i < p->year_off[p->tmax]; ++i)
+        eng->ystate.push_back(p->year_ids[i] < p->nextid ? p->short_state[p->year_ids[i]] : ~0u);
     std::map<uint64_t, uint32_t> pair_index;
     std::vector<uint32_t> A0, B0, use0;
     for (uint32_t t = 1; t < p->tmax; ++t) {
@@ -2599,6 +2857,60 @@ const void *mmt_kernel(const mdp_engine *eng)
     return (const void *)k_fwd_mmt<1, 1024, false>;
 }
 
+// per (year, wave) work items over a year's column tiles of nch[tile]
+// pipeline chunks each (k_fwd_mmt, k_fwd_hs): more than 16 tiles are dealt
+// longest list first to the least-loaded wave (up to tmaxit each); up to 16
+// give every tile a wave and the spare waves to the tiles whose slices are
+// longest (at least two chunks each; slices past the first `inplace` of a
+// tile park their partials, `room` 16-row blocks at most)
+void plan_waves(const std::vector<uint32_t> &nch, uint32_t tmaxit, uint32_t inplace, uint32_t room, uint2 *wp)
+{
+    const uint32_t ncol = (uint32_t)nch.size();
+    if (ncol <= 16) {
+        // waves per tile: one each, the rest to the tile whose slices
+        // are longest (each slice at least two chunks; the parked
+        // partials -- every slice past the first `inplace` of a tile --
+        // within the buffer's rows past the year's tiles)
+        std::vector<uint32_t> w(ncol, 1);
+        uint32_t parked = 0;
+        for (uint32_t spare = 16 - ncol; spare; --spare) {
+            uint32_t best = ncol;
+            for (uint32_t i = 0; i < ncol; ++i)
+                if (nch[i] / (w[i] + 1) >= 2 && (w[i] + 1 <= inplace || parked < room) &&
+                    (best == ncol || nch[i] * w[best] > nch[best] * w[i]))
+                    best = i;
+            if (best == ncol) break;
+            if (++w[best] > inplace) ++parked;
+        }
+        const uint32_t split = *std::max_element(w.begin(), w.end()) > 1 ? 1u : 0u;
+        for (uint32_t wv = 0; wv < 16; ++wv)
+            for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, split << 22);
+        uint32_t wv = 0, pbase = 0;
+        for (uint32_t tile = 0; tile < ncol; ++tile) {
+            for (uint32_t ks = 0; ks < w[tile]; ++ks, ++wv) {
+                const uint32_t cb = nch[tile] * ks / w[tile], ce = nch[tile] * (ks + 1) / w[tile];
+                wp[wv * tmaxit] = make_uint2(cb | ce << 16, tile | ks << 8 | w[tile] << 12 | pbase << 17 |
+                                                               split << 22 | 1u << 24);
+            }
+            pbase += w[tile] > inplace ? w[tile] - inplace : 0;
+        }
+    } else {
+        std::vector<uint32_t> order(ncol), cnt(16, 0);
+        std::vector<uint64_t> load(16, 0);
+        for (uint32_t i = 0; i < ncol; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return nch[x] > nch[y]; });
+        for (uint32_t wv = 0; wv < 16; ++wv)
+            for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, 0u);
+        for (uint32_t tile : order) {
+            uint32_t best = 16;
+            for (uint32_t wv = 0; wv < 16; ++wv)
+                if (cnt[wv] < tmaxit && (best == 16 || load[wv] < load[best])) best = wv;
+            wp[best * tmaxit + cnt[best]++] = make_uint2(nch[tile] << 16, tile | 1u << 12 | 1u << 24);
+            load[best] += nch[tile];
+        }
+    }
+}
+
 // k_fwd_mmt's tables (c-independent): years of at most 1 024 states.
 //  * per (year, column tile) its K entries: every source k with m = 0 ..
 //    the largest nX over the tile's new states (the rest of m <= |A_k| would
@@ -2659,51 +2971,7 @@ void build_mmt_plan(mdp_engine *eng)
             eng->mmt_ktile[(size_t)t * kMmtMaxTiles + tile] = make_uint2((uint32_t)start, nch[tile]);
             fl += 2.0 * 16.0 * (double)(eng->mmt_kt.size() - start);
         }
-        uint2 *wp = eng->mmt_wplan.data() + (size_t)t * 16 * tmaxit;
-        if (ncol <= 16) {
-            // waves per tile: one each, the rest to the tile whose slices
-            // are longest (each slice at least two chunks; the parked
-            // partials -- every slice past the first `inplace` of a tile --
-            // within the buffer's rows past the year's tiles)
-            std::vector<uint32_t> w(ncol, 1);
-            uint32_t parked = 0;
-            const uint32_t room = (rows - ncol * 16) / 16;
-            for (uint32_t spare = 16 - ncol; spare; --spare) {
-                uint32_t best = ncol;
-                for (uint32_t i = 0; i < ncol; ++i)
-                    if (nch[i] / (w[i] + 1) >= 2 && (w[i] + 1 <= inplace || parked < room) &&
-                        (best == ncol || nch[i] * w[best] > nch[best] * w[i]))
-                        best = i;
-                if (best == ncol) break;
-                if (++w[best] > inplace) ++parked;
-            }
-            const uint32_t split = *std::max_element(w.begin(), w.end()) > 1 ? 1u : 0u;
-            for (uint32_t wv = 0; wv < 16; ++wv)
-                for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, split << 22);
-            uint32_t wv = 0, pbase = 0;
-            for (uint32_t tile = 0; tile < ncol; ++tile) {
-                for (uint32_t ks = 0; ks < w[tile]; ++ks, ++wv) {
-                    const uint32_t cb = nch[tile] * ks / w[tile], ce = nch[tile] * (ks + 1) / w[tile];
-                    wp[wv * tmaxit] = make_uint2(cb | ce << 16, tile | ks << 8 | w[tile] << 12 | pbase << 17 |
-                                                                   split << 22 | 1u << 24);
-                }
-                pbase += w[tile] > inplace ? w[tile] - inplace : 0;
-            }
-        } else {
-            std::vector<uint32_t> order(ncol), cnt(16, 0);
-            std::vector<uint64_t> load(16, 0);
-            for (uint32_t i = 0; i < ncol; ++i) order[i] = i;
-            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return nch[x] > nch[y]; });
-            for (uint32_t wv = 0; wv < 16; ++wv)
-                for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, 0u);
-            for (uint32_t tile : order) {
-                uint32_t best = 16;
-                for (uint32_t wv = 0; wv < 16; ++wv)
-                    if (cnt[wv] < tmaxit && (best == 16 || load[wv] < load[best])) best = wv;
-                wp[best * tmaxit + cnt[best]++] = make_uint2(nch[tile] << 16, tile | 1u << 12 | 1u << 24);
-                load[best] += nch[tile];
-            }
-        }
+        plan_waves(nch, tmaxit, inplace, (rows - ncol * 16) / 16, eng->mmt_wplan.data() + (size_t)t * 16 * tmaxit);
         ub += (size_t)npp * npc;
     }
     eng->mmt_flops_pt = fl + 2.0 * (eng->maxA + 1) + (double)eng->np[eng->tmax - 1];
@@ -2713,6 +2981,183 @@ void build_mmt_plan(mdp_engine *eng)
         eng->mmt_kt.clear();
         eng->mmt_cidx.clear();
     }
+}
+
+// k_fwd_hs: the cube of the block's points (128 KiB for each shape)
+size_t hs_lds(const mdp_engine *eng) { return ((size_t)1 << eng->hs_nb) * mmt_pts(eng->hs_rt) * sizeof(double); }
+
+const void *hs_kernel(const mdp_engine *eng)
+{
+    if (eng->hs_nb == 8) return (const void *)k_fwd_hs<4, 8>;
+    if (eng->hs_nb == 9) return (const void *)k_fwd_hs<2, 9>;
+    return (const void *)k_fwd_hs<1, 10>;
+}
+
+// k_fwd_hs's tables (c-independent; nvar <= 10, years of at most 1 024
+// states).  Per year t >= 1:
+//  * butterfly passes over W = the bits of year t - 1's states, greedily the
+//    patch that adds the fewest new cube positions first (ties: fewest
+//    pairs); a pass lists the positions a1 holding a value with the bit set,
+//    bit 31 when a1 ^ bit holds one too (accumulate, else assign).  After the
+//    passes every j below some state of year t - 1 holds U[j];
+//  * the year's states ordered by (B & W, B), so a tile's 16 states share
+//    their reachable hidden states; per tile K = the j in that down-closure
+//    below some state of the tile, ascending, padded to whole pipeline
+//    chunks (row 0, C = 0), and per (K entry, state) the byte offset of the
+//    item Pc[j][B] in the column's Pg row (its zero slot, nitems, for j not
+//    below B, padded states and padded entries);
+//  * the states' cube positions in tile order (~0: padding), the free 16-row
+//    park blocks (no state of the year in them), the wave plan.
+// Year 0's positions head dpos.  Refused (hs = false: k_fwd_mmt runs) for a
+// year with a repeated state or an item the direct plan lacks.
+void build_hs_plan(mdp_engine *eng)
+{
+    eng->hs = false;
+    if (eng->nvar > 10 || eng->tmax < 2 || eng->npmax > 1024 || eng->ystate.size() < eng->tmax) return;
+    const uint32_t nb = std::max<uint32_t>(8u, eng->nvar), rt = nb == 8 ? 4u : nb == 9 ? 2u : 1u, pts = mmt_pts(rt);
+    const uint32_t tmaxit = nb == 10 ? 4u : nb == 9 ? 2u : 1u, cw = 4 * mmt_u(rt), ncube = 1u << nb;
+    const uint32_t zero = eng->nitems;  // the Pg row's zero slot
+    if ((uint64_t)zero * 8u >= 0xffffffffull) return;
+    std::unordered_map<uint64_t, uint32_t> item;  // (j, B) -> item
+    for (uint32_t js = 0; js < eng->nj; ++js)
+        for (uint32_t i = eng->cj_item0[js]; i < eng->cj_item0[js + 1]; ++i)
+            item.emplace(((uint64_t)eng->cj_bits[js] << 32) | eng->itemB[i], i);
+    std::vector<uint32_t> yoff(eng->tmax + 1, 0);
+    for (uint32_t t = 0; t < eng->tmax; ++t) yoff[t + 1] = yoff[t] + eng->np[t];
+    auto st = [&](uint32_t t, uint32_t l) { return eng->ystate[yoff[t] + l]; };
+    eng->hs_kt.clear();
+    eng->hs_cidx.clear();
+    eng->hs_pass.clear();
+    eng->hs_ppos.clear();
+    eng->hs_dpos.clear();
+    eng->hs_ktile.assign((size_t)(eng->tmax + 1) * kMmtMaxTiles, make_uint2(0u, 1u));
+    eng->hs_wplan.assign((size_t)(eng->tmax + 1) * 16 * tmaxit, make_uint2(0u, 0u));
+    eng->hs_pk.assign((size_t)(eng->tmax + 1) * 16, 0u);
+    eng->hs_pbase.assign(eng->tmax + 1, 0u);
+    eng->hs_dbase.assign(eng->tmax + 1, 0u);
+    std::vector<uint8_t> seen(ncube, 0);
+    auto distinct = [&](uint32_t t) {
+        bool ok = true;
+        for (uint32_t l = 0; l < eng->np[t]; ++l) {
+            const uint32_t b = st(t, l);
+            if (b >= ncube || seen[b]) ok = false;
+            else seen[b] = 1;
+        }
+        for (uint32_t l = 0; l < eng->np[t]; ++l)
+            if (st(t, l) < ncube) seen[st(t, l)] = 0;
+        return ok;
+    };
+    if (!distinct(0)) return;
+    for (uint32_t l = 0; l < (eng->np[0] + 15) / 16 * 16; ++l) eng->hs_dpos.push_back(l < eng->np[0] ? st(0, l) : ~0u);
+    double fb = 0.0, fm = 0.0;
+    std::vector<uint8_t> live(ncube);
+    std::vector<uint32_t> lv;
+    for (uint32_t t = 1; t < eng->tmax; ++t) {
+        const uint32_t npp = eng->np[t - 1], npc = eng->np[t], ncol = (npc + 15) / 16;
+        if (!distinct(t)) return;
+        // butterfly passes
+        std::fill(live.begin(), live.end(), 0);
+        lv.clear();
+        uint32_t W = 0;
+        for (uint32_t k = 0; k < npp; ++k) {
+            W |= st(t - 1, k);
+            live[st(t - 1, k)] = 1;
+            lv.push_back(st(t - 1, k));
+        }
+        eng->hs_pbase[t] = (uint32_t)eng->hs_pass.size();
+        for (uint32_t rem = W; rem;) {
+            uint32_t best = 0, bnew = ~0u, bpairs = ~0u;
+            for (uint32_t r = rem; r; r &= r - 1) {
+                const uint32_t bit = r & (0u - r);
+                uint32_t nw = 0, pr = 0;
+                for (uint32_t a : lv)
+                    if (a & bit) {
+                        ++pr;
+                        nw += !live[a ^ bit];
+                    }
+                if (nw < bnew || (nw == bnew && pr < bpairs)) {
+                    best = bit;
+                    bnew = nw;
+                    bpairs = pr;
+                }
+            }
+            rem &= ~best;
+            const uint32_t base = (uint32_t)eng->hs_ppos.size();
+            const size_t nlv = lv.size();
+            for (size_t i = 0; i < nlv; ++i) {
+                const uint32_t a = lv[i];
+                if (!(a & best)) continue;
+                const bool acc = live[a ^ best] != 0;
+                eng->hs_ppos.push_back(a | (acc ? 0x80000000u : 0u));
+                fb += acc ? 3.0 : 2.0;
+            }
+            for (size_t i = 0; i < nlv; ++i)
+                if ((lv[i] & best) && !live[lv[i] ^ best]) {
+                    live[lv[i] ^ best] = 1;
+                    lv.push_back(lv[i] ^ best);
+                }
+            eng->hs_pass.push_back(make_uint4(best, (uint32_t)eng->hs_ppos.size() - base, base, 0u));
+        }
+        // the year's states in tile order
+        std::vector<uint32_t> ord(npc);
+        for (uint32_t l = 0; l < npc; ++l) ord[l] = l;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+            const uint32_t bx = st(t, x), by = st(t, y);
+            return (bx & W) != (by & W) ? (bx & W) < (by & W) : bx < by;
+        });
+        eng->hs_dbase[t] = (uint32_t)eng->hs_dpos.size();
+        for (uint32_t i = 0; i < ncol * 16; ++i) eng->hs_dpos.push_back(i < npc ? st(t, ord[i]) : ~0u);
+        std::vector<uint32_t> nch(ncol);
+        std::vector<uint32_t> K;
+        for (uint32_t tile = 0; tile < ncol; ++tile) {
+            K.clear();
+            for (uint32_t i = 16 * tile; i < std::min(16 * tile + 16, npc); ++i) {
+                const uint32_t key = st(t, ord[i]) & W;
+                for (uint32_t j = key;; j = (j - 1) & key) {  // subsets of key (with j = 0 last)
+                    if (live[j]) K.push_back(j);
+                    if (!j) break;
+                }
+            }
+            std::sort(K.begin(), K.end());
+            K.erase(std::unique(K.begin(), K.end()), K.end());
+            const size_t start = eng->hs_kt.size();
+            for (uint32_t j : K) {
+                eng->hs_kt.push_back(j * pts * 8u);
+                for (uint32_t i = 16 * tile; i < 16 * tile + 16; ++i) {
+                    uint32_t o = zero;
+                    if (i < npc && !(j & ~st(t, ord[i]))) {
+                        auto it = item.find(((uint64_t)j << 32) | st(t, ord[i]));
+                        if (it == item.end()) return;
+                        o = it->second;
+                    }
+                    eng->hs_cidx.push_back(o * 8u);
+                }
+            }
+            while ((eng->hs_kt.size() - start) % cw) {
+                eng->hs_kt.push_back(0u);
+                for (uint32_t l = 0; l < 16; ++l) eng->hs_cidx.push_back(zero * 8u);
+            }
+            nch[tile] = (uint32_t)((eng->hs_kt.size() - start) / cw);
+            eng->hs_ktile[(size_t)t * kMmtMaxTiles + tile] = make_uint2((uint32_t)start, nch[tile]);
+            fm += 2.0 * 16.0 * (double)(eng->hs_kt.size() - start);
+        }
+        // free park blocks
+        std::vector<uint8_t> used(ncube / 16, 0);
+        for (uint32_t l = 0; l < npc; ++l) used[st(t, l) / 16] = 1;
+        uint32_t room = 0;
+        for (uint32_t b = 0; b < ncube / 16 && room < 16; ++b)
+            if (!used[b]) eng->hs_pk[(size_t)t * 16 + room++] = b * 16;
+        plan_waves(nch, tmaxit, 1u, room, eng->hs_wplan.data() + (size_t)t * 16 * tmaxit);
+    }
+    eng->hs_pbase[eng->tmax] = (uint32_t)eng->hs_pass.size();
+    if (eng->hs_kt.empty()) eng->hs_kt.push_back(0u);
+    if (eng->hs_ppos.empty()) eng->hs_ppos.push_back(0u);
+    if (eng->hs_pass.empty()) eng->hs_pass.push_back(make_uint4(0u, 0u, 0u, 0u));
+    eng->hs_mfma_pt = fm;
+    eng->hs_flops_pt = fb + fm + (double)eng->np[eng->tmax - 1];
+    eng->hs_rt = rt;
+    eng->hs_nb = nb;
+    eng->hs = hs_lds(eng) <= device_lds_max() && eng->hs_kt.size() < (1u << 26);
 }
 
 int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
@@ -2731,11 +3176,14 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
     // transition descriptors [k][2^sh >= npcp] (Q-row offset | nX << kOffBits;
     // an absent transition names the zero slot with nX = 0)
     // MDP_WIDE_MMA: 0 -> k_fwd_wide; 1 -> round 5's k_fwd_mma (<= 256
-    // states); unset / 2 -> k_fwd_mmt (<= 1 024 states)
+    // states); unset / 2 -> k_fwd_mmt (<= 1 024 states); 3 -> k_fwd_hs
+    // (nvar <= 10; else k_fwd_mmt)
     const char *mv = eng->opts.get("MDP_WIDE_MMA");
     const int mmode = mv ? atoi(mv) : 2;
     eng->mmt = false;
-    if (mmode == 2) build_mmt_plan(eng);
+    eng->hs = false;
+    if (mmode == 3) build_hs_plan(eng);
+    if (mmode == 2 || (mmode == 3 && !eng->hs)) build_mmt_plan(eng);
     eng->mma = false;
     if (eng->npmax <= 256 && eng->maxA <= 24) {
         if (mmode == 1) {
@@ -3127,6 +3575,7 @@ size_t fused_lds(const mdp_engine *eng, size_t ct_len)
 }
 
 constexpr size_t kWidePgBytes = 256ull << 20;  // wide path: item-factor chunk
+constexpr size_t kHsPgBytes = 2048ull << 20;   // k_fwd_hs: item factors of the columns of one launch
 constexpr size_t kWideVBytes = 1ull << 30;     // wide path: state-vector scratch
 
 // k_fwd_wide: per-lane x^r, y^r tables, r <= maxA
@@ -3232,6 +3681,15 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
                 return rc;
             if (eng->mmt)
                 HIP_TRY(hipFuncSetAttribute(mmt_kernel(eng), hipFuncAttributeMaxDynamicSharedMemorySize, (int)mmt_lds(eng)));
+            if (eng->hs &&
+                ((rc = dev_upload(&d.hs_kt, eng->hs_kt)) || (rc = dev_upload(&d.hs_cidx, eng->hs_cidx)) ||
+                 (rc = dev_upload(&d.hs_pbase, eng->hs_pbase)) || (rc = dev_upload(&d.hs_ppos, eng->hs_ppos)) ||
+                 (rc = dev_upload(&d.hs_dpos, eng->hs_dpos)) || (rc = dev_upload(&d.hs_dbase, eng->hs_dbase)) ||
+                 (rc = dev_upload(&d.hs_pk, eng->hs_pk)) || (rc = dev_upload(&d.hs_ktile, eng->hs_ktile)) ||
+                 (rc = dev_upload(&d.hs_wplan, eng->hs_wplan)) || (rc = dev_upload(&d.hs_pass, eng->hs_pass))))
+                return rc;
+            if (eng->hs)
+                HIP_TRY(hipFuncSetAttribute(hs_kernel(eng), hipFuncAttributeMaxDynamicSharedMemorySize, (int)hs_lds(eng)));
             HIP_TRY(hipFuncSetAttribute((const void *)k_fwd_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)wide_lds(eng)));
             return MDP_OK;
@@ -3269,6 +3727,8 @@ void free_device(DevCtx &d)
                     d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot, d.qlane, d.islot,
                     d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan,
                     d.mmt_kt, d.mmt_ktile, d.mmt_wplan, d.mmt_cidx,
+                    d.hs_kt, d.hs_cidx, d.hs_pbase, d.hs_ppos, d.hs_dpos, d.hs_dbase, d.hs_pk, d.hs_ktile,
+                    d.hs_wplan, d.hs_pass,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -3351,7 +3811,16 @@ int set_grid_dev(mdp_engine *eng, DevCtx &d, const double *e, uint32_t ne, const
         d.wide_cb_items = (uint32_t)std::min(cap_c, std::max<size_t>(1, kWidePgBytes / 8 / std::max<size_t>(1, eng->nitems)));
         if (const char *cv = eng->opts.get("MDP_WIDE_CB"))  // tests: force several launches per slot
             d.wide_cb_items = std::min(d.wide_cb_items, (uint32_t)std::max(1, atoi(cv)));
-        if ((rc = dev_reserve(&d.Pg, &d.cap_pg, (size_t)d.wide_cb_items * eng->nitems + 1))) return rc;
+        if (eng->hs) {  // k_fwd_hs reads the item factors of its columns: rows of nitems + 1 (zero slot)
+            const size_t ldp = (size_t)eng->nitems + 1;
+            d.wide_cb_items = (uint32_t)std::min<size_t>(nc, std::max<size_t>(1, kHsPgBytes / 8 / ldp));
+            if (const char *cv = eng->opts.get("MDP_WIDE_CB"))
+                d.wide_cb_items = std::min(d.wide_cb_items, (uint32_t)std::max(1, atoi(cv)));
+            if ((rc = dev_reserve(&d.Pg, &d.cap_pg, (size_t)d.wide_cb_items * ldp))) return rc;
+            HIP_TRY(hipMemset(d.Pg, 0, (size_t)d.wide_cb_items * ldp * sizeof(double)));
+        } else if ((rc = dev_reserve(&d.Pg, &d.cap_pg, (size_t)d.wide_cb_items * eng->nitems + 1))) {
+            return rc;
+        }
     }
     if (eng->wide) {
         // c values per k_fwd_wide launch: the two state vectors of every
@@ -3580,18 +4049,47 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
     const KernelEvents ev = t_kev;
     t_kev = KernelEvents{};
     if (ev.start) HIP_TRY(hipEventRecord(ev.start, s));
-    if (k == 1) {
+    auto witems = [&](uint32_t c0, uint32_t n, uint32_t ldp) {
+        const dim3 gi((eng->nitems + kBlock - 1) / kBlock, n);
+#define MDP_WITEMS(NV) \
+    do { note_launch(eng, "k_witems<%d>", NV); \
+    hipLaunchKernelGGL((k_witems<NV>), gi, dim3(kBlock), 0, s, d.c, d.nc, c0, eng->nvar, d.Zg, d.sv, eng->nitems, d.items, d.Pg, ldp); } while (0)
+        if (eng->nvar <= 8) MDP_WITEMS(8);
+        else if (eng->nvar <= 16) MDP_WITEMS(16);
+        else MDP_WITEMS(24);
+#undef MDP_WITEMS
+    };
+    if (eng->hs) {
+        // slot 1: the item factors of every column when they fit one Pg
+        // block (kHsPgBytes), else nothing; slot 2: k_fwd_hs, or per column
+        // chunk k_witems then k_fwd_hs
+        const uint32_t cb = d.wide_cb_items, ldp = eng->nitems + 1;
+        const bool one = cb >= d.nc;
+        if (k == 1) {
+            if (one && eng->nitems) witems(0, d.nc, ldp);
+        } else {
+            const uint32_t rt = eng->hs_rt, nb = eng->hs_nb, npb = (d.ne + mmt_pts(rt) - 1) / mmt_pts(rt);
+            for (uint32_t c0 = 0; c0 < d.nc; c0 += cb) {
+                const uint32_t n = std::min(cb, d.nc - c0);
+                if (!one && eng->nitems) witems(c0, n, ldp);
+                const uint64_t nbk = (uint64_t)npb * n;
+                if (nbk > 0x7fffffffull) return mdp_set_error(MDP_EUNSUPPORTED, "grid of %llu k_fwd_hs workgroups", (unsigned long long)nbk);
+                note_launch(eng, "k_fwd_hs<%u,%u>", rt, nb);
+#define MDP_HS(RT, NB) \
+    hipLaunchKernelGGL((k_fwd_hs<RT, NB>), dim3((uint32_t)nbk), dim3(kMmaThreads), hs_lds(eng), s, d.Pg, ldp, c0, d.np_d, \
+                       d.hs_kt, d.hs_cidx, d.hs_ktile, d.hs_wplan, d.hs_pass, d.hs_pbase, d.hs_ppos, d.hs_dpos, \
+                       d.hs_dbase, d.hs_pk, eng->tmax, eng->prior0, d.e, d.ne, out, os.se, os.sc)
+                if (nb == 8) MDP_HS(4, 8);
+                else if (nb == 9) MDP_HS(2, 9);
+                else MDP_HS(1, 10);
+#undef MDP_HS
+            }
+        }
+    } else if (k == 1) {
         const uint32_t cb = d.wide_cb_items;
         for (uint32_t c0 = 0; c0 < d.nc; c0 += cb) {
             const uint32_t n = std::min(cb, d.nc - c0);
-            const dim3 gi((eng->nitems + kBlock - 1) / kBlock, n);
-#define MDP_WITEMS(NV) \
-    do { note_launch(eng, "k_witems<%d>", NV); \
-    hipLaunchKernelGGL((k_witems<NV>), gi, dim3(kBlock), 0, s, d.c, d.nc, c0, eng->nvar, d.Zg, d.sv, eng->nitems, d.items, d.Pg); } while (0)
-            if (eng->nvar <= 8) MDP_WITEMS(8);
-            else if (eng->nvar <= 16) MDP_WITEMS(16);
-            else MDP_WITEMS(24);
-#undef MDP_WITEMS
+            witems(c0, n, eng->nitems);
             const dim3 gq((uint32_t)((eng->ldQ + kBlock - 1) / kBlock), n);
             note_launch(eng, "k_wq");
             hipLaunchKernelGGL(k_wq, gq, dim3(kBlock), 0, s, c0, eng->nitems, d.Pg, eng->ncoef_d, d.qstart, d.qitem,
@@ -4354,6 +4852,7 @@ int mdp_engine_kernel_ms(mdp_engine *eng, double *ms, int max_k)
 const char *mdp_engine_kernel_name(const mdp_engine *eng, int k)
 {
     if (!eng || k < 0 || k >= 3) return "";
+    if (eng->wide && eng->hs) return k == 0 && eng->nitems ? "k_zrows" : k == 1 && eng->nitems ? "k_witems" : k == 2 ? "k_fwd_hs" : "";
     if (eng->wide) return k < 2 && !eng->nitems ? "" : k == 2 && eng->mmt ? "k_fwd_mmt" : k == 2 && eng->mma ? "k_fwd_mma" : kKernelNames[2][k];
     if (eng->jit && eng->qglobal)  // Q rows built in HBM, then the hipRTC forward kernel
         return k < 2 && !eng->nitems ? "" : k == 2 ? "k_forward" : kKernelNames[2][k];
@@ -4433,7 +4932,7 @@ int mdp_engine_work(const mdp_engine *eng, uint64_t ne, uint64_t nc, double *flo
     double per_pt = (double)eng->nuses * (2.0 * (D + 1.0) + 2.0) + 3.0 * (D + 1.0) +
                     2.0 * (double)eng->npmax;
     if (eng->jit) per_pt = eng->jit_flops_pt;  // the generated code's own count
-    if (eng->wide) per_pt = eng->mmt ? eng->mmt_flops_pt : eng->wide_flops_pt;
+    if (eng->wide) per_pt = eng->hs ? eng->hs_flops_pt : eng->mmt ? eng->mmt_flops_pt : eng->wide_flops_pt;
     if (flop_impl) *flop_impl = per_pt * pts;
     // SURVEY.md §8(d) F_alg (dense-in-j formulation)
     double fwd = 0;

@@ -26,6 +26,7 @@ PATHS = {  # path name -> engine knobs
     "default": {}, "nosplit": {"MDP_VSPLIT": "1"}, "split2": {"MDP_VSPLIT": "2"}, "split4": {"MDP_VSPLIT": "4"},
     "wide": {"MDP_WIDE": "1"}, "wideplain": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "0"},
     "mma5": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "1"},
+    "hs": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "3"},
     "epl2": {"MDP_VLDS_EPL": "2"},
 }
 # (pmiss, years, grid, path, variable patches): the config-2 generator with
@@ -67,7 +68,7 @@ for pmiss, T, s, path, nvar in CASES:
     per_pt = (time.perf_counter() - t0) / 8
     w = eng.work(s, s)
     fa = eng.work_fact(s, s)  # the algorithmic minimum (each distinct transition once per point)
-    fwd = [v for k, v in kms.items() if k in ("k_forward", "k_fwd_wide", "k_fwd_mma", "k_fwd_mmt")]
+    fwd = [v for k, v in kms.items() if k in ("k_forward", "k_fwd_wide", "k_fwd_mma", "k_fwd_mmt", "k_fwd_hs")]
     print(json.dumps({"pmiss": pmiss, "nvar": nvar, "years": T, "grid": s, "path": path, "npstates_max": int(model.npstates.max()),
                       "nuses": eng.info()["nuses"], "variant": eng.info()["variant"], "create_s": t_create,
                       "launched": sorted(eng.launched()), "step_ms": step * 1e3,
