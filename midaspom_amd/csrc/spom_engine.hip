@@ -1788,14 +1788,16 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
 // destination rows).  Q3 semantics: ones at year 0's states; L = prior0 x
 // the sum over the last year's states.  Sums reordered against the
 // reference's (positive terms for e in [0, 1]: ~1e-15 relative).
+constexpr uint32_t kHsRadix = 4;  // k_fwd_hs: patches per v Pe pass (at most; the plan's default)
+constexpr uint32_t kHsPre = 4;    // k_fwd_hs: v Pe passes a year whose descriptors are loaded up front
 template <int RT, int NB>
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
     const double *__restrict__ Pg, uint32_t ldp, uint32_t c0, const uint32_t *__restrict__ np,
     const uint32_t *__restrict__ kt, const uint32_t *__restrict__ cidx, const uint2 *__restrict__ ktile,
     const uint2 *__restrict__ wplan, const uint4 *__restrict__ pass, const uint32_t *__restrict__ pbase,
-    const uint32_t *__restrict__ ppos, const uint32_t *__restrict__ dpos, const uint32_t *__restrict__ dbase,
+    const uint2 *__restrict__ ppos, const uint32_t *__restrict__ dpos, const uint32_t *__restrict__ dbase,
     const uint32_t *__restrict__ pk, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
-    double *__restrict__ out, uint32_t ld_out, uint32_t out_cs)
+    double *__restrict__ out, uint32_t ld_out, uint32_t out_cs, uint32_t probe)
 {
     constexpr uint32_t PTS = mmt_pts(RT), NC = 1u << NB, TMAX = NC > 256 ? NC / 256 : 1, U = mmt_u(RT);
     static_assert(TMAX * RT <= 4 && NC * PTS <= 16384, "cube and tiles");
@@ -1879,34 +1881,115 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u) bb[0][u] = cval(dd[0][u]);
     };
+    // y^k of the thread's point (the v Pe passes' last scaling)
+    double *ypw = mlds + (size_t)NC * PTS;  // [k][point], k <= NB
+    if (threadIdx.x < PTS) {
+        double a = 1.0;
+        for (uint32_t k = 0; k <= (uint32_t)NB; ++k, a *= yq) ypw[k * PTS + threadIdx.x] = a;
+    }
+    __syncthreads();
+    // one coset of a v Pe pass (R patches, bit masks mb): read the positions
+    // holding a value (mask inm; the rest count as 0), the R butterflies
+    // V[j] += x V[j | b] in registers, write every subset of them (the
+    // mask's closure) -- in the year's last pass times y^|position|
+    auto coset = [&](auto rc, uint2 ce, const uint32_t (&mb)[kHsRadix], bool last) {
+        constexpr uint32_t R = decltype(rc)::value, NQ = 1u << R;
+        const uint32_t g = ce.x, inm = ce.y;
+        uint32_t outm = inm;
+        outm |= (outm & 0xaaaau) >> 1;
+        outm |= (outm & 0xccccu) >> 2;
+        outm |= (outm & 0xf0f0u) >> 4;
+        outm |= (outm & 0xff00u) >> 8;
+        auto pos = [&](uint32_t qq) {
+            uint32_t o = g;
+#pragma unroll
+            for (uint32_t k = 0; k < R; ++k) o |= (qq >> k) & 1u ? mb[k] : 0u;
+            return o;
+        };
+        double v[NQ];
+#pragma unroll
+        for (uint32_t qq = 0; qq < NQ; ++qq) v[qq] = (inm >> qq) & 1u ? V[(size_t)pos(qq) * PTS + pp] : 0.0;
+#pragma unroll
+        for (uint32_t k = 0; k < R; ++k)
+#pragma unroll
+            for (uint32_t qq = 0; qq < NQ; ++qq)
+                if (qq & (1u << k)) v[qq ^ (1u << k)] = fma(xq, v[qq], v[qq ^ (1u << k)]);
+        if (last) {
+            double sc[R + 1];
+            sc[0] = ypw[__builtin_popcount(g) * PTS + pp];
+#pragma unroll
+            for (uint32_t k = 1; k <= R; ++k) sc[k] = sc[k - 1] * yq;
+#pragma unroll
+            for (uint32_t qq = 0; qq < NQ; ++qq) v[qq] *= sc[__builtin_popcount(qq)];
+        }
+#pragma unroll
+        for (uint32_t qq = 0; qq < NQ; ++qq)
+            if ((outm >> qq) & 1u) V[(size_t)pos(qq) * PTS + pp] = v[qq];
+    };
     for (uint32_t t = 1; t < tmax; ++t) {
-        // v Pe: one butterfly pass per patch of W (pass table: bit mask,
-        // pairs, position-list base; a position's bit 31 says its partner
-        // already holds a value to add to)
-        const uint32_t pb0 = pbase[t], pb1 = pbase[t + 1];
+        // the year's first work item: its K entries, C offsets and first C
+        // values do not depend on the cube, so their loads are in flight
+        // through the v Pe passes
+        mdp_d4 acc[TMAX][RT];
+        Item cur = plan(t, 0);
+        const Item first = cur;
+        if (cur.active && !(probe & 2u)) prime(cur);
+        // v Pe: U[j] = y^|j| sum_{A >= j} v[A] x^(|A| - |j|), the patches of
+        // W up to kHsRadix at a time (pass table: the r patches' bit
+        // positions, r, cosets, coset-list base); the first kHsPre passes'
+        // descriptors and this thread's first coset of each are loaded up
+        // front (one latency a year)
+        const uint32_t pb0 = pbase[t], pb1 = (probe & 1u) ? pb0 : pbase[t + 1];
+        const uint32_t i0 = threadIdx.x / PTS;
+        uint4 pdp[kHsPre];
+        uint2 cep[kHsPre];
+#pragma unroll
+        for (uint32_t k = 0; k < kHsPre; ++k)
+            if (pb0 + k < pb1) {
+                pdp[k] = pass[pb0 + k];
+                cep[k] = i0 < pdp[k].z ? ppos[pdp[k].w + i0] : make_uint2(0u, 0u);
+            }
         for (uint32_t ps = pb0; ps < pb1; ++ps) {
-            const uint4 pd = pass[ps];  // (uniform)
-            const uint32_t bit = pd.x, npairs = pd.y, base = pd.z;
-            for (uint32_t i = threadIdx.x / PTS; i < npairs; i += kMmaThreads / PTS) {
-                const uint32_t pe = ppos[base + i], a1 = pe & 0x7fffffffu;
-                double *v1 = V + (size_t)a1 * PTS + pp, *v0 = V + (size_t)(a1 ^ bit) * PTS + pp;
-                const double w = *v1, z = (pe >> 31) ? *v0 : 0.0;
-                *v0 = fma(xq, w, z);
-                *v1 = yq * w;
+            const uint32_t k0 = ps - pb0;
+            uint4 pd;
+            if (k0 < kHsPre) {
+                pd = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+                for (uint32_t k = 0; k < kHsPre; ++k)
+                    if (k == k0) pd = pdp[k];
+            } else {
+                pd = pass[ps];
+            }
+            const uint32_t r = pd.y, ncos = pd.z, base = pd.w;
+            const bool last = ps + 1 == pb1;
+            uint32_t mb[kHsRadix];
+#pragma unroll
+            for (uint32_t k = 0; k < kHsRadix; ++k) mb[k] = k < r ? 1u << ((pd.x >> (5 * k)) & 31u) : 0u;
+            for (uint32_t i = i0; i < ncos; i += kMmaThreads / PTS) {
+                uint2 ce;
+                if (i == i0 && k0 < kHsPre) {
+                    ce = make_uint2(0u, 0u);
+#pragma unroll
+                    for (uint32_t k = 0; k < kHsPre; ++k)
+                        if (k == k0) ce = cep[k];
+                } else {
+                    ce = ppos[base + i];
+                }
+                if (r == 4) coset(std::integral_constant<uint32_t, 4>{}, ce, mb, last);
+                else if (r == 3) coset(std::integral_constant<uint32_t, 3>{}, ce, mb, last);
+                else if (r == 2) coset(std::integral_constant<uint32_t, 2>{}, ce, mb, last);
+                else coset(std::integral_constant<uint32_t, 1>{}, ce, mb, last);
             }
             __syncthreads();
         }
         // U Pc on the matrix cores
-        mdp_d4 acc[TMAX][RT];
-        Item cur = plan(t, 0);
-        const Item first = cur;
 #pragma unroll
         for (uint32_t i = 0; i < TMAX; ++i) {
 #pragma unroll
             for (uint32_t h = 0; h < RT; ++h) acc[i][h] = mdp_d4{0.0, 0.0, 0.0, 0.0};
             if (i > 0) cur = plan(t, i);
-            if (!cur.active) break;  // a wave's items are its first ones
-            prime(cur);
+            if (!cur.active || (probe & 2u)) break;  // a wave's items are its first ones
+            if (i > 0) prime(cur);
             mdp_d4(&ac)[RT] = acc[i];  // (i is a constant once unrolled)
             auto chunk = [&](uint32_t ch, auto jc) {
                 constexpr uint32_t j = decltype(jc)::value;
@@ -2176,9 +2259,9 @@ struct DevCtx {
     uint2 *mmt_kt = nullptr, *mmt_ktile = nullptr, *mmt_wplan = nullptr;  // k_fwd_mmt tables
     uint32_t *mmt_cidx = nullptr;
     // k_fwd_hs tables
-    uint32_t *hs_kt = nullptr, *hs_cidx = nullptr, *hs_pbase = nullptr, *hs_ppos = nullptr, *hs_dpos = nullptr,
-             *hs_dbase = nullptr, *hs_pk = nullptr;
-    uint2 *hs_ktile = nullptr, *hs_wplan = nullptr;
+    uint32_t *hs_kt = nullptr, *hs_cidx = nullptr, *hs_pbase = nullptr, *hs_dpos = nullptr, *hs_dbase = nullptr,
+             *hs_pk = nullptr;
+    uint2 *hs_ktile = nullptr, *hs_wplan = nullptr, *hs_ppos = nullptr;
     uint4 *hs_pass = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
@@ -2204,8 +2287,8 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
     "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_JIT_SPLIT", "MDP_JIT_ROT",
-    "MDP_WIDE_MMA"};
-const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE"};
+    "MDP_WIDE_MMA", "MDP_HS_RADIX"};
+const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE", "MDP_HS_PROBE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
 #else
@@ -2326,8 +2409,9 @@ struct mdp_engine {
     // states' cube positions in tile order and free 16-row park blocks
     bool hs = false;
     uint32_t hs_rt = 0, hs_nb = 0;
-    std::vector<uint32_t> hs_kt, hs_cidx, hs_pbase, hs_ppos, hs_dpos, hs_dbase, hs_pk;
-    std::vector<uint2> hs_ktile, hs_wplan;
+    uint32_t hs_probe = 0;  // MDP_HS_PROBE (timing probes only, wrong results): 1 skips v Pe, 2 U Pc
+    std::vector<uint32_t> hs_kt, hs_cidx, hs_pbase, hs_dpos, hs_dbase, hs_pk;
+    std::vector<uint2> hs_ktile, hs_wplan, hs_ppos;
     std::vector<uint4> hs_pass;
     double hs_flops_pt = 0, hs_mfma_pt = 0;  // FP64 flops per grid point (padding included), of them MFMA
     std::vector<uint32_t> ystate;  // each year's states (short_state bits), year_off order
@@ -2984,7 +3068,10 @@ void build_mmt_plan(mdp_engine *eng)
 }
 
 // k_fwd_hs: the cube of the block's points (128 KiB for each shape)
-size_t hs_lds(const mdp_engine *eng) { return ((size_t)1 << eng->hs_nb) * mmt_pts(eng->hs_rt) * sizeof(double); }
+size_t hs_lds(const mdp_engine *eng)
+{
+    return (((size_t)1 << eng->hs_nb) + eng->hs_nb + 1) * mmt_pts(eng->hs_rt) * sizeof(double);  // + y^k table
+}
 
 const void *hs_kernel(const mdp_engine *eng)
 {
@@ -2997,9 +3084,10 @@ const void *hs_kernel(const mdp_engine *eng)
 // states).  Per year t >= 1:
 //  * butterfly passes over W = the bits of year t - 1's states, greedily the
 //    patch that adds the fewest new cube positions first (ties: fewest
-//    pairs); a pass lists the positions a1 holding a value with the bit set,
-//    bit 31 when a1 ^ bit holds one too (accumulate, else assign).  After the
-//    passes every j below some state of year t - 1 holds U[j];
+//    values to move), up to kHsRadix patches a pass; a pass lists its
+//    cosets (g, the mask of its positions holding a value; the kernel
+//    writes their subsets).  After the passes every j below some state of
+//    year t - 1 holds U[j];
 //  * the year's states ordered by (B & W, B), so a tile's 16 states share
 //    their reachable hidden states; per tile K = the j in that down-closure
 //    below some state of the tile, ascending, padded to whole pipeline
@@ -3018,6 +3106,11 @@ void build_hs_plan(mdp_engine *eng)
     const uint32_t tmaxit = nb == 10 ? 4u : nb == 9 ? 2u : 1u, cw = 4 * mmt_u(rt), ncube = 1u << nb;
     const uint32_t zero = eng->nitems;  // the Pg row's zero slot
     if ((uint64_t)zero * 8u >= 0xffffffffull) return;
+    // patches per v Pe pass (MDP_HS_RADIX, 1 .. kHsRadix; default 4, the
+    // measured best: profiles/r06/hs -- 1 024 cosets x points fill the block
+    // in one sweep; 5 left half the threads idle on 1 024-state years)
+    uint32_t radix = kHsRadix;
+    if (const char *rv = eng->opts.get("MDP_HS_RADIX")) radix = std::min<uint32_t>(kHsRadix, std::max(1, atoi(rv)));
     std::unordered_map<uint64_t, uint32_t> item;  // (j, B) -> item
     for (uint32_t js = 0; js < eng->nj; ++js)
         for (uint32_t i = eng->cj_item0[js]; i < eng->cj_item0[js + 1]; ++i)
@@ -3064,39 +3157,80 @@ void build_hs_plan(mdp_engine *eng)
             live[st(t - 1, k)] = 1;
             lv.push_back(st(t - 1, k));
         }
-        eng->hs_pbase[t] = (uint32_t)eng->hs_pass.size();
-        for (uint32_t rem = W; rem;) {
-            uint32_t best = 0, bnew = ~0u, bpairs = ~0u;
-            for (uint32_t r = rem; r; r &= r - 1) {
-                const uint32_t bit = r & (0u - r);
-                uint32_t nw = 0, pr = 0;
-                for (uint32_t a : lv)
-                    if (a & bit) {
-                        ++pr;
-                        nw += !live[a ^ bit];
+        // the patches of W in greedy order (the one adding the fewest new
+        // positions first; ties: fewest values to move), then in passes of
+        // three
+        std::vector<uint32_t> border;
+        {
+            std::vector<uint8_t> lt(live);
+            std::vector<uint32_t> l2(lv);
+            for (uint32_t rem = W; rem;) {
+                uint32_t best = 0, bnew = ~0u, bpairs = ~0u;
+                for (uint32_t rr = rem; rr; rr &= rr - 1) {
+                    const uint32_t bit = rr & (0u - rr);
+                    uint32_t nw = 0, pr = 0;
+                    for (uint32_t a : l2)
+                        if (a & bit) {
+                            ++pr;
+                            nw += !lt[a ^ bit];
+                        }
+                    if (nw < bnew || (nw == bnew && pr < bpairs)) {
+                        best = bit;
+                        bnew = nw;
+                        bpairs = pr;
                     }
-                if (nw < bnew || (nw == bnew && pr < bpairs)) {
-                    best = bit;
-                    bnew = nw;
-                    bpairs = pr;
                 }
+                rem &= ~best;
+                border.push_back((uint32_t)__builtin_ctz(best));
+                const size_t n2 = l2.size();
+                for (size_t i = 0; i < n2; ++i)
+                    if ((l2[i] & best) && !lt[l2[i] ^ best]) {
+                        lt[l2[i] ^ best] = 1;
+                        l2.push_back(l2[i] ^ best);
+                    }
             }
-            rem &= ~best;
+        }
+        eng->hs_pbase[t] = (uint32_t)eng->hs_pass.size();
+        const size_t npass = (border.size() + radix - 1) / radix;
+        for (size_t ip = 0, b0 = 0; ip < npass; ++ip) {
+            // passes of near-equal size (radix 3: 8 patches 3 + 3 + 2)
+            const uint32_t r = (uint32_t)((border.size() - b0 + (npass - ip) - 1) / (npass - ip));
+            uint32_t bp[kHsRadix] = {}, mask = 0, bits = 0;
+            for (uint32_t k = 0; k < r; ++k) {
+                bp[k] = border[b0 + k];
+                mask |= 1u << bp[k];
+                bits |= bp[k] << (5 * k);
+            }
+            b0 += r;
+            auto dep = [&](uint32_t q) {
+                uint32_t o = 0;
+                for (uint32_t k = 0; k < r; ++k)
+                    if (q & (1u << k)) o |= 1u << bp[k];
+                return o;
+            };
+            std::map<uint32_t, uint32_t> cos;  // g -> mask of positions holding a value
+            for (uint32_t a : lv) {
+                uint32_t q = 0;
+                for (uint32_t k = 0; k < r; ++k)
+                    if (a & (1u << bp[k])) q |= 1u << k;
+                cos[a & ~mask] |= 1u << q;
+            }
             const uint32_t base = (uint32_t)eng->hs_ppos.size();
-            const size_t nlv = lv.size();
-            for (size_t i = 0; i < nlv; ++i) {
-                const uint32_t a = lv[i];
-                if (!(a & best)) continue;
-                const bool acc = live[a ^ best] != 0;
-                eng->hs_ppos.push_back(a | (acc ? 0x80000000u : 0u));
-                fb += acc ? 3.0 : 2.0;
+            for (auto &kv : cos) {
+                uint32_t outm = kv.second;  // (the kernel's closure)
+                outm |= (outm & 0xaaaau) >> 1;
+                outm |= (outm & 0xccccu) >> 2;
+                outm |= (outm & 0xf0f0u) >> 4;
+                outm |= (outm & 0xff00u) >> 8;
+                eng->hs_ppos.push_back(make_uint2(kv.first, kv.second));
+                fb += 2.0 * (double)r * (double)(1u << (r - 1)) + (ip + 1 == npass ? (double)(1u << r) : 0.0);
+                for (uint32_t q = 0; q < (1u << r); ++q)
+                    if (((outm >> q) & 1u) && !live[kv.first | dep(q)]) {
+                        live[kv.first | dep(q)] = 1;
+                        lv.push_back(kv.first | dep(q));
+                    }
             }
-            for (size_t i = 0; i < nlv; ++i)
-                if ((lv[i] & best) && !live[lv[i] ^ best]) {
-                    live[lv[i] ^ best] = 1;
-                    lv.push_back(lv[i] ^ best);
-                }
-            eng->hs_pass.push_back(make_uint4(best, (uint32_t)eng->hs_ppos.size() - base, base, 0u));
+            eng->hs_pass.push_back(make_uint4(bits, r, (uint32_t)eng->hs_ppos.size() - base, base));
         }
         // the year's states in tile order
         std::vector<uint32_t> ord(npc);
@@ -3151,12 +3285,13 @@ void build_hs_plan(mdp_engine *eng)
     }
     eng->hs_pbase[eng->tmax] = (uint32_t)eng->hs_pass.size();
     if (eng->hs_kt.empty()) eng->hs_kt.push_back(0u);
-    if (eng->hs_ppos.empty()) eng->hs_ppos.push_back(0u);
+    if (eng->hs_ppos.empty()) eng->hs_ppos.push_back(make_uint2(0u, 0u));
     if (eng->hs_pass.empty()) eng->hs_pass.push_back(make_uint4(0u, 0u, 0u, 0u));
     eng->hs_mfma_pt = fm;
     eng->hs_flops_pt = fb + fm + (double)eng->np[eng->tmax - 1];
     eng->hs_rt = rt;
     eng->hs_nb = nb;
+    if (const char *pv = eng->opts.get("MDP_HS_PROBE")) eng->hs_probe = (uint32_t)atoi(pv) & 3u;
     eng->hs = hs_lds(eng) <= device_lds_max() && eng->hs_kt.size() < (1u << 26);
 }
 
@@ -3176,10 +3311,12 @@ int build_wide_plan(mdp_engine *eng, const mdp_problem *p)
     // transition descriptors [k][2^sh >= npcp] (Q-row offset | nX << kOffBits;
     // an absent transition names the zero slot with nX = 0)
     // MDP_WIDE_MMA: 0 -> k_fwd_wide; 1 -> round 5's k_fwd_mma (<= 256
-    // states); unset / 2 -> k_fwd_mmt (<= 1 024 states); 3 -> k_fwd_hs
-    // (nvar <= 10; else k_fwd_mmt)
+    // states); 2 -> k_fwd_mmt (<= 1 024 states); 3 -> k_fwd_hs (nvar <= 10;
+    // else k_fwd_mmt); unset -> k_fwd_hs for years of more than 64 states,
+    // else k_fwd_mmt (measured, profiles/r06/hs: k_fwd_hs 1.3x / 4.4x / 5.2x
+    // / 5.8x faster on 128 / 256 / 512 / 1 024 states, 1.27x slower on 64)
     const char *mv = eng->opts.get("MDP_WIDE_MMA");
-    const int mmode = mv ? atoi(mv) : 2;
+    const int mmode = mv ? atoi(mv) : (eng->npmax > 64 ? 3 : 2);
     eng->mmt = false;
     eng->hs = false;
     if (mmode == 3) build_hs_plan(eng);
@@ -4078,7 +4215,7 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
 #define MDP_HS(RT, NB) \
     hipLaunchKernelGGL((k_fwd_hs<RT, NB>), dim3((uint32_t)nbk), dim3(kMmaThreads), hs_lds(eng), s, d.Pg, ldp, c0, d.np_d, \
                        d.hs_kt, d.hs_cidx, d.hs_ktile, d.hs_wplan, d.hs_pass, d.hs_pbase, d.hs_ppos, d.hs_dpos, \
-                       d.hs_dbase, d.hs_pk, eng->tmax, eng->prior0, d.e, d.ne, out, os.se, os.sc)
+                       d.hs_dbase, d.hs_pk, eng->tmax, eng->prior0, d.e, d.ne, out, os.se, os.sc, eng->hs_probe)
                 if (nb == 8) MDP_HS(4, 8);
                 else if (nb == 9) MDP_HS(2, 9);
                 else MDP_HS(1, 10);

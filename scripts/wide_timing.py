@@ -15,6 +15,9 @@ from pathlib import Path
 import numpy as np
 import torch
 
+if os.environ.get("WIDE_DIAG") == "1":  # measurement-only knobs (MDP_HS_PROBE) need the diag library
+    os.environ["MIDASPOM_DIAG_LIB"] = "1"
+
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import midaspom_amd as mdp  # noqa: E402

@@ -62,7 +62,11 @@ CASES = {
     "wide_mma5": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
                   {"MDP_WIDE": "1", "MDP_WIDE_MMA": "1"}, "k_fwd_mma"),
     "wide_big": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 10, 4, {1: 9})), 70, 37,
-                 {}, "k_fwd_mmt<2,512,1buf>"),
+                 {}, "k_fwd_hs<1,10>"),
+    "wide_big_mmt": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 10, 4, {1: 9})), 70, 37,
+                     {"MDP_WIDE_MMA": "2"}, "k_fwd_mmt<2,512,1buf>"),
+    "wide_hs": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
+                {"MDP_WIDE": "1", "MDP_WIDE_MMA": "3"}, "k_fwd_mmt"),  # 12 variable patches: > 10, k_fwd_mmt
     "wide_plain": (lambda: mdp.Model.from_obs(_wide_obs(np.random.default_rng(3), 12, 5, {1: 6})), 130, 37,
                    {"MDP_WIDE": "1", "MDP_WIDE_MMA": "0"}, "k_fwd_wide"),
 }

@@ -59,6 +59,9 @@ VARIANTS = [
     ("MDP_VSPLIT=2", "wide45"),
     ("MDP_VLDS_EPL=2", "wide45"),
     ("MDP_VLDS_MAXUSES=100", "wide45"),  # past it: the wide kernels take the problem
+    ("MDP_WIDE=1;MDP_WIDE_MMA=3;MDP_HS_RADIX=1", "wide45"),
+    ("MDP_WIDE=1;MDP_WIDE_MMA=3;MDP_HS_RADIX=2", "wide45"),
+    ("MDP_WIDE=1;MDP_WIDE_MMA=3;MDP_HS_RADIX=4", "wide45"),
 ]
 # options that select no kernel: compile-time diagnostics and host threads
 TOOLING = ["MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE"]

@@ -279,7 +279,9 @@ def _wide_engine_run(model, e, c, path, monkeypatch):
     """Run on the named path and check it ran: "default" (years of 17-64
     states: the specialised kernel with its states in LDS; more: the wide
     kernels), "wide" (MDP_WIDE=1: k_witems + k_wq + the matrix-core forward
-    k_fwd_mmt, years of up to 1 024 states), "wide-mma5" (round 5's
+    k_fwd_hs for years of more than 64 states and up to 10 variable patches,
+    else k_fwd_mmt, years of up to 1 024 states), "wide-mmt" (k_fwd_mmt,
+    MDP_WIDE_MMA=2), "wide-mma5" (round 5's
     k_fwd_mma, MDP_WIDE_MMA=1, up to 256 states), "wide-hs" (k_fwd_hs through
     the hidden states, MDP_WIDE_MMA=3, up to 10 variable patches) or
     "wide-plain" (k_fwd_wide, MDP_WIDE_MMA=0)."""
@@ -293,6 +295,8 @@ def _wide_engine_run(model, e, c, path, monkeypatch):
         monkeypatch.setenv("MDP_WIDE_MMA", "1")
     if path == "wide-hs":
         monkeypatch.setenv("MDP_WIDE_MMA", "3")
+    if path == "wide-mmt":
+        monkeypatch.setenv("MDP_WIDE_MMA", "2")
     with mdp.Engine(model) as eng:
         got = eng.loglik_grid(e, c)
         launched, info = eng.launched(), eng.info()
@@ -314,12 +318,15 @@ def launched_forward(model, path):
         return f"k_fwd_hs<{ {8: 4, 9: 2, 10: 1}[nb]},{nb}>"
     if path == "wide-mma5" and npm <= 256:
         return f"k_fwd_mma<{64 if npm <= 64 else 128 if npm <= 128 else 256}>"
-    if path in ("default", "wide", "wide-hs") and npm <= 1024:
+    if path in ("default", "wide") and npm > 64 and nvar <= 10 and len(model.npstates) > 1:
+        nb = max(8, nvar)
+        return f"k_fwd_hs<{ {8: 4, 9: 2, 10: 1}[nb]},{nb}>"
+    if path in ("default", "wide", "wide-hs", "wide-mmt") and npm <= 1024:
         return f"k_fwd_mmt<{'4,128,2buf' if npm <= 128 else '2,256,1buf' if npm <= 256 else '2,512,1buf' if npm <= 512 else '1,1024,1buf'}>"
     return "k_fwd_wide"
 
 
-@pytest.mark.parametrize("path", ["default", "wide", "wide-mma5", "wide-hs", "wide-plain"])
+@pytest.mark.parametrize("path", ["default", "wide", "wide-mma5", "wide-hs", "wide-mmt", "wide-plain"])
 @pytest.mark.parametrize("missing", [{0: 5}, {3: 5}, {2: 6}, {4: 6}, {0: 8}, {3: 8}, {1: 5, 2: 6}, {0: 6, 4: 7},
                                      {1: 8, 2: 7}, {2: 7, 3: 8}])
 def test_wide_years_vs_oracle(missing, path, monkeypatch):
@@ -355,8 +362,8 @@ def test_random_wide_problems(seed, monkeypatch):
     e, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.2])))
     c, _ = mdp.grid(int(rng.integers(2, 6)), 0.0, float(rng.choice([1.0, 1.5])))
     ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c, threads=16)
-    for path, cb in (("default", None), ("wide", None), ("wide-mma5", None), ("wide-hs", None), ("wide-plain", None),
-                     ("wide", "1"), ("wide-hs", "1")):
+    for path, cb in (("default", None), ("wide", None), ("wide-mma5", None), ("wide-hs", None), ("wide-mmt", None),
+                     ("wide-plain", None), ("wide", "1"), ("wide-hs", "1")):
         if cb:
             monkeypatch.setenv("MDP_WIDE_CB", cb)
         got = _wide_engine_run(model, e, c, path, monkeypatch)
@@ -373,7 +380,7 @@ def _big_obs(rng, missing, full=()):
     return obs
 
 
-@pytest.mark.parametrize("path", ["default", "wide-hs", "wide-plain"])
+@pytest.mark.parametrize("path", ["default", "wide-mmt", "wide-plain"])
 @pytest.mark.parametrize("missing,full", [({1: 9}, ()), ({0: 9}, ()), ({2: 9, 3: 9}, ()), ({4: 8}, (2,)),
                                           ({}, (0,)), ({1: 9}, (2, 3)), ({3: 7}, (5,))],
                          ids=["512@1", "512@0", "512@2+3", "1024@2", "1024@0", "512@1+1024@2+3", "1024@5"])
@@ -396,7 +403,7 @@ def test_big_years_vs_oracle(missing, full, path, monkeypatch):
     assert_loglik_close(got, ref)
 
 
-@pytest.mark.parametrize("path", ["default", "wide-hs", "wide-plain"])
+@pytest.mark.parametrize("path", ["default", "wide-mmt", "wide-plain"])
 def test_big_survey_series_sampled(tmp_path, path, monkeypatch):
     """The 10-variable-patch survey series of scripts/wide_timing.py (60 %
     unvisited: years of up to 1 024 states, two of 512; 643 328 uses per
@@ -438,7 +445,7 @@ def test_wide_survey_series_sampled(tmp_path, path, monkeypatch):
     assert_loglik_close(got[ie, ic], ref)
 
 
-@pytest.mark.parametrize("path", ["default", "wide-hs", "wide-plain"])
+@pytest.mark.parametrize("path", ["default", "wide-mmt", "wide-plain"])
 def test_wide_survey_series_128_states(tmp_path, path, monkeypatch):
     """The 60 %-unvisited survey series of scripts/wide_timing.py (up to 128
     states a year, 66 416 uses per point): k_fwd_mmt<4> by default, and
@@ -459,7 +466,7 @@ def test_wide_survey_series_128_states(tmp_path, path, monkeypatch):
     assert_loglik_close(got[ie, ic], ref)
 
 
-@pytest.mark.parametrize("path", ["default", "wide-hs"])
+@pytest.mark.parametrize("path", ["default", "wide-mmt"])
 def test_wide_survey_series_256_states(tmp_path, path, monkeypatch):
     """A 75 %-unvisited survey series (three years of 256 states, 257 024
     uses per point): k_fwd_mmt<4> (64 points a block)
@@ -491,7 +498,8 @@ def test_wide_path_matches_direct_path(golden, monkeypatch, fname, s):
     with mdp.Engine(model) as eng:
         assert eng.info()["variant"] >= 20000
         b = eng.loglik_grid(g, g)
-        assert set(eng.kernel_ms()) <= {"k_zrows", "k_witems+k_wq", "k_fwd_wide", "k_fwd_mma", "k_fwd_mmt"}
+        assert set(eng.kernel_ms()) <= {"k_zrows", "k_witems+k_wq", "k_witems", "k_fwd_wide", "k_fwd_mma", "k_fwd_mmt",
+                                        "k_fwd_hs"}
     assert_loglik_close(b, a, atol=1e-11)
 
 
