@@ -1889,17 +1889,12 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
     }
     __syncthreads();
     // one coset of a v Pe pass (R patches, bit masks mb): read the positions
-    // holding a value (mask inm; the rest count as 0), the R butterflies
-    // V[j] += x V[j | b] in registers, write every subset of them (the
-    // mask's closure) -- in the year's last pass times y^|position|
+    // of mask inm (the rest count as 0), the R butterflies V[j] += x V[j | b]
+    // in registers, write the positions of mask outm (those some later pass
+    // or the year's products read) -- in the year's last pass times y^|j|
     auto coset = [&](auto rc, uint2 ce, const uint32_t (&mb)[kHsRadix], bool last) {
         constexpr uint32_t R = decltype(rc)::value, NQ = 1u << R;
-        const uint32_t g = ce.x, inm = ce.y;
-        uint32_t outm = inm;
-        outm |= (outm & 0xaaaau) >> 1;
-        outm |= (outm & 0xccccu) >> 2;
-        outm |= (outm & 0xf0f0u) >> 4;
-        outm |= (outm & 0xff00u) >> 8;
+        const uint32_t g = ce.x, inm = ce.y & 0xffffu, outm = ce.y >> 16;
         auto pos = [&](uint32_t qq) {
             uint32_t o = g;
 #pragma unroll
@@ -3082,12 +3077,12 @@ const void *hs_kernel(const mdp_engine *eng)
 
 // k_fwd_hs's tables (c-independent; nvar <= 10, years of at most 1 024
 // states).  Per year t >= 1:
-//  * butterfly passes over W = the bits of year t - 1's states, greedily the
-//    patch that adds the fewest new cube positions first (ties: fewest
-//    values to move), up to kHsRadix patches a pass; a pass lists its
-//    cosets (g, the mask of its positions holding a value; the kernel
-//    writes their subsets).  After the passes every j below some state of
-//    year t - 1 holds U[j];
+//  * butterfly passes over W = the bits of year t - 1's states, up to
+//    kHsRadix patches a pass: first the patches set in no hidden state the
+//    year's products read, then greedily the one adding the fewest new cube
+//    positions; a pass lists its cosets (g, the masks of the positions it
+//    reads and writes: only those whose value still reaches a hidden state
+//    the products read).  After the passes every such j holds U[j];
 //  * the year's states ordered by (B & W, B), so a tile's 16 states share
 //    their reachable hidden states; per tile K = the j in that down-closure
 //    below some state of the tile, ascending, padded to whole pipeline
@@ -3157,43 +3152,74 @@ void build_hs_plan(mdp_engine *eng)
             live[st(t - 1, k)] = 1;
             lv.push_back(st(t - 1, k));
         }
-        // the patches of W in greedy order (the one adding the fewest new
-        // positions first; ties: fewest values to move), then in passes of
-        // three
+        // D: the hidden states below some state of year t - 1 (U's
+        // support); N: those below some state of year t (U's reads, the
+        // union of the year's K lists); M(rem): the positions whose value
+        // still reaches N by the butterflies over the patches rem (N's
+        // up-closure over rem) -- a pass reads live positions in M(before)
+        // and writes positions in M(after) only
+        std::vector<uint8_t> Dm(ncube, 0), Nm(ncube, 0), Mb(ncube), Ma(ncube);
+        for (uint32_t k = 0; k < npp; ++k) Dm[st(t - 1, k)] = 1;
+        for (uint32_t bit = 1; bit < ncube; bit <<= 1)
+            for (uint32_t q = 0; q < ncube; ++q)
+                if ((q & bit) && Dm[q]) Dm[q ^ bit] = 1;
+        uint32_t nused = 0;  // patches set in some j of N
+        for (uint32_t l = 0; l < npc; ++l) {
+            const uint32_t key = st(t, l) & W;
+            for (uint32_t j = key;; j = (j - 1) & key) {
+                if (Dm[j] && !Nm[j]) {
+                    Nm[j] = 1;
+                    nused |= j;
+                }
+                if (!j) break;
+            }
+        }
+        auto upclose = [&](uint32_t rem, std::vector<uint8_t> &M) {
+            M = Nm;
+            for (uint32_t bit = 1; bit < ncube; bit <<= 1)
+                if (rem & bit)
+                    for (uint32_t q = 0; q < ncube; ++q)
+                        if (!(q & bit) && M[q]) M[q | bit] = 1;
+        };
+        // the patches of W: first those set in no j of N (each halves what
+        // later passes touch), then greedily the one adding the fewest new
+        // positions (ties: fewest values to move)
         std::vector<uint32_t> border;
         {
             std::vector<uint8_t> lt(live);
             std::vector<uint32_t> l2(lv);
-            for (uint32_t rem = W; rem;) {
-                uint32_t best = 0, bnew = ~0u, bpairs = ~0u;
-                for (uint32_t rr = rem; rr; rr &= rr - 1) {
-                    const uint32_t bit = rr & (0u - rr);
-                    uint32_t nw = 0, pr = 0;
-                    for (uint32_t a : l2)
-                        if (a & bit) {
-                            ++pr;
-                            nw += !lt[a ^ bit];
+            for (int phase = 0; phase < 2; ++phase)
+                for (uint32_t rem = W & (phase ? nused : ~nused); rem;) {
+                    uint32_t best = 0, bnew = ~0u, bpairs = ~0u;
+                    for (uint32_t rr = rem; rr; rr &= rr - 1) {
+                        const uint32_t bit = rr & (0u - rr);
+                        uint32_t nw = 0, pr = 0;
+                        for (uint32_t a : l2)
+                            if (a & bit) {
+                                ++pr;
+                                nw += !lt[a ^ bit];
+                            }
+                        if (nw < bnew || (nw == bnew && pr < bpairs)) {
+                            best = bit;
+                            bnew = nw;
+                            bpairs = pr;
                         }
-                    if (nw < bnew || (nw == bnew && pr < bpairs)) {
-                        best = bit;
-                        bnew = nw;
-                        bpairs = pr;
                     }
+                    rem &= ~best;
+                    border.push_back((uint32_t)__builtin_ctz(best));
+                    const size_t n2 = l2.size();
+                    for (size_t i = 0; i < n2; ++i)
+                        if ((l2[i] & best) && !lt[l2[i] ^ best]) {
+                            lt[l2[i] ^ best] = 1;
+                            l2.push_back(l2[i] ^ best);
+                        }
                 }
-                rem &= ~best;
-                border.push_back((uint32_t)__builtin_ctz(best));
-                const size_t n2 = l2.size();
-                for (size_t i = 0; i < n2; ++i)
-                    if ((l2[i] & best) && !lt[l2[i] ^ best]) {
-                        lt[l2[i] ^ best] = 1;
-                        l2.push_back(l2[i] ^ best);
-                    }
-            }
         }
         eng->hs_pbase[t] = (uint32_t)eng->hs_pass.size();
         const size_t npass = (border.size() + radix - 1) / radix;
+        uint32_t remw = W;
         for (size_t ip = 0, b0 = 0; ip < npass; ++ip) {
-            // passes of near-equal size (radix 3: 8 patches 3 + 3 + 2)
+            // passes of near-equal size (radix 4: 10 patches 4 + 3 + 3)
             const uint32_t r = (uint32_t)((border.size() - b0 + (npass - ip) - 1) / (npass - ip));
             uint32_t bp[kHsRadix] = {}, mask = 0, bits = 0;
             for (uint32_t k = 0; k < r; ++k) {
@@ -3202,14 +3228,18 @@ void build_hs_plan(mdp_engine *eng)
                 bits |= bp[k] << (5 * k);
             }
             b0 += r;
+            upclose(remw, Mb);
+            remw &= ~mask;
+            upclose(remw, Ma);
             auto dep = [&](uint32_t q) {
                 uint32_t o = 0;
                 for (uint32_t k = 0; k < r; ++k)
                     if (q & (1u << k)) o |= 1u << bp[k];
                 return o;
             };
-            std::map<uint32_t, uint32_t> cos;  // g -> mask of positions holding a value
+            std::map<uint32_t, uint32_t> cos;  // g -> mask of positions read
             for (uint32_t a : lv) {
+                if (!Mb[a]) continue;
                 uint32_t q = 0;
                 for (uint32_t k = 0; k < r; ++k)
                     if (a & (1u << bp[k])) q |= 1u << k;
@@ -3217,12 +3247,15 @@ void build_hs_plan(mdp_engine *eng)
             }
             const uint32_t base = (uint32_t)eng->hs_ppos.size();
             for (auto &kv : cos) {
-                uint32_t outm = kv.second;  // (the kernel's closure)
-                outm |= (outm & 0xaaaau) >> 1;
-                outm |= (outm & 0xccccu) >> 2;
-                outm |= (outm & 0xf0f0u) >> 4;
-                outm |= (outm & 0xff00u) >> 8;
-                eng->hs_ppos.push_back(make_uint2(kv.first, kv.second));
+                uint32_t cl = kv.second;  // the read positions' subsets
+                cl |= (cl & 0xaaaau) >> 1;
+                cl |= (cl & 0xccccu) >> 2;
+                cl |= (cl & 0xf0f0u) >> 4;
+                cl |= (cl & 0xff00u) >> 8;
+                uint32_t outm = 0;
+                for (uint32_t q = 0; q < (1u << r); ++q)
+                    if (((cl >> q) & 1u) && Ma[kv.first | dep(q)]) outm |= 1u << q;
+                eng->hs_ppos.push_back(make_uint2(kv.first, kv.second | outm << 16));
                 fb += 2.0 * (double)r * (double)(1u << (r - 1)) + (ip + 1 == npass ? (double)(1u << r) : 0.0);
                 for (uint32_t q = 0; q < (1u << r); ++q)
                     if (((outm >> q) & 1u) && !live[kv.first | dep(q)]) {
@@ -3248,7 +3281,7 @@ void build_hs_plan(mdp_engine *eng)
             for (uint32_t i = 16 * tile; i < std::min(16 * tile + 16, npc); ++i) {
                 const uint32_t key = st(t, ord[i]) & W;
                 for (uint32_t j = key;; j = (j - 1) & key) {  // subsets of key (with j = 0 last)
-                    if (live[j]) K.push_back(j);
+                    if (Dm[j]) K.push_back(j);
                     if (!j) break;
                 }
             }
