@@ -1790,13 +1790,23 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
 // reference's (positive terms for e in [0, 1]: ~1e-15 relative).
 constexpr uint32_t kHsRadix = 4;  // k_fwd_hs: patches per v Pe pass (at most; the plan's default)
 constexpr uint32_t kHsPre = 4;    // k_fwd_hs: v Pe passes a year whose descriptors are loaded up front
+// diag build, MDP_HS_PROBE bit 2: workgroup 0's wave 0 stamps the shader
+// clock at each phase of each year into out[] (results not stored)
+#ifdef MDP_DIAG_BUILD
+#define MDP_HS_STAMP(k)                                                                                      \
+    do {                                                                                                     \
+        if ((probe & 4u) && blockIdx.x == 0 && threadIdx.x == 0) out[(size_t)t * 8 + (k)] = (double)clock64(); \
+    } while (0)
+#else
+#define MDP_HS_STAMP(k) do { } while (0)
+#endif
 template <int RT, int NB>
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
     const double *__restrict__ Pg, uint32_t ldp, uint32_t c0, const uint32_t *__restrict__ np,
     const uint32_t *__restrict__ kt, const uint32_t *__restrict__ cidx, const uint2 *__restrict__ ktile,
     const uint2 *__restrict__ wplan, const uint4 *__restrict__ pass, const uint32_t *__restrict__ pbase,
     const uint2 *__restrict__ ppos, const uint32_t *__restrict__ dpos, const uint32_t *__restrict__ dbase,
-    const uint32_t *__restrict__ pk, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
+    const uint2 *__restrict__ dpk, const uint32_t *__restrict__ pk, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
     double *__restrict__ out, uint32_t ld_out, uint32_t out_cs, uint32_t probe)
 {
     constexpr uint32_t PTS = mmt_pts(RT), NC = 1u << NB, TMAX = NC > 256 ? NC / 256 : 1, U = mmt_u(RT);
@@ -1892,9 +1902,12 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
     // of mask inm (the rest count as 0), the R butterflies V[j] += x V[j | b]
     // in registers, write the positions of mask outm (those some later pass
     // or the year's products read) -- in the year's last pass times y^|j|
+    // (a wave's cosets share their masks, build_hs_plan: uniform branches
+    // skip the positions no lane of the wave reads or writes)
     auto coset = [&](auto rc, uint2 ce, const uint32_t (&mb)[kHsRadix], bool last) {
         constexpr uint32_t R = decltype(rc)::value, NQ = 1u << R;
-        const uint32_t g = ce.x, inm = ce.y & 0xffffu, outm = ce.y >> 16;
+        const uint32_t my = __builtin_amdgcn_readfirstlane(ce.y);
+        const uint32_t g = ce.x, inm = my & 0xffffu, outm = my >> 16;
         auto pos = [&](uint32_t qq) {
             uint32_t o = g;
 #pragma unroll
@@ -1903,7 +1916,12 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
         };
         double v[NQ];
 #pragma unroll
-        for (uint32_t qq = 0; qq < NQ; ++qq) v[qq] = (inm >> qq) & 1u ? V[(size_t)pos(qq) * PTS + pp] : 0.0;
+        for (uint32_t qq = 0; qq < NQ; ++qq) {
+            if ((inm >> qq) & 1u)
+                v[qq] = V[(size_t)pos(qq) * PTS + pp];
+            else
+                v[qq] = 0.0;
+        }
 #pragma unroll
         for (uint32_t k = 0; k < R; ++k)
 #pragma unroll
@@ -1921,31 +1939,47 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
         for (uint32_t qq = 0; qq < NQ; ++qq)
             if ((outm >> qq) & 1u) V[(size_t)pos(qq) * PTS + pp] = v[qq];
     };
-    for (uint32_t t = 1; t < tmax; ++t) {
-        // the year's first work item: its K entries, C offsets and first C
-        // values do not depend on the cube, so their loads are in flight
-        // through the v Pe passes
-        mdp_d4 acc[TMAX][RT];
-        Item cur = plan(t, 0);
-        const Item first = cur;
-        if (cur.active && !(probe & 2u)) prime(cur);
-        // v Pe: U[j] = y^|j| sum_{A >= j} v[A] x^(|A| - |j|), the patches of
-        // W up to kHsRadix at a time (pass table: the r patches' bit
-        // positions, r, cosets, coset-list base); the first kHsPre passes'
-        // descriptors and this thread's first coset of each are loaded up
-        // front (one latency a year)
-        const uint32_t pb0 = pbase[t], pb1 = (probe & 1u) ? pb0 : pbase[t + 1];
-        const uint32_t i0 = threadIdx.x / PTS;
-        uint4 pdp[kHsPre];
-        uint2 cep[kHsPre];
+    // v Pe pass tables of a year: the pass range, the first kHsPre passes'
+    // descriptors and this thread's first coset of each -- loaded a year
+    // ahead (during the previous year's products), so no year waits on them
+    const uint32_t i0 = threadIdx.x / PTS;
+    uint32_t pb0 = 0, pb1 = 0;
+    uint4 pdp[kHsPre];
+    uint2 cep[kHsPre];
+    auto load_passes = [&](uint32_t ty) {
+        pb0 = pbase[ty];
+        pb1 = (probe & 1u) ? pb0 : pbase[ty + 1];
 #pragma unroll
         for (uint32_t k = 0; k < kHsPre; ++k)
             if (pb0 + k < pb1) {
                 pdp[k] = pass[pb0 + k];
                 cep[k] = i0 < pdp[k].z ? ppos[pdp[k].w + i0] : make_uint2(0u, 0u);
             }
+    };
+    if (tmax > 1) load_passes(1);
+    for (uint32_t t = 1; t < tmax; ++t) {
+        // the year's first work item: its K entries, C offsets and first C
+        // values do not depend on the cube, so their loads are in flight
+        // through the v Pe passes; so are the positions its new states are
+        // stored at (dpk: 4 x 16 bits per lane and tile, 0xffff: padding)
+        mdp_d4 acc[TMAX][RT];
+        Item cur = plan(t, 0);
+        const Item first = cur;
+        if (cur.active && !(probe & 2u)) prime(cur);
+        const uint32_t db = dbase[t];
+        uint2 dk[TMAX];
+#pragma unroll
+        for (uint32_t i = 0; i < TMAX; ++i) {
+            const uint2 w2 = wplan[(t * 16 + wv) * TMAX + i];
+            dk[i] = (w2.y >> 24) ? dpk[(db / 16 + (w2.y & 0xffu)) * 4 + kk] : make_uint2(~0u, ~0u);
+        }
+        // v Pe: U[j] = y^|j| sum_{A >= j} v[A] x^(|A| - |j|), the patches of
+        // W up to kHsRadix at a time (pass table: the r patches' bit
+        // positions, r, cosets, coset-list base)
+        MDP_HS_STAMP(0);
         for (uint32_t ps = pb0; ps < pb1; ++ps) {
             const uint32_t k0 = ps - pb0;
+            if (ps == pb0) MDP_HS_STAMP(1);
             uint4 pd;
             if (k0 < kHsPre) {
                 pd = make_uint4(0u, 0u, 0u, 0u);
@@ -1977,6 +2011,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
             }
             __syncthreads();
         }
+        MDP_HS_STAMP(2);
         // U Pc on the matrix cores
 #pragma unroll
         for (uint32_t i = 0; i < TMAX; ++i) {
@@ -2015,15 +2050,17 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
             if (ch + 1 < cur.ce) chunk(ch + 1, std::integral_constant<uint32_t, 1>{});
             if (ch + 2 < cur.ce) chunk(ch + 2, std::integral_constant<uint32_t, 2>{});
         }
+        MDP_HS_STAMP(3);
+        if (t + 1 < tmax) load_passes(t + 1);
         __syncthreads();  // every wave has read U
+        MDP_HS_STAMP(4);
         // the lane's accumulators: new states tile * 16 + kk + 4 r (tile
-        // order; dpos: their cube positions, ~0 for padding) of point h * 16 + col
-        const uint32_t db = dbase[t];
-        auto store = [&](uint32_t tile, const mdp_d4 (&a)[RT]) {
+        // order) of point h * 16 + col
+        auto store = [&](uint2 d2, const mdp_d4 (&a)[RT]) {
 #pragma unroll
             for (uint32_t r = 0; r < 4; ++r) {
-                const uint32_t pos = dpos[db + tile * 16 + kk + 4 * r];
-                if (pos == ~0u) continue;
+                const uint32_t pos = ((r < 2 ? d2.x : d2.y) >> (16 * (r & 1))) & 0xffffu;
+                if (pos == 0xffffu) continue;
                 double *dst = V + (size_t)pos * PTS + col;
 #pragma unroll
                 for (uint32_t h = 0; h < RT; ++h) dst[h * 16] = a[h][r];
@@ -2057,11 +2094,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
         for (uint32_t i = 0; i < TMAX; ++i) {
             const Item it = i == 0 ? first : plan(t, i);
             if (!it.active || it.ks != 0) break;
-            store(it.tile, acc[i]);
+            store(dk[i], acc[i]);
         }
+        MDP_HS_STAMP(5);
         __syncthreads();
+        MDP_HS_STAMP(6);
     }
-    if (threadIdx.x < PTS) {
+    if (threadIdx.x < PTS && !(probe & 4u)) {
         const uint32_t ie = p0 + threadIdx.x, dl = dbase[tmax - 1], npl = (np[tmax - 1] + 15) / 16 * 16;
         double L = 0.0;
         for (uint32_t l = 0; l < npl; ++l) {
@@ -2256,7 +2295,7 @@ struct DevCtx {
     // k_fwd_hs tables
     uint32_t *hs_kt = nullptr, *hs_cidx = nullptr, *hs_pbase = nullptr, *hs_dpos = nullptr, *hs_dbase = nullptr,
              *hs_pk = nullptr;
-    uint2 *hs_ktile = nullptr, *hs_wplan = nullptr, *hs_ppos = nullptr;
+    uint2 *hs_ktile = nullptr, *hs_wplan = nullptr, *hs_ppos = nullptr, *hs_dpk = nullptr;
     uint4 *hs_pass = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
@@ -2406,7 +2445,7 @@ struct mdp_engine {
     uint32_t hs_rt = 0, hs_nb = 0;
     uint32_t hs_probe = 0;  // MDP_HS_PROBE (timing probes only, wrong results): 1 skips v Pe, 2 U Pc
     std::vector<uint32_t> hs_kt, hs_cidx, hs_pbase, hs_dpos, hs_dbase, hs_pk;
-    std::vector<uint2> hs_ktile, hs_wplan, hs_ppos;
+    std::vector<uint2> hs_ktile, hs_wplan, hs_ppos, hs_dpk;
     std::vector<uint4> hs_pass;
     double hs_flops_pt = 0, hs_mfma_pt = 0;  // FP64 flops per grid point (padding included), of them MFMA
     std::vector<uint32_t> ystate;  // each year's states (short_state bits), year_off order
@@ -3246,6 +3285,7 @@ void build_hs_plan(mdp_engine *eng)
                 cos[a & ~mask] |= 1u << q;
             }
             const uint32_t base = (uint32_t)eng->hs_ppos.size();
+            std::map<uint32_t, std::vector<uint32_t>> bymask;  // read | write << 16 -> its cosets
             for (auto &kv : cos) {
                 uint32_t cl = kv.second;  // the read positions' subsets
                 cl |= (cl & 0xaaaau) >> 1;
@@ -3255,7 +3295,26 @@ void build_hs_plan(mdp_engine *eng)
                 uint32_t outm = 0;
                 for (uint32_t q = 0; q < (1u << r); ++q)
                     if (((cl >> q) & 1u) && Ma[kv.first | dep(q)]) outm |= 1u << q;
-                eng->hs_ppos.push_back(make_uint2(kv.first, kv.second | outm << 16));
+                bymask[kv.second | outm << 16].push_back(kv.first);
+            }
+            // cosets grouped by masks, pts / 64 ... a wave's worth at a time
+            // (64 / pts cosets a wave), each wave padded with copies of its
+            // first coset (a lane of the same wave: identical values)
+            const uint32_t cpw = 64u / pts;
+            for (auto &mv : bymask)
+                for (size_t i = 0; i < mv.second.size(); i += cpw)
+                    for (uint32_t k = 0; k < cpw; ++k)
+                        eng->hs_ppos.push_back(make_uint2(i + k < mv.second.size() ? mv.second[i + k] : mv.second[i],
+                                                          mv.first));
+            for (auto &kv : cos) {
+                uint32_t cl = kv.second;
+                cl |= (cl & 0xaaaau) >> 1;
+                cl |= (cl & 0xccccu) >> 2;
+                cl |= (cl & 0xf0f0u) >> 4;
+                cl |= (cl & 0xff00u) >> 8;
+                uint32_t outm = 0;
+                for (uint32_t q = 0; q < (1u << r); ++q)
+                    if (((cl >> q) & 1u) && Ma[kv.first | dep(q)]) outm |= 1u << q;
                 fb += 2.0 * (double)r * (double)(1u << (r - 1)) + (ip + 1 == npass ? (double)(1u << r) : 0.0);
                 for (uint32_t q = 0; q < (1u << r); ++q)
                     if (((outm >> q) & 1u) && !live[kv.first | dep(q)]) {
@@ -3317,6 +3376,18 @@ void build_hs_plan(mdp_engine *eng)
         plan_waves(nch, tmaxit, 1u, room, eng->hs_wplan.data() + (size_t)t * 16 * tmaxit);
     }
     eng->hs_pbase[eng->tmax] = (uint32_t)eng->hs_pass.size();
+    // the store positions per (16 positions of dpos, lane group kk): entries
+    // kk + 4 r, r = 0 .. 3, 16 bits each (0xffff: padding)
+    eng->hs_dpk.assign(eng->hs_dpos.size() / 16 * 4, make_uint2(0u, 0u));
+    for (size_t b = 0; b < eng->hs_dpos.size() / 16; ++b)
+        for (uint32_t kq = 0; kq < 4; ++kq) {
+            uint32_t w[4];
+            for (uint32_t r = 0; r < 4; ++r) {
+                const uint32_t ps = eng->hs_dpos[b * 16 + kq + 4 * r];
+                w[r] = ps == ~0u ? 0xffffu : ps;
+            }
+            eng->hs_dpk[b * 4 + kq] = make_uint2(w[0] | w[1] << 16, w[2] | w[3] << 16);
+        }
     if (eng->hs_kt.empty()) eng->hs_kt.push_back(0u);
     if (eng->hs_ppos.empty()) eng->hs_ppos.push_back(make_uint2(0u, 0u));
     if (eng->hs_pass.empty()) eng->hs_pass.push_back(make_uint4(0u, 0u, 0u, 0u));
@@ -3324,7 +3395,7 @@ void build_hs_plan(mdp_engine *eng)
     eng->hs_flops_pt = fb + fm + (double)eng->np[eng->tmax - 1];
     eng->hs_rt = rt;
     eng->hs_nb = nb;
-    if (const char *pv = eng->opts.get("MDP_HS_PROBE")) eng->hs_probe = (uint32_t)atoi(pv) & 3u;
+    if (const char *pv = eng->opts.get("MDP_HS_PROBE")) eng->hs_probe = (uint32_t)atoi(pv) & 7u;
     eng->hs = hs_lds(eng) <= device_lds_max() && eng->hs_kt.size() < (1u << 26);
 }
 
@@ -3856,7 +3927,8 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
                  (rc = dev_upload(&d.hs_pbase, eng->hs_pbase)) || (rc = dev_upload(&d.hs_ppos, eng->hs_ppos)) ||
                  (rc = dev_upload(&d.hs_dpos, eng->hs_dpos)) || (rc = dev_upload(&d.hs_dbase, eng->hs_dbase)) ||
                  (rc = dev_upload(&d.hs_pk, eng->hs_pk)) || (rc = dev_upload(&d.hs_ktile, eng->hs_ktile)) ||
-                 (rc = dev_upload(&d.hs_wplan, eng->hs_wplan)) || (rc = dev_upload(&d.hs_pass, eng->hs_pass))))
+                 (rc = dev_upload(&d.hs_wplan, eng->hs_wplan)) || (rc = dev_upload(&d.hs_pass, eng->hs_pass)) ||
+                 (rc = dev_upload(&d.hs_dpk, eng->hs_dpk))))
                 return rc;
             if (eng->hs)
                 HIP_TRY(hipFuncSetAttribute(hs_kernel(eng), hipFuncAttributeMaxDynamicSharedMemorySize, (int)hs_lds(eng)));
@@ -3898,7 +3970,7 @@ void free_device(DevCtx &d)
                     d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan,
                     d.mmt_kt, d.mmt_ktile, d.mmt_wplan, d.mmt_cidx,
                     d.hs_kt, d.hs_cidx, d.hs_pbase, d.hs_ppos, d.hs_dpos, d.hs_dbase, d.hs_pk, d.hs_ktile,
-                    d.hs_wplan, d.hs_pass,
+                    d.hs_wplan, d.hs_pass, d.hs_dpk,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
         if (ptr) (void)hipFree(ptr);
@@ -4248,7 +4320,7 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
 #define MDP_HS(RT, NB) \
     hipLaunchKernelGGL((k_fwd_hs<RT, NB>), dim3((uint32_t)nbk), dim3(kMmaThreads), hs_lds(eng), s, d.Pg, ldp, c0, d.np_d, \
                        d.hs_kt, d.hs_cidx, d.hs_ktile, d.hs_wplan, d.hs_pass, d.hs_pbase, d.hs_ppos, d.hs_dpos, \
-                       d.hs_dbase, d.hs_pk, eng->tmax, eng->prior0, d.e, d.ne, out, os.se, os.sc, eng->hs_probe)
+                       d.hs_dbase, d.hs_dpk, d.hs_pk, eng->tmax, eng->prior0, d.e, d.ne, out, os.se, os.sc, eng->hs_probe)
                 if (nb == 8) MDP_HS(4, 8);
                 else if (nb == 9) MDP_HS(2, 9);
                 else MDP_HS(1, 10);
