@@ -1803,9 +1803,8 @@ constexpr uint32_t kHsPre = 4;    // k_fwd_hs: v Pe passes a year whose descript
 template <int RT, int NB>
 __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
     const double *__restrict__ Pg, uint32_t ldp, uint32_t c0, const uint32_t *__restrict__ np,
-    const uint32_t *__restrict__ kt, const uint32_t *__restrict__ cidx, const uint2 *__restrict__ ktile,
-    const uint2 *__restrict__ wplan, const uint4 *__restrict__ pass, const uint32_t *__restrict__ pbase,
-    const uint2 *__restrict__ ppos, const uint32_t *__restrict__ dpos, const uint32_t *__restrict__ dbase,
+    const uint32_t *__restrict__ kt, const uint32_t *__restrict__ cidx, const uint4 *__restrict__ wplan,
+    const uint4 *__restrict__ pass, const uint32_t *__restrict__ pbase, const uint2 *__restrict__ ppos, const uint32_t *__restrict__ dpos, const uint32_t *__restrict__ dbase,
     const uint2 *__restrict__ dpk, const uint32_t *__restrict__ pk, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
     double *__restrict__ out, uint32_t ld_out, uint32_t out_cs, uint32_t probe)
 {
@@ -1847,9 +1846,12 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
         bool active, split;
         const uint32_t *kl, *cl;
     };
+    // item i of this wave in year t (wplan: chunk range, tile | slice |
+    // slices | park base | split | valid, the tile's K-list start and
+    // chunks: one scalar load, no dependent one)
     auto plan = [&](uint32_t t, uint32_t i) {
         Item it;
-        const uint2 wp = wplan[(t * 16 + wv) * TMAX + i];
+        const uint4 wp = wplan[(t * 16 + wv) * TMAX + i];
         it.cb = wp.x & 0xffffu;
         it.ce = wp.x >> 16;
         it.tile = wp.y & 0xffu;
@@ -1858,11 +1860,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
         it.pbase = (wp.y >> 17) & 31u;
         it.split = (wp.y >> 22) & 1u;
         it.active = (wp.y >> 24) != 0u;
-        const uint2 kt2 = ktile[t * kMmtMaxTiles + it.tile];
-        const uint32_t k0 = __builtin_amdgcn_readfirstlane(kt2.x);
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(wp.z);
         it.kl = kt + k0;
         it.cl = cidx + (size_t)k0 * 16;
-        it.nch = kt2.y;
+        it.nch = wp.w;
         return it;
     };
     // K entry (one per 16 lanes): the LDS byte offset of U's row j; per lane
@@ -1970,7 +1971,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
         uint2 dk[TMAX];
 #pragma unroll
         for (uint32_t i = 0; i < TMAX; ++i) {
-            const uint2 w2 = wplan[(t * 16 + wv) * TMAX + i];
+            const uint4 w2 = wplan[(t * 16 + wv) * TMAX + i];
             dk[i] = (w2.y >> 24) ? dpk[(db / 16 + (w2.y & 0xffu)) * 4 + kk] : make_uint2(~0u, ~0u);
         }
         // v Pe: U[j] = y^|j| sum_{A >= j} v[A] x^(|A| - |j|), the patches of
@@ -2295,7 +2296,8 @@ struct DevCtx {
     // k_fwd_hs tables
     uint32_t *hs_kt = nullptr, *hs_cidx = nullptr, *hs_pbase = nullptr, *hs_dpos = nullptr, *hs_dbase = nullptr,
              *hs_pk = nullptr;
-    uint2 *hs_ktile = nullptr, *hs_wplan = nullptr, *hs_ppos = nullptr, *hs_dpk = nullptr;
+    uint2 *hs_ppos = nullptr, *hs_dpk = nullptr;
+    uint4 *hs_wplan = nullptr;
     uint4 *hs_pass = nullptr;
     uint32_t wide_cb_items = 1, wide_cb_fwd = 1;  // c values per k_witems / k_fwd_wide launch
     std::vector<hipEvent_t> ev;  // kNumEv events per profiled run, reused
@@ -2445,7 +2447,8 @@ struct mdp_engine {
     uint32_t hs_rt = 0, hs_nb = 0;
     uint32_t hs_probe = 0;  // MDP_HS_PROBE (timing probes only, wrong results): 1 skips v Pe, 2 U Pc
     std::vector<uint32_t> hs_kt, hs_cidx, hs_pbase, hs_dpos, hs_dbase, hs_pk;
-    std::vector<uint2> hs_ktile, hs_wplan, hs_ppos, hs_dpk;
+    std::vector<uint2> hs_ppos, hs_dpk;
+    std::vector<uint4> hs_wplan;
     std::vector<uint4> hs_pass;
     double hs_flops_pt = 0, hs_mfma_pt = 0;  // FP64 flops per grid point (padding included), of them MFMA
     std::vector<uint32_t> ystate;  // each year's states (short_state bits), year_off order
@@ -3157,8 +3160,8 @@ void build_hs_plan(mdp_engine *eng)
     eng->hs_pass.clear();
     eng->hs_ppos.clear();
     eng->hs_dpos.clear();
-    eng->hs_ktile.assign((size_t)(eng->tmax + 1) * kMmtMaxTiles, make_uint2(0u, 1u));
-    eng->hs_wplan.assign((size_t)(eng->tmax + 1) * 16 * tmaxit, make_uint2(0u, 0u));
+    std::vector<uint2> ktile(kMmtMaxTiles), wtmp(16 * tmaxit);
+    eng->hs_wplan.assign((size_t)(eng->tmax + 1) * 16 * tmaxit, make_uint4(0u, 0u, 0u, 1u));
     eng->hs_pk.assign((size_t)(eng->tmax + 1) * 16, 0u);
     eng->hs_pbase.assign(eng->tmax + 1, 0u);
     eng->hs_dbase.assign(eng->tmax + 1, 0u);
@@ -3364,7 +3367,7 @@ void build_hs_plan(mdp_engine *eng)
                 for (uint32_t l = 0; l < 16; ++l) eng->hs_cidx.push_back(zero * 8u);
             }
             nch[tile] = (uint32_t)((eng->hs_kt.size() - start) / cw);
-            eng->hs_ktile[(size_t)t * kMmtMaxTiles + tile] = make_uint2((uint32_t)start, nch[tile]);
+            ktile[tile] = make_uint2((uint32_t)start, nch[tile]);
             fm += 2.0 * 16.0 * (double)(eng->hs_kt.size() - start);
         }
         // free park blocks
@@ -3373,7 +3376,12 @@ void build_hs_plan(mdp_engine *eng)
         uint32_t room = 0;
         for (uint32_t b = 0; b < ncube / 16 && room < 16; ++b)
             if (!used[b]) eng->hs_pk[(size_t)t * 16 + room++] = b * 16;
-        plan_waves(nch, tmaxit, 1u, room, eng->hs_wplan.data() + (size_t)t * 16 * tmaxit);
+        plan_waves(nch, tmaxit, 1u, room, wtmp.data());
+        for (uint32_t i = 0; i < 16 * tmaxit; ++i) {
+            const uint2 kt2 = ktile[wtmp[i].y & 0xffu];
+            eng->hs_wplan[(size_t)t * 16 * tmaxit + i] =
+                (wtmp[i].y >> 24) ? make_uint4(wtmp[i].x, wtmp[i].y, kt2.x, kt2.y) : make_uint4(wtmp[i].x, wtmp[i].y, 0u, 1u);
+        }
     }
     eng->hs_pbase[eng->tmax] = (uint32_t)eng->hs_pass.size();
     // the store positions per (16 positions of dpos, lane group kk): entries
@@ -3926,7 +3934,7 @@ int init_device(mdp_engine *eng, DevCtx &d, const mdp_problem *p)
                 ((rc = dev_upload(&d.hs_kt, eng->hs_kt)) || (rc = dev_upload(&d.hs_cidx, eng->hs_cidx)) ||
                  (rc = dev_upload(&d.hs_pbase, eng->hs_pbase)) || (rc = dev_upload(&d.hs_ppos, eng->hs_ppos)) ||
                  (rc = dev_upload(&d.hs_dpos, eng->hs_dpos)) || (rc = dev_upload(&d.hs_dbase, eng->hs_dbase)) ||
-                 (rc = dev_upload(&d.hs_pk, eng->hs_pk)) || (rc = dev_upload(&d.hs_ktile, eng->hs_ktile)) ||
+                 (rc = dev_upload(&d.hs_pk, eng->hs_pk)) ||
                  (rc = dev_upload(&d.hs_wplan, eng->hs_wplan)) || (rc = dev_upload(&d.hs_pass, eng->hs_pass)) ||
                  (rc = dev_upload(&d.hs_dpk, eng->hs_dpk))))
                 return rc;
@@ -3969,7 +3977,7 @@ void free_device(DevCtx &d)
                     d.Pg, d.V, d.np_d, d.udesc_w, d.zc, d.plist, d.qslot, d.qlane, d.islot,
                     d.mma_kt, d.mma_kbase, d.mma_desc, d.mma_dbase, d.mma_wplan,
                     d.mmt_kt, d.mmt_ktile, d.mmt_wplan, d.mmt_cidx,
-                    d.hs_kt, d.hs_cidx, d.hs_pbase, d.hs_ppos, d.hs_dpos, d.hs_dbase, d.hs_pk, d.hs_ktile,
+                    d.hs_kt, d.hs_cidx, d.hs_pbase, d.hs_ppos, d.hs_dpos, d.hs_dbase, d.hs_pk,
                     d.hs_wplan, d.hs_pass, d.hs_dpk,
                     d.stamps[0], d.stamps[1], d.stamps[2]};
     for (void *ptr : ptrs)
@@ -4319,7 +4327,7 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
                 note_launch(eng, "k_fwd_hs<%u,%u>", rt, nb);
 #define MDP_HS(RT, NB) \
     hipLaunchKernelGGL((k_fwd_hs<RT, NB>), dim3((uint32_t)nbk), dim3(kMmaThreads), hs_lds(eng), s, d.Pg, ldp, c0, d.np_d, \
-                       d.hs_kt, d.hs_cidx, d.hs_ktile, d.hs_wplan, d.hs_pass, d.hs_pbase, d.hs_ppos, d.hs_dpos, \
+                       d.hs_kt, d.hs_cidx, d.hs_wplan, d.hs_pass, d.hs_pbase, d.hs_ppos, d.hs_dpos, \
                        d.hs_dbase, d.hs_dpk, d.hs_pk, eng->tmax, eng->prior0, d.e, d.ne, out, os.se, os.sc, eng->hs_probe)
                 if (nb == 8) MDP_HS(4, 8);
                 else if (nb == 9) MDP_HS(2, 9);
