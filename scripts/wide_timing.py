@@ -30,6 +30,7 @@ PATHS = {  # path name -> engine knobs
     "wide": {"MDP_WIDE": "1"}, "wideplain": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "0"},
     "mma5": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "1"},
     "hs": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "3"},
+    "mmt": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "2"},
     "epl2": {"MDP_VLDS_EPL": "2"},
 }
 # (pmiss, years, grid, path, variable patches): the config-2 generator with
