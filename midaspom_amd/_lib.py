@@ -205,7 +205,7 @@ ENGINE_OPTION_NAMES = (
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
     "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_JIT_SPLIT", "MDP_JIT_ROT",
-    "MDP_WIDE_MMA", "MDP_HS_RADIX",
+    "MDP_WIDE_MMA", "MDP_HS_RADIX", "MDP_HS_WAVES",
     # measurement-only: accepted by the diag build alone
     "MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE", "MDP_HS_PROBE")
 SCENARIO_OPTION_NAMES = ("MDP_SCN_BIG", "MDP_SCN_ROW")

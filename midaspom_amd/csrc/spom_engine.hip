@@ -1800,16 +1800,17 @@ constexpr uint32_t kHsPre = 4;    // k_fwd_hs: v Pe passes a year whose descript
 #else
 #define MDP_HS_STAMP(k) do { } while (0)
 #endif
-template <int RT, int NB>
-__global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
+template <int RT, int NB, int NW>
+__global__ __launch_bounds__(NW * 64, 4) void k_fwd_hs(  // (4 waves a SIMD: two 8-wave blocks a CU)
     const double *__restrict__ Pg, uint32_t ldp, uint32_t c0, const uint32_t *__restrict__ np,
     const uint32_t *__restrict__ kt, const uint32_t *__restrict__ cidx, const uint4 *__restrict__ wplan,
     const uint4 *__restrict__ pass, const uint32_t *__restrict__ pbase, const uint2 *__restrict__ ppos, const uint32_t *__restrict__ dpos, const uint32_t *__restrict__ dbase,
     const uint2 *__restrict__ dpk, const uint32_t *__restrict__ pk, uint32_t tmax, double prior0, const double *__restrict__ evals, uint32_t ne,
     double *__restrict__ out, uint32_t ld_out, uint32_t out_cs, uint32_t probe)
 {
-    constexpr uint32_t PTS = mmt_pts(RT), NC = 1u << NB, TMAX = NC > 256 ? NC / 256 : 1, U = mmt_u(RT);
-    static_assert(TMAX * RT <= 4 && NC * PTS <= 16384, "cube and tiles");
+    constexpr uint32_t PTS = mmt_pts(RT), NC = 1u << NB, NTH = NW * 64, TMAX = NC / 16 > NW ? NC / 16 / NW : 1,
+                       U = mmt_u(RT);
+    static_assert(TMAX * RT <= 4 && NC * PTS <= 16384 && NTH % PTS == 0, "cube and tiles");
     extern __shared__ __attribute__((aligned(16))) double mlds[];
     double *V = mlds;  // [j][point]
     const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1817,7 +1818,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
     const uint32_t npb = (ne + PTS - 1) / PTS, full = gridDim.x & ~7u, b = blockIdx.x;
     const uint32_t lb = b < full ? (b & 7u) * (full >> 3) + (b >> 3) : b;
     const uint32_t p0 = (lb % npb) * PTS, cl = lb / npb, ic = c0 + cl;
-    // this thread's point in the pass loops (1 024 is a multiple of PTS)
+    // this thread's point in the pass loops (NTH is a multiple of PTS)
     const uint32_t pp = threadIdx.x % PTS;
     double xq, yq;
     {
@@ -1829,11 +1830,11 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
     // the cube starts at zero (a position no year has written holds a finite
     // value whenever it is read: padded K entries meet it with C = 0), then
     // ones at year 0's states (Q3)
-    for (uint32_t i = threadIdx.x; i < NC * PTS; i += kMmaThreads) V[i] = 0.0;
+    for (uint32_t i = threadIdx.x; i < NC * PTS; i += NTH) V[i] = 0.0;
     __syncthreads();
     {
         const uint32_t n0 = (np[0] + 15) / 16 * 16, d0 = dbase[0];
-        for (uint32_t i = threadIdx.x; i < n0 * PTS; i += kMmaThreads) {
+        for (uint32_t i = threadIdx.x; i < n0 * PTS; i += NTH) {
             const uint32_t pos = dpos[d0 + i / PTS];
             if (pos != ~0u) V[pos * PTS + i % PTS] = 1.0;
         }
@@ -1851,7 +1852,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
     // chunks: one scalar load, no dependent one)
     auto plan = [&](uint32_t t, uint32_t i) {
         Item it;
-        const uint4 wp = wplan[(t * 16 + wv) * TMAX + i];
+        const uint4 wp = wplan[(t * NW + wv) * TMAX + i];
         it.cb = wp.x & 0xffffu;
         it.ce = wp.x >> 16;
         it.tile = wp.y & 0xffu;
@@ -1971,7 +1972,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
         uint2 dk[TMAX];
 #pragma unroll
         for (uint32_t i = 0; i < TMAX; ++i) {
-            const uint4 w2 = wplan[(t * 16 + wv) * TMAX + i];
+            const uint4 w2 = wplan[(t * NW + wv) * TMAX + i];
             dk[i] = (w2.y >> 24) ? dpk[(db / 16 + (w2.y & 0xffu)) * 4 + kk] : make_uint2(~0u, ~0u);
         }
         // v Pe: U[j] = y^|j| sum_{A >= j} v[A] x^(|A| - |j|), the patches of
@@ -1995,7 +1996,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_hs(
             uint32_t mb[kHsRadix];
 #pragma unroll
             for (uint32_t k = 0; k < kHsRadix; ++k) mb[k] = k < r ? 1u << ((pd.x >> (5 * k)) & 31u) : 0u;
-            for (uint32_t i = i0; i < ncos; i += kMmaThreads / PTS) {
+            for (uint32_t i = i0; i < ncos; i += NTH / PTS) {
                 uint2 ce;
                 if (i == i0 && k0 < kHsPre) {
                     ce = make_uint2(0u, 0u);
@@ -2323,7 +2324,7 @@ const char *const kEngineOptNames[] = {
     "MDP_JIT_EFAST", "MDP_QROWS_XCD", "MDP_FWD", "MDP_WIDE", "MDP_VSPLIT", "MDP_VLDS_EPL", "MDP_VLDS_MAXUSES",
     "MDP_JIT_CHUNK", "MDP_JIT_GATHER", "MDP_QGLOBAL", "MDP_FAST_LOG", "MDP_JIT_KBLOCK", "MDP_WIDE_CB",
     "MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE", "MDP_JIT_SPLIT", "MDP_JIT_ROT",
-    "MDP_WIDE_MMA", "MDP_HS_RADIX"};
+    "MDP_WIDE_MMA", "MDP_HS_RADIX", "MDP_HS_WAVES"};
 const char *const kDiagOptNames[] = {"MDP_DIAG", "MDP_JIT_HACK", "MDP_JIT_WPE", "MDP_HS_PROBE"};
 #ifdef MDP_DIAG_BUILD
 constexpr bool kDiagBuild = true;
@@ -2444,7 +2445,7 @@ struct mdp_engine {
     // states and their item offsets, per year butterfly passes, the new
     // states' cube positions in tile order and free 16-row park blocks
     bool hs = false;
-    uint32_t hs_rt = 0, hs_nb = 0;
+    uint32_t hs_rt = 0, hs_nb = 0, hs_nw = 16;
     uint32_t hs_probe = 0;  // MDP_HS_PROBE (timing probes only, wrong results): 1 skips v Pe, 2 U Pc
     std::vector<uint32_t> hs_kt, hs_cidx, hs_pbase, hs_dpos, hs_dbase, hs_pk;
     std::vector<uint2> hs_ppos, hs_dpk;
@@ -2984,17 +2985,18 @@ const void *mmt_kernel(const mdp_engine *eng)
 // give every tile a wave and the spare waves to the tiles whose slices are
 // longest (at least two chunks each; slices past the first `inplace` of a
 // tile park their partials, `room` 16-row blocks at most)
-void plan_waves(const std::vector<uint32_t> &nch, uint32_t tmaxit, uint32_t inplace, uint32_t room, uint2 *wp)
+void plan_waves(const std::vector<uint32_t> &nch, uint32_t tmaxit, uint32_t inplace, uint32_t room, uint2 *wp,
+                uint32_t nw = 16)
 {
     const uint32_t ncol = (uint32_t)nch.size();
-    if (ncol <= 16) {
+    if (ncol <= nw) {
         // waves per tile: one each, the rest to the tile whose slices
         // are longest (each slice at least two chunks; the parked
         // partials -- every slice past the first `inplace` of a tile --
         // within the buffer's rows past the year's tiles)
         std::vector<uint32_t> w(ncol, 1);
         uint32_t parked = 0;
-        for (uint32_t spare = 16 - ncol; spare; --spare) {
+        for (uint32_t spare = nw - ncol; spare; --spare) {
             uint32_t best = ncol;
             for (uint32_t i = 0; i < ncol; ++i)
                 if (nch[i] / (w[i] + 1) >= 2 && (w[i] + 1 <= inplace || parked < room) &&
@@ -3004,7 +3006,7 @@ void plan_waves(const std::vector<uint32_t> &nch, uint32_t tmaxit, uint32_t inpl
             if (++w[best] > inplace) ++parked;
         }
         const uint32_t split = *std::max_element(w.begin(), w.end()) > 1 ? 1u : 0u;
-        for (uint32_t wv = 0; wv < 16; ++wv)
+        for (uint32_t wv = 0; wv < nw; ++wv)
             for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, split << 22);
         uint32_t wv = 0, pbase = 0;
         for (uint32_t tile = 0; tile < ncol; ++tile) {
@@ -3016,16 +3018,16 @@ void plan_waves(const std::vector<uint32_t> &nch, uint32_t tmaxit, uint32_t inpl
             pbase += w[tile] > inplace ? w[tile] - inplace : 0;
         }
     } else {
-        std::vector<uint32_t> order(ncol), cnt(16, 0);
-        std::vector<uint64_t> load(16, 0);
+        std::vector<uint32_t> order(ncol), cnt(nw, 0);
+        std::vector<uint64_t> load(nw, 0);
         for (uint32_t i = 0; i < ncol; ++i) order[i] = i;
         std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return nch[x] > nch[y]; });
-        for (uint32_t wv = 0; wv < 16; ++wv)
+        for (uint32_t wv = 0; wv < nw; ++wv)
             for (uint32_t i = 0; i < tmaxit; ++i) wp[wv * tmaxit + i] = make_uint2(0u, 0u);
         for (uint32_t tile : order) {
-            uint32_t best = 16;
-            for (uint32_t wv = 0; wv < 16; ++wv)
-                if (cnt[wv] < tmaxit && (best == 16 || load[wv] < load[best])) best = wv;
+            uint32_t best = nw;
+            for (uint32_t wv = 0; wv < nw; ++wv)
+                if (cnt[wv] < tmaxit && (best == nw || load[wv] < load[best])) best = wv;
             wp[best * tmaxit + cnt[best]++] = make_uint2(nch[tile] << 16, tile | 1u << 12 | 1u << 24);
             load[best] += nch[tile];
         }
@@ -3112,9 +3114,9 @@ size_t hs_lds(const mdp_engine *eng)
 
 const void *hs_kernel(const mdp_engine *eng)
 {
-    if (eng->hs_nb == 8) return (const void *)k_fwd_hs<4, 8>;
-    if (eng->hs_nb == 9) return (const void *)k_fwd_hs<2, 9>;
-    return (const void *)k_fwd_hs<1, 10>;
+    if (eng->hs_nb == 8) return eng->hs_nw == 8 ? (const void *)k_fwd_hs<2, 8, 8> : (const void *)k_fwd_hs<4, 8, 16>;
+    if (eng->hs_nb == 9) return (const void *)k_fwd_hs<2, 9, 16>;
+    return (const void *)k_fwd_hs<1, 10, 16>;
 }
 
 // k_fwd_hs's tables (c-independent; nvar <= 10, years of at most 1 024
@@ -3139,8 +3141,15 @@ void build_hs_plan(mdp_engine *eng)
 {
     eng->hs = false;
     if (eng->nvar > 10 || eng->tmax < 2 || eng->npmax > 1024 || eng->ystate.size() < eng->tmax) return;
-    const uint32_t nb = std::max<uint32_t>(8u, eng->nvar), rt = nb == 8 ? 4u : nb == 9 ? 2u : 1u, pts = mmt_pts(rt);
-    const uint32_t tmaxit = nb == 10 ? 4u : nb == 9 ? 2u : 1u, cw = 4 * mmt_u(rt), ncube = 1u << nb;
+    const uint32_t nb = std::max<uint32_t>(8u, eng->nvar);
+    // waves a block (MDP_HS_WAVES): 8 for 8 variable patches (32 points, a
+    // 64 KiB cube: two blocks a CU, whose phases overlap; measured 5 % faster
+    // on the 256-state series, equal on the 128-state one, profiles/r06/hs),
+    // else 16
+    uint32_t nw = nb == 8 ? 8u : 16u;
+    if (const char *wv = eng->opts.get("MDP_HS_WAVES")) nw = atoi(wv) == 8 && nb == 8 ? 8u : 16u;
+    const uint32_t rt = nb == 8 ? (nw == 8 ? 2u : 4u) : nb == 9 ? 2u : 1u, pts = mmt_pts(rt);
+    const uint32_t ncube = 1u << nb, tmaxit = ncube / 16 > nw ? ncube / 16 / nw : 1u, cw = 4 * mmt_u(rt);
     const uint32_t zero = eng->nitems;  // the Pg row's zero slot
     if ((uint64_t)zero * 8u >= 0xffffffffull) return;
     // patches per v Pe pass (MDP_HS_RADIX, 1 .. kHsRadix; default 4, the
@@ -3160,8 +3169,8 @@ void build_hs_plan(mdp_engine *eng)
     eng->hs_pass.clear();
     eng->hs_ppos.clear();
     eng->hs_dpos.clear();
-    std::vector<uint2> ktile(kMmtMaxTiles), wtmp(16 * tmaxit);
-    eng->hs_wplan.assign((size_t)(eng->tmax + 1) * 16 * tmaxit, make_uint4(0u, 0u, 0u, 1u));
+    std::vector<uint2> ktile(kMmtMaxTiles), wtmp(nw * tmaxit);
+    eng->hs_wplan.assign((size_t)(eng->tmax + 1) * nw * tmaxit, make_uint4(0u, 0u, 0u, 1u));
     eng->hs_pk.assign((size_t)(eng->tmax + 1) * 16, 0u);
     eng->hs_pbase.assign(eng->tmax + 1, 0u);
     eng->hs_dbase.assign(eng->tmax + 1, 0u);
@@ -3376,10 +3385,10 @@ void build_hs_plan(mdp_engine *eng)
         uint32_t room = 0;
         for (uint32_t b = 0; b < ncube / 16 && room < 16; ++b)
             if (!used[b]) eng->hs_pk[(size_t)t * 16 + room++] = b * 16;
-        plan_waves(nch, tmaxit, 1u, room, wtmp.data());
-        for (uint32_t i = 0; i < 16 * tmaxit; ++i) {
+        plan_waves(nch, tmaxit, 1u, room, wtmp.data(), nw);
+        for (uint32_t i = 0; i < nw * tmaxit; ++i) {
             const uint2 kt2 = ktile[wtmp[i].y & 0xffu];
-            eng->hs_wplan[(size_t)t * 16 * tmaxit + i] =
+            eng->hs_wplan[(size_t)t * nw * tmaxit + i] =
                 (wtmp[i].y >> 24) ? make_uint4(wtmp[i].x, wtmp[i].y, kt2.x, kt2.y) : make_uint4(wtmp[i].x, wtmp[i].y, 0u, 1u);
         }
     }
@@ -3403,6 +3412,7 @@ void build_hs_plan(mdp_engine *eng)
     eng->hs_flops_pt = fb + fm + (double)eng->np[eng->tmax - 1];
     eng->hs_rt = rt;
     eng->hs_nb = nb;
+    eng->hs_nw = nw;
     if (const char *pv = eng->opts.get("MDP_HS_PROBE")) eng->hs_probe = (uint32_t)atoi(pv) & 7u;
     eng->hs = hs_lds(eng) <= device_lds_max() && eng->hs_kt.size() < (1u << 26);
 }
@@ -4325,13 +4335,14 @@ int launch_wide(const mdp_engine *eng, const DevCtx &d, int k, double *out, OutS
                 const uint64_t nbk = (uint64_t)npb * n;
                 if (nbk > 0x7fffffffull) return mdp_set_error(MDP_EUNSUPPORTED, "grid of %llu k_fwd_hs workgroups", (unsigned long long)nbk);
                 note_launch(eng, "k_fwd_hs<%u,%u>", rt, nb);
-#define MDP_HS(RT, NB) \
-    hipLaunchKernelGGL((k_fwd_hs<RT, NB>), dim3((uint32_t)nbk), dim3(kMmaThreads), hs_lds(eng), s, d.Pg, ldp, c0, d.np_d, \
+#define MDP_HS(RT, NB, NW) \
+    hipLaunchKernelGGL((k_fwd_hs<RT, NB, NW>), dim3((uint32_t)nbk), dim3(NW * 64), hs_lds(eng), s, d.Pg, ldp, c0, d.np_d, \
                        d.hs_kt, d.hs_cidx, d.hs_wplan, d.hs_pass, d.hs_pbase, d.hs_ppos, d.hs_dpos, \
                        d.hs_dbase, d.hs_dpk, d.hs_pk, eng->tmax, eng->prior0, d.e, d.ne, out, os.se, os.sc, eng->hs_probe)
-                if (nb == 8) MDP_HS(4, 8);
-                else if (nb == 9) MDP_HS(2, 9);
-                else MDP_HS(1, 10);
+                if (nb == 8 && eng->hs_nw == 8) MDP_HS(2, 8, 8);
+                else if (nb == 8) MDP_HS(4, 8, 16);
+                else if (nb == 9) MDP_HS(2, 9, 16);
+                else MDP_HS(1, 10, 16);
 #undef MDP_HS
             }
         }

@@ -590,12 +590,14 @@ std::string mdp_jit_forward_source(MdpJitPlan &pl)
              // per Q entry its item count and first QUN item indices
              "    constexpr int KPC = (FC * NITEMS + NT - 1) / NT;\n"
              "    constexpr int KQ = (FC * LDQ + NT - 1) / NT;\n"
-             // item w of pass k: odd passes run from the last thread down, so
-             // the partial last pass lands on the waves without Z rows; a wave
+             // item w of pass k: even passes run from the last thread down, so
+             // a single pass (config 2: 588 items on 1 024 threads) lands on
+             // the waves without Z rows, which then run beside them (round 6:
+             // kernel 8.27 -> 8.16 us in the A/B, profiles/r06/cfg2); a wave
              // with no item in a pass skips it (exec-empty branch)
              "    double Fp[KPC];\n"
              "    u32 zi[KPC];\n"
-             "#define ITEM_W(k) ((k) * NT + (((k) & 1) ? NT - 1 - threadIdx.x : threadIdx.x))\n"
+             "#define ITEM_W(k) ((k) * NT + (((k) & 1) ? threadIdx.x : NT - 1 - threadIdx.x))\n"
              "#define ZW(k) ((k) * NT + threadIdx.x)\n#define QW(k) ((k) * NT + threadIdx.x)\n"
 "#pragma unroll\n"
              "    for (int k = 0; k < KPC; ++k) {\n"

@@ -31,6 +31,7 @@ PATHS = {  # path name -> engine knobs
     "mma5": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "1"},
     "hs": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "3"},
     "mmt": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "2"},
+    "hs8": {"MDP_WIDE": "1", "MDP_WIDE_MMA": "3", "MDP_HS_WAVES": "8"},
     "epl2": {"MDP_VLDS_EPL": "2"},
 }
 # (pmiss, years, grid, path, variable patches): the config-2 generator with

@@ -62,6 +62,8 @@ VARIANTS = [
     ("MDP_WIDE=1;MDP_WIDE_MMA=3;MDP_HS_RADIX=1", "wide45"),
     ("MDP_WIDE=1;MDP_WIDE_MMA=3;MDP_HS_RADIX=2", "wide45"),
     ("MDP_WIDE=1;MDP_WIDE_MMA=3;MDP_HS_RADIX=4", "wide45"),
+    ("MDP_WIDE=1;MDP_WIDE_MMA=3;MDP_HS_WAVES=8", "wide45"),
+    ("MDP_WIDE=1;MDP_WIDE_MMA=3;MDP_HS_WAVES=16", "wide45"),
 ]
 # options that select no kernel: compile-time diagnostics and host threads
 TOOLING = ["MDP_JIT_CHECK", "MDP_JIT_DUMP", "MDP_JIT_THREADS", "MDP_JIT_VERBOSE"]

@@ -313,14 +313,15 @@ def launched_forward(model, path):
     """The wide forward kernel instantiation `path` runs for this model."""
     npm = int(model.npstates.max())
     nvar = len(model.var_cols)
+    rt8 = 4 if os.environ.get("MDP_HS_WAVES") == "16" else 2  # (8 waves a block by default: 32 points)
     if path == "wide-hs" and nvar <= 10 and len(model.npstates) > 1:
         nb = max(8, nvar)
-        return f"k_fwd_hs<{ {8: 4, 9: 2, 10: 1}[nb]},{nb}>"
+        return f"k_fwd_hs<{ {8: rt8, 9: 2, 10: 1}[nb]},{nb}>"
     if path == "wide-mma5" and npm <= 256:
         return f"k_fwd_mma<{64 if npm <= 64 else 128 if npm <= 128 else 256}>"
     if path in ("default", "wide") and npm > 64 and nvar <= 10 and len(model.npstates) > 1:
         nb = max(8, nvar)
-        return f"k_fwd_hs<{ {8: 4, 9: 2, 10: 1}[nb]},{nb}>"
+        return f"k_fwd_hs<{ {8: rt8, 9: 2, 10: 1}[nb]},{nb}>"
     if path in ("default", "wide", "wide-hs", "wide-mmt") and npm <= 1024:
         return f"k_fwd_mmt<{'4,128,2buf' if npm <= 128 else '2,256,1buf' if npm <= 256 else '2,512,1buf' if npm <= 512 else '1,1024,1buf'}>"
     return "k_fwd_wide"
