@@ -686,6 +686,32 @@ def test_cli_flags_match_oracle_cli(golden, tmp_path, fname, flags):
     assert_posterior_close(got, ref)
 
 
+@pytest.mark.parametrize("pmiss,nvar,T,s", [(0.6, 8, 50, 9), (0.6, 10, 30, 5)], ids=["128states", "1024states"])
+def test_cli_wide_series_match_oracle_cli(tmp_path, pmiss, nvar, T, s):
+    """The drop-in CLI on survey series whose years reach 128 and 1 024
+    states (the wide path, `k_fwd_hs` by default) against the oracle's CLI
+    with the same command line: same 'Total log-likelihood=' line and file
+    layout, posteriors within the parity bar."""
+    f = synth.write(tmp_path / "wide.txt", **dict(synth.CONFIG2, pmiss=pmiss, seed=5, T=T, nvar=nvar))
+    out, ref_out = tmp_path / "post.txt", tmp_path / "ref.txt"
+    flags = ["-s", str(s), "-m", "400", "-d", "100"]
+    r = subprocess.run([str(_lib.CLI_PATH), *flags, "-i", str(f), "-o", str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    orc = subprocess.run([str(oracle.CLI), *flags, "-i", str(f), "-o", str(ref_out)],
+                         capture_output=True, text=True, timeout=120)
+    assert orc.returncode == 0, orc.stderr
+    total = [ln for ln in r.stdout.splitlines() if ln.startswith("Total log-likelihood=")]
+    assert total == [ln for ln in orc.stdout.splitlines() if ln.startswith("Total log-likelihood=")]
+    got_txt, ref_txt = out.read_text(), ref_out.read_text()
+    assert [ln.count("\t") for ln in got_txt.split("\n")] == [ln.count("\t") for ln in ref_txt.split("\n")]
+    got_cells, ref_cells = got_txt.split(), ref_txt.split()
+    assert [x == "-nan" for x in got_cells] == [x == "-nan" for x in ref_cells]
+    got = np.array([float(x) for x in got_cells]).reshape(s, s)
+    ref = np.array([float(x) for x in ref_cells]).reshape(s, s)
+    assert_posterior_close(got, ref)
+
+
 def test_cli_all_nan_file(tmp_path):
     inp = tmp_path / "q5.txt"
     inp.write_text("0 1 1 1\n0 0 0 0\n0 1 0 1\n")
