@@ -144,7 +144,8 @@ def test_q5_impossible_transition(tmp_path):
 # ---------------------------------------------------------------------------
 # fuzzing: random problems covering every forward-kernel variant
 # ---------------------------------------------------------------------------
-@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic", "wide", "wide-chunked", "wide-plain"])
+@pytest.fixture(params=["direct", "direct-qrows", "direct-plain", "generic", "wide", "wide-chunked", "wide-plain", "wide-hs",
+                        "wide-hs-chunked"])
 def engine_path(request, monkeypatch):
     """Every engine path: the direct one (the hipRTC-specialised forward
     kernel; on these small grids it computes its column's Q itself), the same
@@ -152,7 +153,8 @@ def engine_path(request, monkeypatch):
     transition cache and XCD ordering off (MDP_JIT_SLOTS=0, MDP_JIT_XCD=0), and
     the generic kernels (MDP_JIT=0), and the wide path that years with more
     than 16 states need (MDP_WIDE=1: its forward on the matrix cores,
-    k_fwd_mma; chunked: one c value per item launch; plain: k_fwd_wide)."""
+    k_fwd_mmt; chunked: one c value per item launch; plain: k_fwd_wide; hs:
+    k_fwd_hs through the hidden states, whole and one c value per launch)."""
     for k in ("MDP_JIT", "MDP_JIT_SLOTS", "MDP_JIT_XCD", "MDP_FUSED", "MDP_WIDE", "MDP_WIDE_CB", "MDP_WIDE_MMA"):
         monkeypatch.delenv(k, raising=False)
     if request.param.startswith("wide"):
@@ -161,6 +163,10 @@ def engine_path(request, monkeypatch):
             monkeypatch.setenv("MDP_WIDE_CB", "1")
         if request.param == "wide-plain":
             monkeypatch.setenv("MDP_WIDE_MMA", "0")
+        if request.param.startswith("wide-hs"):
+            monkeypatch.setenv("MDP_WIDE_MMA", "3")
+        if request.param == "wide-hs-chunked":
+            monkeypatch.setenv("MDP_WIDE_CB", "1")
     elif request.param == "generic":
         monkeypatch.setenv("MDP_JIT", "0")
     elif request.param == "direct-qrows":
