@@ -27,8 +27,8 @@ def _problem(model):
     return n, nvar, off, yid, model.short_state, M, varc, float(model.prior[0])
 
 
-def _q_table(model, c):
-    """Q_ab[m](c) of every consecutive-year pair: Pc[j][B] summed over j <= A&B, |j| = m."""
+def _pc_fn(model, c):
+    """Pc[j][B](c) of the reference (main_MIDASPOM.c:18-50), memoised per j."""
     n, nvar, off, yid, ss, M, varc, _ = _problem(model)
     isvar = np.zeros(n, bool)
     isvar[varc] = True
@@ -57,6 +57,14 @@ def _q_table(model, c):
                 f *= 1.0 - p[k]
         return f
 
+    return pc
+
+
+def _q_table(model, c):
+    """Q_ab[m](c) of every consecutive-year pair: Pc[j][B] summed over j <= A&B, |j| = m."""
+    n, nvar, off, yid, ss, M, varc, _ = _problem(model)
+    pc = _pc_fn(model, c)
+    Q = {}
     for t in range(1, len(off) - 1):
         for a_ in yid[off[t - 1]:off[t]]:
             for b_ in yid[off[t]:off[t + 1]]:
@@ -185,3 +193,63 @@ def test_gemm_form_matches_direct(golden, fname):
                 assert abs(g - ref) <= 1e-11 * max(1.0, abs(ref)), (e, c, g, ref)
             else:
                 assert not np.isfinite(g), (e, c, g, ref)
+
+
+def _forward_hs(model, c, e):
+    """The hidden-state form of k_fwd_hs (csrc/spom_engine.hip, DESIGN.md
+    §4.5): per year U[j] = y^|j| sum_{A >= j} v[A] x^(|A| - |j|) by one
+    butterfly pass per patch of W (V[j] += x V[j | b], y^|j| applied once at
+    the end), then n[l] = sum_{j <= B_l, j in D} Pc[j][B_l] U[j]."""
+    n, nvar, off, yid, ss, M, varc, prior = _problem(model)
+    pc = _pc_fn(model, c)
+    x = min(e, 1.0)
+    y = 1.0 - x
+    v = {int(ss[k]): 1.0 for k in yid[off[0]:off[1]]}
+    for t in range(1, len(off) - 1):
+        W = 0
+        for A in v:
+            W |= A
+        U = dict(v)
+        for b in range(nvar):
+            bit = 1 << b
+            if not W & bit:
+                continue
+            for a1 in [a for a in U if a & bit]:
+                U[a1 ^ bit] = U.get(a1 ^ bit, 0.0) + x * U[a1]
+        U = {j: u * y ** bin(j).count("1") for j, u in U.items()}
+        nv = {}
+        for bl in yid[off[t]:off[t + 1]]:
+            B = int(ss[bl])
+            key, acc, j = B & W, 0.0, B & W
+            while True:
+                if j in U:
+                    acc += pc(j, B) * U[j]
+                if j == 0:
+                    break
+                j = (j - 1) & key
+            nv[B] = acc
+        v = nv
+    L = sum(v.values()) * prior
+    return np.log(L) if L > 0 else -np.inf
+
+
+@pytest.mark.parametrize("fname", ["manual_p3_obs.txt", "occupancies.txt", "config2_64x50.txt", "wide45"])
+def test_hidden_state_form_matches_direct(golden, tmp_path, fname):
+    """k_fwd_hs's factorisation (v Pe by butterflies over the hidden states,
+    then U Pc) against the direct per-transition sum, on the shipped inputs
+    and on a survey-like series with years of up to 64 states."""
+    from midaspom_amd import synth
+    if fname == "wide45":
+        f = synth.write(tmp_path / "w.txt", **dict(synth.CONFIG2, pmiss=0.45, seed=5, T=6))
+    else:
+        f = golden / fname
+    model = mdp.Model.load(f, m=400, d=100)
+    for c in (0.1, 0.52):
+        Q = _q_table(model, c)
+        for e in (0.0, 0.2, 0.5, 0.8, 1.0, 1.3):
+            ref = _forward(model, Q, e, False)
+            got = _forward_hs(model, c, e)
+            if np.isfinite(ref):
+                assert abs(got - ref) <= 1e-11 * max(1.0, abs(ref)), (e, c, got, ref)
+            else:
+                assert not np.isfinite(got), (e, c, got, ref)
