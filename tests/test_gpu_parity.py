@@ -377,6 +377,29 @@ def test_random_wide_problems(seed, monkeypatch):
         assert_loglik_close(got, ref)
 
 
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MDP_FUZZ_HS", "6"))))  # more: a longer fuzz
+def test_random_hidden_state_problems(seed, monkeypatch):
+    """Random 10-patch problems with 5-9 unvisited patches in random years
+    (32-512 states, consecutive big years included) and random dispersal /
+    grid bounds, on k_fwd_hs (8-, 9- and 10-variable cubes; whole and one c
+    value per launch) against the oracle."""
+    rng = np.random.default_rng(9100 + seed)
+    T = int(rng.integers(3, 7))
+    years = rng.choice(T, size=int(rng.integers(1, min(T, 3) + 1)), replace=False)
+    missing = {int(y): int(rng.integers(5, 10)) for y in years}
+    obs = _wide_obs(rng, 10, T, missing)
+    m, d, p = float(rng.choice([100, 400])), float(rng.choice([50, 100, 200])), float(rng.choice([0.5, 0.3]))
+    model = mdp.Model.from_obs(obs, m=m, p=p, d=d)
+    e, _ = mdp.grid(int(rng.integers(2, 5)), 0.0, float(rng.choice([1.0, 1.2])))
+    c, _ = mdp.grid(int(rng.integers(2, 5)), 0.0, float(rng.choice([1.0, 1.5])))
+    ref = oracle.OracleModel.from_obs(obs, m, p, d).loglik_grid(e, c, threads=16)
+    for cb in (None, "1"):
+        if cb:
+            monkeypatch.setenv("MDP_WIDE_CB", cb)
+        got = _wide_engine_run(model, e, c, "wide-hs", monkeypatch)
+        assert_loglik_close(got, ref)
+
+
 def _big_obs(rng, missing, full=()):
     """10 patches x 6 years (2^10 hidden states): `missing` = {year: k}
     unvisited patches among patches 1-9 (2^k states), and every patch
