@@ -1758,36 +1758,40 @@ __global__ __launch_bounds__(kMmaThreads) void k_fwd_mmt(
     }
 }
 
-// k_fwd_hs<RT, NB> (round 6): the wide forward through the hidden states.
-// The reference's own factorisation (main_MIDASPOM.c:18-50, :363, :371-384):
-// P = Pe Pc over the hidden states j, so year t is
-//     U[p][j] = sum_{k: A_k >= j} v[p][k] x^(|A_k| - |j|) y^|j|     (v Pe)
+// k_fwd_hs<RT, NB, NW> (round 6): the wide forward through the hidden
+// states.  The reference's own factorisation (main_MIDASPOM.c:18-50, :363,
+// :371-384): P = Pe Pc over the hidden states j, so year t is
+//     U[p][j] = y^|j| sum_{k: A_k >= j} v[p][k] x^(|A_k| - |j|)    (v Pe)
 //     n[p][l] = sum_{j <= B_l} Pc[j][B_l] U[p][j]                  (U Pc)
 // instead of one (nX+1)-term polynomial per transition (k, l): for a year of
 // 2^f completions of f unvisited patches that is ~3^f (j, l) terms per
 // point, not ~2^f 2^f (|A|+1) -- 10-25x fewer for years of 256-1 024 states.
-// The block's points keep one vector over the whole 2^NB cube of hidden
-// states in LDS, V[j][p] (NB = nvar <= 10; 2^NB x 16 RT doubles = 128 KiB):
+// An NW-wave block's 16 RT points keep one vector over the whole 2^NB cube
+// of hidden states in LDS, V[j][p] (NB = max(8, nvar) <= 10; 64 or 128 KiB),
+// plus a y^k table:
 //  * v Pe: Pe is a tensor product over the patches (per patch: occupied ->
-//    extinct w.p. x, survives w.p. y), applied in place as one butterfly pass
-//    per patch of W = the bits occupied in some state of year t - 1: first
-//    the patches unobserved that year (F; every pair of positions is a
-//    state), then the always-occupied ones (O), each writing its "extinct"
-//    half by assignment (those positions held no state: no zeroing needed).
-//    Position lists per pass come from the host (pass tables);
+//    extinct w.p. x, survives w.p. y), applied in place by passes of up to
+//    kHsRadix patches of W = the bits occupied in some state of year t - 1:
+//    a thread loads a coset's positions, runs the butterflies V[j] +=
+//    x V[j | b] in registers and writes back, y^|j| applied in the year's
+//    last pass.  The host's pass tables (build_hs_plan) name per coset the
+//    positions to read and to write -- only those whose value still reaches
+//    a hidden state the year's products read -- and give a wave's cosets the
+//    same masks, so uniform branches skip the rest;
 //  * U Pc: the per-year GEMM on the matrix cores as k_fwd_mmt's, with K = the
-//    hidden states j a column tile of new states can reach (subsets of the
-//    tile's union within W), the W operand U[j][p] read straight from the
-//    cube, and the C operand Pc[j][B_l] gathered from the column's item
-//    factors (k_witems' Pg rows, ld = nitems + 1: a zero slot at nitems for
-//    j not <= B_l) through a host table of offsets;
+//    hidden states j a column tile of new states reaches, the W operand
+//    U[j][p] read straight from the cube, and the C operand Pc[j][B_l]
+//    gathered from the column's item factors (k_witems' Pg rows, ld =
+//    nitems + 1: a zero slot at nitems for j not <= B_l) through a host
+//    table of offsets;
 //  * the year's new states are stored at their own cube positions B_l (after
-//    a barrier: U is dead by then), ready for the next year's butterflies.
-// Tiles per wave as k_fwd_mmt (longest lists first past 16 tiles; smaller
-// years give a tile up to two waves, slice 1 parked in the tile's own
-// destination rows).  Q3 semantics: ones at year 0's states; L = prior0 x
-// the sum over the last year's states.  Sums reordered against the
-// reference's (positive terms for e in [0, 1]: ~1e-15 relative).
+//    a barrier: U is dead by then), ready for the next year's passes.
+// Tiles are dealt to waves as k_fwd_mmt's (longest lists first past NW
+// tiles; smaller years give the spare waves slices of the longest lists,
+// parked in 16-row cube blocks that hold none of the year's states).  Q3
+// semantics: ones at year 0's states; L = prior0 x the sum over the last
+// year's states.  Sums reordered against the reference's (positive terms
+// for e in [0, 1]: ~1e-15 relative).
 constexpr uint32_t kHsRadix = 4;  // k_fwd_hs: patches per v Pe pass (at most; the plan's default)
 constexpr uint32_t kHsPre = 4;    // k_fwd_hs: v Pe passes a year whose descriptors are loaded up front
 // diag build, MDP_HS_PROBE bit 2: workgroup 0's wave 0 stamps the shader
